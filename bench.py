@@ -1,0 +1,226 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s + ms/frame of the trace path on BASELINE.json config C2.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    (N > 1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N)
+
+A step is one frame of the reference's render loop (src/Global/Renderer.cu:264-317): the
+instance update callback (Main.cu updateInstance, native), the host TLAS rebuild + upload,
+and the trace kernel over the frame — for N > 1 each rank traces its interleaved 64x64
+screen tiles, the tile slabs are gathered to rank 0 over RCCL (torch.distributed "nccl") and
+assembled into the frame on rank 0.  Scene, BVHs and framebuffer stay in HBM; nothing is
+copied to the host inside the timed region.
+
+Rank 0 prints one JSON line (see DESIGN.md §4 for every field's definition).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "real-time-gpu-ray-tracer_amd"))
+
+METRIC = "Mrays/sec + ms/frame, 1920×1080 1spp primary+shadow, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+TILE = 64
+
+# algorithmic bytes per work item
+B_PAIR, B_TRI, B_SPH, B_QUAD, B_INST, B_HIT, B_PIXEL = 64, 48, 16, 80, 80, 208, 4
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--config", default="C2")
+    p.add_argument("--exact", action="store_true", help="time the EXACT (parity) kernel instead of FAST")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-seconds", type=float, default=12.0)
+    return p.parse_args()
+
+
+def algorithmic_bytes(st):
+    spheres = st["sphere_quad_tests"] - st["quad_tests"]
+    return (B_PAIR * st["aabb_tests"] / 2 + B_TRI * st["triangle_tests"] + B_SPH * spheres +
+            B_QUAD * st["quad_tests"] + B_INST * st["instance_visits"] + B_HIT * st["hits"] +
+            B_PIXEL * st["pixels"])
+
+
+def cpu_baseline(scene, cfg, budget_s):
+    """The oracle ("port") on the host cores: whole C2 frames, repeated until ~budget_s."""
+    from oracle.oracle import OracleScene
+    threads = max(1, min(16, os.cpu_count() or 1))
+    o = OracleScene(scene, build_seed=0)
+    o.camera(cfg.width, cfg.height)
+    rays = 0
+    frames = 0
+    t0 = time.perf_counter()
+    while True:
+        o.update(frames)
+        _, _, cnt = o.render(threads=threads, want_rgb=False, want_rgba=True)
+        rays += cnt["rays"]
+        frames += 1
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(rays / dt / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/rt_oracle.c, {frames} full {cfg.width}x{cfg.height} C2 frames "
+                      f"(frames 0..{frames - 1}), {threads} threads, {dt:.1f} s, {rays} rays",
+            "ms_per_frame": round(dt * 1e3 / frames, 2)}
+
+
+def load_traffic(kernel_prefix):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this bench command."""
+    path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        if d.get("kernel", "").startswith(kernel_prefix):
+            return d.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
+    n = max(1, world)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from rtamd import Renderer, scenes
+
+    torch.cuda.set_device(local_rank)
+    if n > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    cfg = scenes.CONFIGS[args.config]
+    scene = scenes.config_scene(cfg)
+    r = Renderer(scene, device=local_rank).build_acceleration_structure(0).configure_camera(cfg.width, cfg.height)
+    info = r.info()
+    stream = torch.cuda.current_stream().cuda_stream
+
+    tiles = None
+    if n > 1:
+        tiles = (TILE, TILE, rank, n)
+        slab_tiles = max(r.tiles_for_rank(TILE, TILE, k, n) for k in range(n))
+        slab_px = slab_tiles * TILE * TILE
+        slab = torch.zeros(slab_px * 4, dtype=torch.uint8, device="cuda")
+        gathered = torch.zeros(n * slab_px * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
+        frame_buf = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
+    else:
+        frame_buf = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda")
+
+    def step(frame):
+        if n == 1:
+            _, _, st = r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=frame_buf.data_ptr(),
+                                stream=stream)
+            return st
+        _, _, st = r.render(frame, exact=args.exact, want_rgba=False, tiles=tiles, rgba8_device=slab.data_ptr(),
+                            stream=stream)
+        dist.gather(slab, list(gathered.chunk(n)) if rank == 0 else None, dst=0)
+        if rank == 0:
+            r.assemble_tiles(gathered.data_ptr(), slab_tiles, TILE, TILE, n, frame_buf.data_ptr(), stream)
+        return st
+
+    for f in range(args.warmup):
+        step(f)
+    torch.cuda.synchronize()
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    rays = 0
+    kernel_ms = []
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        st = step(args.warmup + k)
+        rays += int(st["rays"])
+        kernel_ms.append(st["kernel_ms"])
+    torch.cuda.synchronize()
+    if n > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    # max over ranks of the elapsed time; total rays over ranks
+    if n > 1:
+        t = torch.tensor([elapsed, float(rays)], dtype=torch.float64, device="cuda")
+        tmax = t.clone()
+        dist.all_reduce(tmax[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        elapsed, rays = float(tmax[0]), int(t[1])
+
+    # untimed work-counting pass (same frame as the first timed step) for the roofline
+    _, _, cst = r.render(args.warmup, exact=args.exact, want_rgba=False, count_work=True,
+                         rgba8_device=(slab if n > 1 else frame_buf).data_ptr(), tiles=tiles, stream=stream)
+    if n > 1:
+        dist.barrier()
+
+    if rank == 0:
+        avg_kernel_ms = float(np.mean(kernel_ms))
+        bytes_launch = algorithmic_bytes(cst)
+        achieved = bytes_launch / (avg_kernel_ms * 1e-3) / 1e9
+        kname = "render_kernel" + ("_exact" if args.exact else "")
+        traffic = load_traffic("rtamd::dev_exact::render_kernel" if args.exact else "rtamd::dev_fast::render_kernel")
+        value = rays / elapsed / 1e6
+        out = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": n,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": f"{cfg.name}: {cfg.description}",
+                "width": cfg.width, "height": cfg.height, "spp": cfg.spp, "depth": cfg.depth,
+                "triangles": scene.triangle_count, "instances": len(scene.instances),
+                "blas_node_pairs": info["blas_node_pairs"],
+                "parallelism": f"screen-tiles{n} ({TILE}x{TILE} interleaved, RCCL gather)" if n > 1 else "single-gpu",
+                "kernel": "EXACT" if args.exact else "FAST",
+            },
+            "rays_per_frame": round(rays / args.steps, 1),
+            "kernel_ms": round(avg_kernel_ms, 4),
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "kernel": kname,
+                "algorithmic_bytes_per_launch": int(bytes_launch),
+                "work_per_launch": {k: int(cst[k]) for k in ("rays", "pixels", "aabb_tests", "triangle_tests",
+                                                             "sphere_quad_tests", "quad_tests", "instance_visits", "hits")},
+            },
+            "cpu_baseline": None,
+        }
+        if n == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(scene, cfg, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    if n > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    r.cleanup()
+
+
+if __name__ == "__main__":
+    main()

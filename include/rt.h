@@ -1,0 +1,301 @@
+/*
+ * rt.h — C ABI of the MI355X-native trace path (drop-in for the reference's
+ * Scene / Camera / render(framebuffer) lifecycle).
+ *
+ * The reference has no FFI; its boundary is the static C++ class `Renderer`
+ * (include/Global/Renderer.cuh:109-146) plus the kernel contract
+ * `render(const TraverseData*, cudaSurfaceObject_t)` with a `__constant__ Camera`
+ * (include/Global/RendererImpl.cuh:196-199).  Every entry point below names the
+ * reference call it replaces.  All types are plain C: no torch, no HIP types.
+ *
+ * Conventions
+ *  - Every call returns rt_status; on failure rt_last_error() returns a
+ *    thread-local message.  The library never exit()s (the reference exits with
+ *    -200 on any CUDA error, src/Global/Global.cu:34-41).
+ *  - A scene is not thread-safe; use one scene per host thread (the reference
+ *    drives everything from one thread, src/Global/Renderer.cu:180-366).
+ *  - Framebuffer layout matches the reference surface: row-major W x H RGBA8,
+ *    row 0 = bottom of the image (viewport origin bottom-left,
+ *    src/Global/RenderPin.cu:91-92).
+ */
+#ifndef RT_H
+#define RT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1u
+
+typedef enum rt_status {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARGUMENT = 1,
+    RT_ERR_DEVICE = 2,          /* HIP runtime error, or no GPU present        */
+    RT_ERR_OUT_OF_MEMORY = 3,
+    RT_ERR_STATE = 4,           /* call out of lifecycle order                 */
+    RT_ERR_UNSUPPORTED = 5
+} rt_status;
+
+/* include/Basic/BasicTypes.cuh:9-11 */
+typedef enum rt_primitive_type {
+    RT_PRIM_SPHERE = 0,
+    RT_PRIM_PARALLELOGRAM = 1,
+    RT_PRIM_TRIANGLE = 2
+} rt_primitive_type;
+
+/* include/Basic/BasicTypes.cuh:14-16 */
+typedef enum rt_material_type {
+    RT_MAT_ROUGH = 0,
+    RT_MAT_METAL = 1
+} rt_material_type;
+
+typedef struct rt_vec3 { float x, y, z; } rt_vec3;
+
+/* Sphere(MaterialType, size_t, Point3 center, float radius) — include/Geometry/Sphere.cuh:27 */
+typedef struct rt_sphere {
+    rt_vec3 center;
+    float radius;
+    uint32_t material_type;
+    uint32_t material_index;
+} rt_sphere;
+
+/* Parallelogram(MaterialType, size_t, q, u, v) — include/Geometry/Parallelogram.cuh:26-39 */
+typedef struct rt_parallelogram {
+    rt_vec3 q, u, v;
+    uint32_t material_type;
+    uint32_t material_index;
+} rt_parallelogram;
+
+/* Triangle(MaterialType, size_t, vertexes[, vertexNormals]) — include/Geometry/Triangle.cuh:26-46.
+ * has_normals = 0 selects the 3-vertex constructor (all three normals = unit(e1 x e2)). */
+typedef struct rt_triangle {
+    rt_vec3 vertex[3];
+    rt_vec3 normal[3];
+    uint32_t material_type;
+    uint32_t material_index;
+    uint32_t has_normals;
+    uint32_t reserved;
+} rt_triangle;
+
+/* Rough{albedo} — include/Material/Rough.cuh:11-12; Metal{albedo, fuzz} — include/Material/Metal.cuh:11-13 */
+typedef struct rt_rough { rt_vec3 albedo; } rt_rough;
+typedef struct rt_metal { rt_vec3 albedo; float fuzz; } rt_metal;
+
+/* Instance::updateTransformArguments(shift, rotate(degrees, x->y->z), scale)
+ * — src/AS/Instance.cu:4-17, src/Util/Matrix.cu:183-249. */
+typedef struct rt_xform {
+    rt_vec3 shift;
+    rt_vec3 rotate_deg;
+    rt_vec3 scale;
+} rt_xform;
+
+/* One entry of the reference instance map {PrimitiveType, primitiveIndex}
+ * (src/Global/Main.cu:93-99) plus the fields VTK instances carry
+ * (src/Global/VTKReader.cu:204-214).
+ *  primitive_count == 0 -> single-primitive instance; local bounds / centroid come
+ *    from the primitive (src/Global/RenderPin.cu:124-139).
+ *  primitive_count  > 0 -> a group of primitive_count primitives of one type starting at
+ *    primitive_index; has_local_bounds = 1 supplies the pre-transform bounds/centroid the
+ *    VTK reader would (bounds = [xmin,xmax,ymin,ymax,zmin,zmax]); has_local_bounds = 0
+ *    uses the union of the primitive boxes and the mean of primitive centroids (extension).
+ */
+typedef struct rt_instance_desc {
+    uint32_t primitive_type;
+    uint32_t primitive_index;
+    uint32_t primitive_count;
+    uint32_t has_local_bounds;
+    float local_bounds[6];
+    rt_vec3 local_centroid;
+    rt_xform xform;           /* initial transform (used when no update callback is set) */
+} rt_instance_desc;
+
+/* Per-frame instance update, replaces
+ * void (*updateInstances)(Instance*, size_t instanceCount, size_t frameCount)
+ * (include/Global/Renderer.cuh:94).  The callback rewrites the (shift, rotate, scale)
+ * triple of each instance; the library then recomputes matrices and bounds exactly like
+ * Instance::updateTransformArguments and rebuilds the TLAS (src/Global/Renderer.cu:269-276). */
+typedef void (*rt_update_fn)(void *user, rt_xform *xforms, size_t instance_count, uint64_t frame);
+
+/* GeometryData + MaterialData + instance map (include/Global/Renderer.cuh:33-43,
+ * src/Global/Renderer.cu:9-121).  The caller keeps ownership; the library copies. */
+typedef struct rt_scene_desc {
+    const rt_sphere *spheres;               size_t sphere_count;
+    const rt_parallelogram *parallelograms; size_t parallelogram_count;
+    const rt_triangle *triangles;           size_t triangle_count;
+    const rt_rough *roughs;                 size_t rough_count;
+    const rt_metal *metals;                 size_t metal_count;
+    const rt_instance_desc *instances;      size_t instance_count;
+    rt_update_fn update;
+    void *update_user;
+} rt_scene_desc;
+
+/* CameraInput — include/Global/Renderer.cuh:54-64 (field for field). */
+typedef struct rt_camera_input {
+    rt_vec3 background;
+    rt_vec3 center;
+    rt_vec3 target;
+    float fov;                 /* horizontal field of view, degrees */
+    rt_vec3 up;
+    float focus_disk_radius;
+    float sample_range;        /* carried, unused (as in the reference) */
+    uint32_t sample_count;     /* traced samples = floor(sqrt(n))^2 (RenderPin.cu:93) */
+    uint32_t ray_trace_depth;
+} rt_camera_input;
+
+/* BVH build policy.  COMPAT_MEDIAN restates BLAS::constructBLAS / TLAS::constructTLAS
+ * (src/AS/BLAS.cu:4-117, src/AS/TLAS.cu:4-129): top-down median split on a pseudo-random
+ * axis, leaf <= 4 primitives (BLAS) / <= 2 instances (TLAS).  The reference draws the axis
+ * from std::mt19937(random_device); here the axis stream is a pinned function of `seed`
+ * so builds are reproducible, and centroid ties are broken by primitive index. */
+typedef enum rt_build_mode {
+    RT_BUILD_COMPAT_MEDIAN = 0
+} rt_build_mode;
+
+typedef enum rt_render_flags {
+    RT_RENDER_EXACT = 1u << 0,        /* bit-faithful arithmetic (IEEE division, no FMA) */
+    RT_RENDER_COUNT_WORK = 1u << 1,   /* fill rt_stats work counters (slower)              */
+    RT_RENDER_NO_SYNC = 1u << 2,      /* return after enqueue (device outputs only)        */
+    RT_RENDER_SKIP_UPDATE = 1u << 3   /* do not run the instance update / TLAS rebuild     */
+} rt_render_flags;
+
+/* Per-call options for rt_render.  Zero-initialise, then set what you need. */
+typedef struct rt_render_opts {
+    uint64_t frame_seed;       /* replaces clock64() in curand_init (Kernel.cu:114); 0 -> 0x5EED */
+    uint32_t flags;            /* rt_render_flags */
+    /* Screen-tile sharding (multi-GPU): the frame is cut into tile_w x tile_h tiles in
+     * row-major tile order; this call renders tiles t with t % tile_count == tile_rank.
+     * tile_count == 0 renders the whole frame into the frame-layout outputs.
+     * With tile_count > 0, device outputs are written tile-compact: local tile k occupies
+     * pixels [k*tile_w*tile_h, (k+1)*tile_w*tile_h), row-major inside the tile. */
+    uint32_t tile_w, tile_h;
+    uint32_t tile_rank, tile_count;
+    /* Optional device outputs (hipMalloc'd / torch device memory on this scene's GPU). */
+    void *rgba8_device;        /* uchar4 per pixel */
+    void *rgb32_device;        /* 3 floats per pixel, linear average before gamma */
+    void *stream;              /* hipStream_t to enqueue on; NULL -> the scene's stream */
+} rt_render_opts;
+
+typedef struct rt_stats {
+    uint64_t rays;             /* closest-hit traversals (one per TLAS::hit call, Kernel.cu:68) */
+    uint64_t pixels;
+    uint64_t aabb_tests;       /* filled with RT_RENDER_COUNT_WORK */
+    uint64_t triangle_tests;
+    uint64_t sphere_quad_tests;  /* sphere + parallelogram tests                                */
+    uint64_t quad_tests;         /* parallelogram tests                                         */
+    uint64_t instance_visits;
+    uint64_t hits;               /* closest hits found (rays - misses)                          */
+    double kernel_ms;          /* device time of the trace kernel (HIP events)             */
+    double frame_ms;           /* host wall time of the call                               */
+    double update_ms;          /* host time of instance update + TLAS rebuild + upload     */
+} rt_stats;
+
+/* Closest-hit record for rt_trace_rays (per-ray parity tests). */
+typedef struct rt_hit {
+    float t;
+    uint32_t instance;         /* 0xFFFFFFFF = miss */
+    uint32_t primitive_type;
+    uint32_t primitive_index;  /* index into the caller's primitive array */
+    rt_vec3 point;             /* world-space hit point   (Instance.cu:41) */
+    rt_vec3 normal;            /* world-space unit normal (Instance.cu:44) */
+    uint32_t material_type;
+    uint32_t material_index;
+} rt_hit;
+
+typedef struct rt_scene rt_scene;
+
+/* --- lifecycle ---------------------------------------------------------------- */
+
+uint32_t rt_abi_version(void);
+const char *rt_last_error(void);
+/* Number of visible GPUs (0 when no HIP device is present). */
+int rt_device_count(void);
+
+/* Renderer::commitGeometryData + commitMaterialData + configureInstances
+ * (src/Global/Renderer.cu:9-121).  Copies the description; no device work yet. */
+rt_status rt_scene_create(const rt_scene_desc *desc, int device, rt_scene **out_scene);
+
+/* Renderer::buildAccelerationStructure (src/Global/Renderer.cu:123-155): builds every BLAS
+ * (deduplicated per (type, primitiveIndex), RenderPin.cu:99-201), uploads geometry, BVHs
+ * and materials to HBM, and builds the frame-0 TLAS. */
+rt_status rt_scene_build(rt_scene *scene, rt_build_mode mode, uint64_t seed);
+
+/* Renderer::configureCamera (src/Global/Renderer.cu:157-178) ->
+ * RendererImpl::calculateCameraProperties (src/Global/RenderPin.cu:73-95). */
+rt_status rt_camera_set(rt_scene *scene, const rt_camera_input *camera,
+                        uint32_t width, uint32_t height);
+
+/* Host half of one iteration of startRender (src/Global/Renderer.cu:264-303): run the
+ * instance update for `frame`, rebuild the TLAS and upload it (double-buffered). */
+rt_status rt_scene_update(rt_scene *scene, uint64_t frame);
+
+/* Device half of one iteration of startRender (src/Global/Renderer.cu:305-317) = the
+ * `render` kernel (src/Global/Kernel.cu:105-147).  Unless RT_RENDER_SKIP_UPDATE is set,
+ * first calls rt_scene_update(scene, frame).  Host outputs (may be NULL) receive the
+ * frame after completion; device outputs are described in rt_render_opts. */
+rt_status rt_render(rt_scene *scene, uint64_t frame, const rt_render_opts *opts,
+                    uint8_t *rgba8_host, float *rgb32_host, rt_stats *stats);
+
+/* Assemble tile-compact buffers gathered from `tile_count` ranks into a frame-layout RGBA8
+ * device buffer (the multi-GPU gather's scatter step).  `gathered` holds tile_count slabs of
+ * slab_tiles tiles each (rank r's slab = its tiles in render order, padded). */
+rt_status rt_assemble_tiles(rt_scene *scene, const void *gathered_device, uint32_t slab_tiles,
+                            uint32_t tile_w, uint32_t tile_h, uint32_t tile_count,
+                            void *frame_rgba8_device, void *stream);
+
+/* Number of tiles rank `tile_rank` owns for the current camera size. */
+uint32_t rt_tiles_for_rank(const rt_scene *scene, uint32_t tile_w, uint32_t tile_h,
+                           uint32_t tile_rank, uint32_t tile_count);
+
+/* Trace arbitrary world rays (origin xyz, direction xyz per ray) against the current TLAS
+ * with t in [0.001, inf) and return the closest hit (TLAS::hit, src/AS/TLAS.cu:131-201). */
+rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_count,
+                        uint32_t flags, rt_hit *hits_host);
+
+/* Blocks until all work the scene enqueued has finished. */
+rt_status rt_synchronize(rt_scene *scene);
+
+/* Renderer::cleanup (src/Global/Renderer.cu:368-391). */
+void rt_scene_destroy(rt_scene *scene);
+
+/* --- introspection (tests / tooling) -------------------------------------------- */
+
+typedef struct rt_scene_info {
+    uint64_t blas_count;
+    uint64_t blas_node_pairs;      /* interior nodes over all BLAS (= node-pair records) */
+    uint64_t blas_leaves;
+    uint64_t tlas_node_pairs;
+    uint64_t device_bytes;         /* HBM held by the scene */
+    uint32_t width, height;
+    uint32_t sqrt_sample_count;
+    uint32_t ray_trace_depth;
+} rt_scene_info;
+
+rt_status rt_scene_get_info(const rt_scene *scene, rt_scene_info *info);
+
+/* Export a BLAS in the reference's node form (BLASNode array + BLASIndex array,
+ * include/AS/BLAS.cuh:20-34) for tree-identity tests.  Pass NULL buffers to query sizes.
+ * nodes: 8 floats per node {xmin,xmax,ymin,ymax,zmin,zmax, count, index} (count/index as
+ * exact float-encoded integers < 2^24 are NOT assumed: use the uint32 arrays). */
+rt_status rt_scene_export_blas(const rt_scene *scene, uint32_t blas_index,
+                               float *node_boxes /* 6 per node */, uint32_t *node_count_index /* 2 per node */,
+                               uint32_t *prim_refs /* primitive index per slot */,
+                               uint32_t *n_nodes, uint32_t *n_prims);
+
+/* Export the current TLAS (include/AS/TLAS.cuh:24-39) in the same form; prim_refs receive
+ * instance indices. */
+rt_status rt_scene_export_tlas(const rt_scene *scene,
+                               float *node_boxes, uint32_t *node_count_index,
+                               uint32_t *instance_refs, uint32_t *n_nodes, uint32_t *n_refs);
+
+/* Built-in copy of the demo animation (src/Global/Main.cu:6-42 updateInstance) so that
+ * benchmarks do not cross into Python per frame.  Matches rt_update_fn; `user` unused. */
+void rt_demo_update(void *user, rt_xform *xforms, size_t instance_count, uint64_t frame);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RT_H */

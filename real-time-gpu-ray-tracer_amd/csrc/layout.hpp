@@ -1,0 +1,137 @@
+// layout.hpp — HBM data layout of a scene, shared by the host builder and the HIP kernels.
+//
+// The reference stores AoS BLASNode/TLASNode records of 40 B (24 B box + two size_t,
+// include/AS/BLAS.cuh:20-34), 16 B {type,size_t} index pairs, 112 B triangles and 464 B
+// instances, and fetches them node by node with a re-test of every popped node.  This layout
+// keeps exactly the same trees (same topology, same leaf order) but stores them as
+//   * node PAIRS: the two child boxes of one interior node in one 64 B record (4 x dwordx4),
+//     so visiting a node = one 64 B fetch that tests both children (BLAS.cu:180-202);
+//   * leaf-ordered primitive arrays: a leaf's primitives are contiguous, so the per-slot index
+//     array (BLAS.cu:72-77) disappears; hot intersection data (v0,e1,e2) is split from cold
+//     shading data (vertex normals, material) that is only read for the final hit;
+//   * instance hot records (inverse 3x4 + BLAS root box/ref, 80 B) split from cold records
+//     (forward 3x4 + inverse-transpose 3x4, 96 B) used once per closest hit.
+#pragma once
+#include <stdint.h>
+
+namespace rtamd {
+
+// ---- node references (32 bit) --------------------------------------------------------
+// interior:            [31]=0 [30]=level [29:0]  node-pair index
+// leaf:                [31]=1 [30]=level [29:28] primitive type (BLAS) [27:26] count-1
+//                      [25:0] first slot (BLAS: slot in the type's leaf-ordered array;
+//                      TLAS: slot in tlas_slots)
+// level: 0 = TLAS (world-space ray), 1 = BLAS (instance-space ray)
+constexpr uint32_t REF_LEAF = 1u << 31;
+constexpr uint32_t REF_BLAS = 1u << 30;
+constexpr uint32_t REF_INDEX_MASK = (1u << 30) - 1u;
+constexpr uint32_t REF_START_MASK = (1u << 26) - 1u;
+constexpr uint32_t MAX_LEAF_SLOTS = 1u << 26;
+
+__host__ __device__ inline uint32_t make_interior_ref(uint32_t pair, bool blas) {
+    return (blas ? REF_BLAS : 0u) | (pair & REF_INDEX_MASK);
+}
+__host__ __device__ inline uint32_t make_leaf_ref(uint32_t start, uint32_t count, uint32_t ptype, bool blas) {
+    return REF_LEAF | (blas ? REF_BLAS : 0u) | ((ptype & 3u) << 28) | (((count - 1u) & 3u) << 26) |
+           (start & REF_START_MASK);
+}
+__host__ __device__ inline uint32_t ref_leaf_start(uint32_t r) { return r & REF_START_MASK; }
+__host__ __device__ inline uint32_t ref_leaf_count(uint32_t r) { return ((r >> 26) & 3u) + 1u; }
+__host__ __device__ inline uint32_t ref_leaf_type(uint32_t r) { return (r >> 28) & 3u; }
+
+// ---- records -------------------------------------------------------------------------
+struct alignas(16) NodePair {       // 64 B
+    float c0[6];                    // child 0 box {xmin,xmax,ymin,ymax,zmin,zmax}
+    float c1[6];                    // child 1 box
+    uint32_t ref0, ref1;            // child refs (child 0 = `left`, child 1 = `left+1`)
+    uint32_t pad0, pad1;
+};
+static_assert(sizeof(NodePair) == 64, "NodePair must be 64 B");
+
+struct alignas(16) TriHot {         // 48 B: Moller-Trumbore operands (Triangle.cu:4-44)
+    float v0[3]; float pad0;
+    float e1[3]; float pad1;
+    float e2[3]; float pad2;
+};
+struct alignas(16) TriCold {        // 48 B: vertex normals + material + caller index
+    float n0[3]; uint32_t material;     // material = slot | (type << 31)
+    float n1[3]; uint32_t orig_index;
+    float n2[3]; uint32_t pad;
+};
+struct alignas(16) SphereHot {      // 16 B (Sphere.cu:4-49)
+    float center[3]; float radius;
+};
+struct alignas(16) QuadHot {        // 80 B: every value Parallelogram::hit reads or recomputes
+    float n[3]; float d;            // unit plane normal, plane constant (Parallelogram.cuh:31-38)
+    float q[3]; float den;          // origin, |u x v|^2 (Parallelogram.cu:23-24)
+    float u[3]; float pad0;
+    float v[3]; float pad1;
+    float nx[3]; float pad2;        // u x v, unnormalised (Parallelogram.cu:23)
+};
+struct alignas(16) PrimCold {       // 16 B: sphere / quad material and caller index
+    uint32_t material; uint32_t orig_index; uint32_t pad0, pad1;
+};
+
+struct alignas(16) InstHot {        // 80 B: what Instance::hit needs before BLAS traversal
+    float inv[12];                  // rows 1..3 of transformInverse (4 cols)  (Instance.cu:26-27)
+    float root_box[6];              // BLAS root node box (local space)
+    uint32_t root_ref;              // BLAS root ref (leaf or interior, level = BLAS)
+    uint32_t pad;
+};
+static_assert(sizeof(InstHot) == 80, "InstHot must be 80 B");
+struct alignas(16) InstCold {       // 96 B: hit finalisation (Instance.cu:41-45)
+    float fwd[12];                  // rows 1..3 of transformMatrix
+    float nrm[12];                  // rows 1..3 of normalTransformMatrix
+};
+
+constexpr uint32_t MAT_METAL_BIT = 1u << 31;
+
+// ---- kernel arguments ----------------------------------------------------------------
+struct SceneGPU {
+    const NodePair *blas_pairs;
+    const NodePair *tlas_pairs;
+    const uint32_t *tlas_slots;     // TLAS leaf slot -> instance index
+    const InstHot *inst_hot;
+    const InstCold *inst_cold;
+    const TriHot *tri_hot;
+    const TriCold *tri_cold;
+    const SphereHot *sph_hot;
+    const PrimCold *sph_cold;
+    const QuadHot *quad_hot;
+    const PrimCold *quad_cold;
+    const float *materials;         // 4 floats per slot: albedo.xyz, fuzz (roughs then metals)
+    float tlas_root_box[6];
+    uint32_t tlas_root_ref;
+    uint32_t instance_count;
+};
+
+struct CameraGPU {                  // Camera (RendererImpl.cuh:32-61), precomputed on host
+    float pixel_origin[3];
+    float dx[3], dy[3];
+    float center[3];
+    float cu[3], cv[3];
+    float background[3];
+    float focus_radius;
+    float recip_sqrt;
+    uint32_t sqrt_s;
+    uint32_t depth;
+    uint32_t width, height;
+    uint32_t pitch;                 // ceil(W/16)*16: the padded width of Kernel.cu:109
+    uint64_t frame_seed;
+};
+
+struct OutputGPU {
+    uint8_t *rgba;                  // uchar4 per pixel
+    float *rgb;                     // optional
+    uint32_t units;                 // number of 8x8 work units
+    uint32_t units_x;               // frame layout: units per row
+    // tile layout (tile_count > 0)
+    uint32_t tile_w, tile_h, tile_rank, tile_count, tiles_x;
+};
+
+// Counter slots (device uint64 array)
+enum CounterSlot : uint32_t {
+    CNT_RAYS = 0, CNT_PIXELS, CNT_PAIRS, CNT_TRI, CNT_SPHQUAD, CNT_QUAD, CNT_INST, CNT_HITS, CNT_OVERFLOW, CNT_NUM
+};
+
+}  // namespace rtamd

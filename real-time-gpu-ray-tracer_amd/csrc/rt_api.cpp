@@ -1,0 +1,722 @@
+// rt_api.cpp — the C ABI (include/rt.h): scene lifecycle, BLAS/TLAS builds, HBM upload,
+// per-frame instance update with double-buffered TLAS upload, and kernel launches.
+//
+// Mirrors the reference's host orchestration (src/Global/Renderer.cu, RenderPin.cu,
+// RenderGlob.cu) without windowing: commit geometry/materials, configure instances, build the
+// acceleration structures, configure the camera, then per frame update instances, rebuild the
+// TLAS on the host, upload it on a stream that is ordered against the previous frame's kernel
+// through events (Renderer.cu:236-317), and launch the trace kernel.  Errors return rt_status
+// with a thread-local message instead of exit() (Global.cu:34-41).
+#include <hip/hip_runtime.h>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/rt.h"
+#include "bvh_build.hpp"
+#include "host_math.hpp"
+#include "layout.hpp"
+
+namespace rtamd {
+hipError_t launch_render_exact(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *, hipStream_t);
+hipError_t launch_render_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *, hipStream_t);
+hipError_t launch_trace_rays_exact(const SceneGPU &, const float *, uint32_t, rt_hit *, hipStream_t);
+hipError_t launch_trace_rays_fast(const SceneGPU &, const float *, uint32_t, rt_hit *, hipStream_t);
+hipError_t launch_assemble(const void *, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, void *, hipStream_t);
+}  // namespace rtamd
+
+using namespace rtamd;
+
+namespace {
+
+thread_local std::string g_error;
+
+rt_status fail(rt_status s, const std::string &msg) {
+    g_error = msg;
+    return s;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess)                                                                      \
+            return fail(e_ == hipErrorOutOfMemory ? RT_ERR_OUT_OF_MEMORY : RT_ERR_DEVICE,          \
+                        std::string(#expr) + ": " + hipGetErrorString(e_));                       \
+    } while (0)
+
+constexpr uint32_t BLAS_LEAF_CAP = 4;   // BLAS.cuh:17
+constexpr uint32_t TLAS_LEAF_CAP = 2;   // TLAS.cuh:22
+
+struct InstState {
+    uint32_t ptype, pindex, pcount, blas;
+    hm::Box box;
+    hm::V3 centroid;
+    hm::Mat fwd, inv, nrm;
+    hm::Box tbox;
+    hm::V3 tcentroid;
+    rt_xform x;
+};
+
+struct BlasHost {
+    uint32_t type;
+    Tree tree;
+    FlatTree flat;
+    uint32_t pair_base, slot_base;
+};
+
+template <typename T>
+struct DevBuf {
+    T *p = nullptr;
+    size_t n = 0;
+    void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+};
+
+size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
+
+}  // namespace
+
+struct rt_scene {
+    int device = 0;
+    // caller data (copied, Renderer.cu:31-39)
+    std::vector<rt_sphere> spheres;
+    std::vector<rt_parallelogram> quads;
+    std::vector<rt_triangle> tris;
+    std::vector<rt_rough> roughs;
+    std::vector<rt_metal> metals;
+    std::vector<rt_instance_desc> inst_desc;
+    rt_update_fn update = nullptr;
+    void *update_user = nullptr;
+
+    std::vector<InstState> inst;
+    std::vector<BlasHost> blas;
+    Tree tlas;
+    FlatTree tlas_flat;
+    uint64_t build_seed = 0;
+    bool built = false;
+    uint64_t frame = 0;
+
+    // HBM: static scene data
+    DevBuf<NodePair> blas_pairs;
+    DevBuf<TriHot> tri_hot;
+    DevBuf<TriCold> tri_cold;
+    DevBuf<SphereHot> sph_hot;
+    DevBuf<PrimCold> sph_cold;
+    DevBuf<QuadHot> quad_hot;
+    DevBuf<PrimCold> quad_cold;
+    DevBuf<float> materials;
+    uint64_t blas_pair_count = 0, blas_leaf_count = 0;
+
+    // per-frame data, double-buffered: [tlas pairs | tlas slots | inst hot | inst cold]
+    size_t frame_block = 0, off_slots = 0, off_hot = 0, off_cold = 0;
+    uint8_t *staging[2] = {nullptr, nullptr};     // pinned host
+    uint8_t *frame_dev[2] = {nullptr, nullptr};   // HBM
+    hipEvent_t ev_copied[2] = {nullptr, nullptr}; // upload from staging[b] finished
+    hipEvent_t ev_used[2] = {nullptr, nullptr};   // last kernel reading frame_dev[b] finished
+    int active = -1;
+    uint32_t tlas_root_ref = 0;
+    float tlas_root_box[6] = {0, 0, 0, 0, 0, 0};
+
+    hipStream_t stream = nullptr;
+    hipEvent_t k_start = nullptr, k_stop = nullptr;
+    unsigned long long *counters = nullptr;       // HBM CNT_NUM
+    unsigned long long *counters_host = nullptr;  // pinned
+
+    // camera
+    bool cam_ok = false;
+    CameraGPU cam{};
+    uint32_t width = 0, height = 0;
+
+    // scene-owned outputs
+    DevBuf<uint8_t> out_rgba;
+    DevBuf<float> out_rgb;
+
+    ~rt_scene() {
+        (void)hipSetDevice(device);
+        if (stream) (void)hipStreamSynchronize(stream);
+        blas_pairs.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
+        quad_hot.release(); quad_cold.release(); materials.release(); out_rgba.release(); out_rgb.release();
+        for (int b = 0; b < 2; b++) {
+            if (staging[b]) (void)hipHostFree(staging[b]);
+            if (frame_dev[b]) (void)hipFree(frame_dev[b]);
+            if (ev_copied[b]) (void)hipEventDestroy(ev_copied[b]);
+            if (ev_used[b]) (void)hipEventDestroy(ev_used[b]);
+        }
+        if (counters) (void)hipFree(counters);
+        if (counters_host) (void)hipHostFree(counters_host);
+        if (k_start) (void)hipEventDestroy(k_start);
+        if (k_stop) (void)hipEventDestroy(k_stop);
+        if (stream) (void)hipStreamDestroy(stream);
+    }
+};
+
+namespace {
+
+// Instance::updateTransformArguments (src/AS/Instance.cu:4-17)
+void instance_update(InstState &in, const rt_xform &x) {
+    in.x = x;
+    in.fwd = hm::shift_matrix(hm::of(x.shift)) * hm::rotate_matrix(hm::of(x.rotate_deg)) * hm::scale_matrix(hm::of(x.scale));
+    in.inv = hm::inverse(in.fwd);
+    in.nrm = hm::transpose(in.inv);
+    in.tbox = hm::transform_box(in.box, in.fwd);
+    in.tcentroid = hm::apply_point(in.fwd, in.centroid);
+}
+
+hm::Box prim_box(const rt_scene *s, uint32_t type, uint32_t i) {
+    if (type == RT_PRIM_SPHERE) return hm::sphere_box(s->spheres[i]);
+    if (type == RT_PRIM_PARALLELOGRAM) return hm::quad_box(s->quads[i]);
+    return hm::tri_box(s->tris[i]);
+}
+hm::V3 prim_centroid(const rt_scene *s, uint32_t type, uint32_t i) {
+    if (type == RT_PRIM_SPHERE) return hm::sphere_centroid(s->spheres[i]);
+    if (type == RT_PRIM_PARALLELOGRAM) return hm::quad_centroid(s->quads[i]);
+    return hm::tri_centroid(s->tris[i]);
+}
+size_t prim_len(const rt_scene *s, uint32_t type) {
+    return type == RT_PRIM_SPHERE ? s->spheres.size() : (type == RT_PRIM_PARALLELOGRAM ? s->quads.size() : s->tris.size());
+}
+
+uint32_t material_slot(const rt_scene *s, uint32_t type, uint32_t index, bool &ok) {
+    if (type == RT_MAT_ROUGH && index < s->roughs.size()) return index;
+    if (type == RT_MAT_METAL && index < s->metals.size()) return (uint32_t)(s->roughs.size() + index) | MAT_METAL_BIT;
+    ok = false;
+    return 0;
+}
+
+void store_rows(float *dst, const hm::Mat &m) {   // rows 1..3, cols 1..4
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 4; j++) dst[4 * i + j] = m.d[i + 1][j + 1];
+}
+
+// Host half of one frame: update callback, instance matrices, TLAS rebuild, staging, upload.
+rt_status frame_update(rt_scene *s, uint64_t frame) {
+    const int b = s->active < 0 ? 0 : 1 - s->active;
+    HIP_TRY(hipEventSynchronize(s->ev_copied[b]));     // staging[b] no longer read by a pending copy
+    if (s->update) {                                  // Renderer.cu:269
+        std::vector<rt_xform> xs(s->inst.size());
+        for (size_t i = 0; i < xs.size(); i++) xs[i] = s->inst[i].x;
+        s->update(s->update_user, xs.data(), xs.size(), frame);
+        for (size_t i = 0; i < xs.size(); i++) instance_update(s->inst[i], xs[i]);
+    }
+    // TLAS::constructTLAS over transformed instance boxes (Renderer.cu:275, TLAS.cu:4-129)
+    std::vector<BuildItem> items(s->inst.size());
+    for (size_t i = 0; i < items.size(); i++) items[i] = {s->inst[i].tbox, s->inst[i].tcentroid, (uint32_t)i};
+    s->tlas = build_median_tree(std::move(items), TLAS_LEAF_CAP, hm::tlas_axis_state(s->build_seed, frame));
+    s->tlas_flat = flatten_tree(s->tlas, 0, 0, 0, false);
+    s->tlas_root_ref = s->tlas_flat.root_ref;
+    std::memcpy(s->tlas_root_box, s->tlas_flat.root_box, sizeof s->tlas_root_box);
+
+    uint8_t *st = s->staging[b];
+    std::memcpy(st, s->tlas_flat.pairs.data(), s->tlas_flat.pairs.size() * sizeof(NodePair));
+    std::memcpy(st + s->off_slots, s->tlas.refs.data(), s->tlas.refs.size() * sizeof(uint32_t));
+    InstHot *hot = reinterpret_cast<InstHot *>(st + s->off_hot);
+    InstCold *cold = reinterpret_cast<InstCold *>(st + s->off_cold);
+    for (size_t i = 0; i < s->inst.size(); i++) {
+        const InstState &in = s->inst[i];
+        const BlasHost &bl = s->blas[in.blas];
+        store_rows(hot[i].inv, in.inv);
+        std::memcpy(hot[i].root_box, bl.flat.root_box, sizeof hot[i].root_box);
+        hot[i].root_ref = bl.flat.root_ref;
+        hot[i].pad = 0;
+        store_rows(cold[i].fwd, in.fwd);
+        store_rows(cold[i].nrm, in.nrm);
+    }
+    HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_used[b], 0));        // frame_dev[b] free on device
+    HIP_TRY(hipMemcpyAsync(s->frame_dev[b], st, s->frame_block, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(hipEventRecord(s->ev_copied[b], s->stream));
+    s->active = b;
+    s->frame = frame;
+    return RT_OK;
+}
+
+SceneGPU scene_gpu(const rt_scene *s) {
+    SceneGPU g{};
+    const int b = s->active;
+    g.blas_pairs = s->blas_pairs.p;
+    g.tlas_pairs = reinterpret_cast<const NodePair *>(s->frame_dev[b]);
+    g.tlas_slots = reinterpret_cast<const uint32_t *>(s->frame_dev[b] + s->off_slots);
+    g.inst_hot = reinterpret_cast<const InstHot *>(s->frame_dev[b] + s->off_hot);
+    g.inst_cold = reinterpret_cast<const InstCold *>(s->frame_dev[b] + s->off_cold);
+    g.tri_hot = s->tri_hot.p; g.tri_cold = s->tri_cold.p;
+    g.sph_hot = s->sph_hot.p; g.sph_cold = s->sph_cold.p;
+    g.quad_hot = s->quad_hot.p; g.quad_cold = s->quad_cold.p;
+    g.materials = s->materials.p;
+    std::memcpy(g.tlas_root_box, s->tlas_root_box, sizeof g.tlas_root_box);
+    g.tlas_root_ref = s->tlas_root_ref;
+    g.instance_count = (uint32_t)s->inst.size();
+    return g;
+}
+
+template <typename T>
+rt_status upload(DevBuf<T> &buf, const std::vector<T> &v) {
+    buf.release();
+    const size_t n = v.empty() ? 1 : v.size();
+    HIP_TRY(hipMalloc(&buf.p, n * sizeof(T)));
+    buf.n = v.size();
+    if (!v.empty()) HIP_TRY(hipMemcpy(buf.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t tw, uint32_t th, uint32_t rank, uint32_t count) {
+    if (tw == 0 || th == 0 || count == 0) return 0;
+    const uint32_t total = ((w + tw - 1) / tw) * ((h + th - 1) / th);
+    return rank < total ? (total - rank + count - 1) / count : 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t rt_abi_version(void) { return RT_ABI_VERSION; }
+
+const char *rt_last_error(void) { return g_error.c_str(); }
+
+int rt_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+rt_status rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
+    if (!d || !out) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
+    *out = nullptr;
+    if (d->instance_count == 0) return fail(RT_ERR_INVALID_ARGUMENT, "scene has no instances");
+    if ((d->sphere_count && !d->spheres) || (d->parallelogram_count && !d->parallelograms) ||
+        (d->triangle_count && !d->triangles) || (d->rough_count && !d->roughs) || (d->metal_count && !d->metals) ||
+        !d->instances)
+        return fail(RT_ERR_INVALID_ARGUMENT, "count without array");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return fail(RT_ERR_DEVICE, "no HIP device present");
+    if (device < 0 || device >= ndev) return fail(RT_ERR_INVALID_ARGUMENT, "device index out of range");
+    auto *s = new (std::nothrow) rt_scene();
+    if (!s) return fail(RT_ERR_OUT_OF_MEMORY, "host allocation failed");
+    s->device = device;
+    s->spheres.assign(d->spheres, d->spheres + d->sphere_count);
+    s->quads.assign(d->parallelograms, d->parallelograms + d->parallelogram_count);
+    s->tris.assign(d->triangles, d->triangles + d->triangle_count);
+    s->roughs.assign(d->roughs, d->roughs + d->rough_count);
+    s->metals.assign(d->metals, d->metals + d->metal_count);
+    s->inst_desc.assign(d->instances, d->instances + d->instance_count);
+    s->update = d->update;
+    s->update_user = d->update_user;
+    // validate instance map (RenderPin.cu:119-172 would read out of bounds instead)
+    for (const auto &id : s->inst_desc) {
+        if (id.primitive_type > RT_PRIM_TRIANGLE) { delete s; return fail(RT_ERR_INVALID_ARGUMENT, "bad primitive type"); }
+        const size_t len = prim_len(s, id.primitive_type);
+        const size_t cnt = id.primitive_count ? id.primitive_count : 1;
+        if ((size_t)id.primitive_index + cnt > len) { delete s; return fail(RT_ERR_INVALID_ARGUMENT, "instance primitive range out of bounds"); }
+    }
+    *out = s;
+    return RT_OK;
+}
+
+rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
+    if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
+    if (mode != RT_BUILD_COMPAT_MEDIAN) return fail(RT_ERR_UNSUPPORTED, "unsupported build mode");
+    HIP_TRY(hipSetDevice(s->device));
+    s->build_seed = seed;
+    s->inst.clear();
+    s->blas.clear();
+
+    // buildBLASPinMem (RenderPin.cu:99-201): complete instances, one BLAS per unique (type, index).
+    // The reference's map stores the instance index instead of the BLAS index (RenderPin.cu:151);
+    // the BLAS index is stored here (identical whenever the reference's demo order is used).
+    std::vector<std::pair<uint64_t, uint32_t>> seen;
+    uint32_t pair_base = 0;
+    uint32_t slot_base[3] = {0, 0, 0};
+    for (size_t i = 0; i < s->inst_desc.size(); i++) {
+        const rt_instance_desc &id = s->inst_desc[i];
+        InstState in{};
+        in.ptype = id.primitive_type; in.pindex = id.primitive_index; in.pcount = id.primitive_count;
+        if (in.pcount == 0) {
+            in.pcount = 1;                                           // objectPrimitiveCount()
+            in.box = prim_box(s, in.ptype, in.pindex);
+            in.centroid = prim_centroid(s, in.ptype, in.pindex);
+        } else if (id.has_local_bounds) {                            // VTKReader.cu:204-209
+            in.box = hm::Box::from_ranges({id.local_bounds[0], id.local_bounds[1]}, {id.local_bounds[2], id.local_bounds[3]},
+                                          {id.local_bounds[4], id.local_bounds[5]});
+            in.centroid = hm::of(id.local_centroid);
+        } else {                                                     // extension: union box, mean centroid
+            hm::Box bb = prim_box(s, in.ptype, in.pindex);
+            double c[3] = {0, 0, 0};
+            for (uint32_t k = 0; k < in.pcount; k++) {
+                if (k) bb = hm::Box::merge(bb, prim_box(s, in.ptype, in.pindex + k));
+                const hm::V3 pc = prim_centroid(s, in.ptype, in.pindex + k);
+                for (int a = 0; a < 3; a++) c[a] += pc[a];
+            }
+            in.box = bb;
+            in.centroid = hm::v3((float)(c[0] / in.pcount), (float)(c[1] / in.pcount), (float)(c[2] / in.pcount));
+        }
+        const uint64_t key = ((uint64_t)in.ptype << 32) | in.pindex;
+        bool dup = false;
+        for (const auto &kv : seen)
+            if (kv.first == key) { in.blas = kv.second; dup = true; break; }
+        if (!dup) {
+            in.blas = (uint32_t)s->blas.size();
+            seen.push_back({key, in.blas});
+            BlasHost bh;
+            bh.type = in.ptype;
+            std::vector<BuildItem> items(in.pcount);
+            for (uint32_t k = 0; k < in.pcount; k++)
+                items[k] = {prim_box(s, in.ptype, in.pindex + k), prim_centroid(s, in.ptype, in.pindex + k), in.pindex + k};
+            bh.tree = build_median_tree(std::move(items), BLAS_LEAF_CAP, hm::blas_axis_state(seed, in.blas));
+            bh.pair_base = pair_base;
+            bh.slot_base = slot_base[in.ptype];
+            if ((uint64_t)slot_base[in.ptype] + in.pcount >= MAX_LEAF_SLOTS)
+                return fail(RT_ERR_UNSUPPORTED, "too many primitives of one type (2^26 leaf slots)");
+            bh.flat = flatten_tree(bh.tree, pair_base, bh.slot_base, in.ptype, true);
+            pair_base += (uint32_t)bh.flat.pairs.size();
+            slot_base[in.ptype] += in.pcount;
+            s->blas.push_back(std::move(bh));
+        }
+        s->inst.push_back(in);
+    }
+
+    // leaf-ordered primitive arrays + node pairs
+    std::vector<NodePair> pairs;
+    pairs.reserve(pair_base);
+    std::vector<TriHot> th; std::vector<TriCold> tc;
+    std::vector<SphereHot> sh; std::vector<PrimCold> sc;
+    std::vector<QuadHot> qh; std::vector<PrimCold> qc;
+    th.reserve(slot_base[2]); tc.reserve(slot_base[2]);
+    bool mat_ok = true;
+    s->blas_leaf_count = 0;
+    for (const BlasHost &bh : s->blas) {
+        pairs.insert(pairs.end(), bh.flat.pairs.begin(), bh.flat.pairs.end());
+        s->blas_leaf_count += bh.flat.leaves;
+        for (uint32_t pi : bh.tree.refs) {
+            if (bh.type == RT_PRIM_TRIANGLE) {
+                const rt_triangle &t = s->tris[pi];
+                const hm::TriDerived dv = hm::tri_derive(t);
+                TriHot h{};
+                TriCold c{};
+                for (int a = 0; a < 3; a++) {
+                    h.v0[a] = hm::of(t.vertex[0])[a]; h.e1[a] = dv.e1[a]; h.e2[a] = dv.e2[a];
+                    c.n0[a] = dv.n[0][a]; c.n1[a] = dv.n[1][a]; c.n2[a] = dv.n[2][a];
+                }
+                c.material = material_slot(s, t.material_type, t.material_index, mat_ok);
+                c.orig_index = pi;
+                th.push_back(h); tc.push_back(c);
+            } else if (bh.type == RT_PRIM_SPHERE) {
+                const rt_sphere &sp = s->spheres[pi];
+                sh.push_back(SphereHot{{sp.center.x, sp.center.y, sp.center.z}, sp.radius});
+                sc.push_back(PrimCold{material_slot(s, sp.material_type, sp.material_index, mat_ok), pi, 0, 0});
+            } else {
+                const rt_parallelogram &p = s->quads[pi];
+                const hm::QuadDerived dv = hm::quad_derive(p);
+                QuadHot q{};
+                for (int a = 0; a < 3; a++) {
+                    q.n[a] = dv.n[a]; q.q[a] = hm::of(p.q)[a]; q.u[a] = hm::of(p.u)[a]; q.v[a] = hm::of(p.v)[a];
+                    q.nx[a] = dv.nx[a];
+                }
+                q.d = dv.d; q.den = dv.den;
+                qh.push_back(q);
+                qc.push_back(PrimCold{material_slot(s, p.material_type, p.material_index, mat_ok), pi, 0, 0});
+            }
+        }
+    }
+    if (!mat_ok) return fail(RT_ERR_INVALID_ARGUMENT, "primitive references a material out of range");
+    std::vector<float> mats;
+    for (const auto &r : s->roughs) { mats.push_back(r.albedo.x); mats.push_back(r.albedo.y); mats.push_back(r.albedo.z); mats.push_back(0.0f); }
+    for (const auto &m : s->metals) { mats.push_back(m.albedo.x); mats.push_back(m.albedo.y); mats.push_back(m.albedo.z); mats.push_back(m.fuzz); }
+    s->blas_pair_count = pairs.size();
+
+    rt_status st;
+    if ((st = upload(s->blas_pairs, pairs)) != RT_OK) return st;
+    if ((st = upload(s->tri_hot, th)) != RT_OK) return st;
+    if ((st = upload(s->tri_cold, tc)) != RT_OK) return st;
+    if ((st = upload(s->sph_hot, sh)) != RT_OK) return st;
+    if ((st = upload(s->sph_cold, sc)) != RT_OK) return st;
+    if ((st = upload(s->quad_hot, qh)) != RT_OK) return st;
+    if ((st = upload(s->quad_cold, qc)) != RT_OK) return st;
+    if ((st = upload(s->materials, mats)) != RT_OK) return st;
+
+    // per-frame double buffers
+    const size_t n = s->inst.size();
+    s->off_slots = align16(n * sizeof(NodePair));
+    s->off_hot = align16(s->off_slots + n * sizeof(uint32_t));
+    s->off_cold = align16(s->off_hot + n * sizeof(InstHot));
+    s->frame_block = align16(s->off_cold + n * sizeof(InstCold));
+    if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    for (int b = 0; b < 2; b++) {
+        if (s->staging[b]) { (void)hipHostFree(s->staging[b]); s->staging[b] = nullptr; }
+        if (s->frame_dev[b]) { (void)hipFree(s->frame_dev[b]); s->frame_dev[b] = nullptr; }
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->staging[b]), s->frame_block, hipHostMallocDefault));
+        HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->frame_dev[b]), s->frame_block));
+        if (!s->ev_copied[b]) HIP_TRY(hipEventCreateWithFlags(&s->ev_copied[b], hipEventDisableTiming));
+        if (!s->ev_used[b]) HIP_TRY(hipEventCreateWithFlags(&s->ev_used[b], hipEventDisableTiming));
+    }
+    if (!s->k_start) HIP_TRY(hipEventCreate(&s->k_start));
+    if (!s->k_stop) HIP_TRY(hipEventCreate(&s->k_stop));
+    if (!s->counters) HIP_TRY(hipMalloc(&s->counters, CNT_NUM * sizeof(unsigned long long)));
+    if (!s->counters_host)
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->counters_host), CNT_NUM * sizeof(unsigned long long), hipHostMallocDefault));
+    s->active = -1;
+
+    // initial transforms, then the frame-0 update + TLAS (Renderer.cu:110-111, 148-150)
+    for (size_t i = 0; i < n; i++) instance_update(s->inst[i], s->inst_desc[i].xform);
+    s->built = true;
+    return frame_update(s, 0);
+}
+
+rt_status rt_camera_set(rt_scene *s, const rt_camera_input *c, uint32_t w, uint32_t h) {
+    if (!s || !c) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
+    if (w == 0 || h == 0 || w > 32768 || h > 32768) return fail(RT_ERR_INVALID_ARGUMENT, "bad framebuffer size");
+    if (c->sample_count == 0) return fail(RT_ERR_INVALID_ARGUMENT, "sample_count must be >= 1");
+    // RendererImpl::calculateCameraProperties (src/Global/RenderPin.cu:73-95)
+    using namespace hm;
+    const V3 center = of(c->center), target = of(c->target), up = of(c->up);
+    const float fd = distance(center, target);
+    const float theta = c->fov * PI / 180.0f;
+    const float vw = 2.0f * std::tan(theta / 2.0f) * fd;
+    const float vh = vw / ((float)w * 1.0f / (float)h);
+    const V3 W = unit(target - center);
+    const V3 U = unit(cross(W, up));
+    const V3 V = unit(cross(U, W));
+    const V3 vx = U * vw, vy = V * vh;
+    const V3 dx = vx / (float)w, dy = vy / (float)h;
+    const V3 vorg = center + W * fd - vx * 0.5f - vy * 0.5f;
+    const V3 po = vorg + dx * 0.5f + dy * 0.5f;
+    CameraGPU &g = s->cam;
+    for (int a = 0; a < 3; a++) {
+        g.pixel_origin[a] = po[a]; g.dx[a] = dx[a]; g.dy[a] = dy[a]; g.center[a] = center[a];
+        g.cu[a] = U[a]; g.cv[a] = V[a]; g.background[a] = of(c->background)[a];
+    }
+    g.focus_radius = c->focus_disk_radius;
+    g.sqrt_s = (uint32_t)std::sqrt((double)c->sample_count);            // RenderPin.cu:93
+    g.recip_sqrt = 1.0f / (float)g.sqrt_s;                              // RenderPin.cu:94
+    g.depth = c->ray_trace_depth;
+    g.width = w; g.height = h;
+    g.pitch = (w + 15u) / 16u * 16u;                                    // 16x16 blocks (SDL_OpenGLWindow.cu:119-122)
+    s->width = w; s->height = h;
+    s->cam_ok = true;
+    return RT_OK;
+}
+
+rt_status rt_scene_update(rt_scene *s, uint64_t frame) {
+    if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
+    if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
+    HIP_TRY(hipSetDevice(s->device));
+    return frame_update(s, frame);
+}
+
+uint32_t rt_tiles_for_rank(const rt_scene *s, uint32_t tw, uint32_t th, uint32_t rank, uint32_t count) {
+    if (!s || !s->cam_ok) return 0;
+    return tiles_for_rank(s->width, s->height, tw, th, rank, count);
+}
+
+rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uint8_t *rgba_host, float *rgb_host,
+                    rt_stats *stats) {
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
+    if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
+    if (!s->cam_ok) return fail(RT_ERR_STATE, "rt_camera_set has not been called");
+    rt_render_opts o{};
+    if (opts) o = *opts;
+    if (o.frame_seed == 0) o.frame_seed = 0x5EED;
+    HIP_TRY(hipSetDevice(s->device));
+    double update_ms = 0.0;
+    if (!(o.flags & RT_RENDER_SKIP_UPDATE)) {
+        const auto u0 = std::chrono::steady_clock::now();
+        const rt_status st = frame_update(s, frame);
+        if (st != RT_OK) return st;
+        update_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - u0).count();
+    }
+    hipStream_t stream = o.stream ? static_cast<hipStream_t>(o.stream) : s->stream;
+
+    OutputGPU out{};
+    const uint32_t W = s->width, H = s->height;
+    size_t npix;
+    if (o.tile_count == 0) {
+        out.units_x = (W + 7) / 8;
+        out.units = out.units_x * ((H + 7) / 8);
+        npix = (size_t)W * H;
+    } else {
+        if (o.tile_w == 0 || o.tile_h == 0 || o.tile_w % 8 || o.tile_h % 8 || o.tile_rank >= o.tile_count)
+            return fail(RT_ERR_INVALID_ARGUMENT, "tiles must be multiples of 8 and tile_rank < tile_count");
+        const uint32_t mine = tiles_for_rank(W, H, o.tile_w, o.tile_h, o.tile_rank, o.tile_count);
+        out.tile_w = o.tile_w; out.tile_h = o.tile_h; out.tile_rank = o.tile_rank; out.tile_count = o.tile_count;
+        out.tiles_x = (W + o.tile_w - 1) / o.tile_w;
+        out.units = mine * (o.tile_w / 8) * (o.tile_h / 8);
+        npix = (size_t)mine * o.tile_w * o.tile_h;
+    }
+    // outputs: caller device buffers, else scene-owned
+    if (o.rgba8_device) {
+        out.rgba = static_cast<uint8_t *>(o.rgba8_device);
+    } else {
+        if (s->out_rgba.n < npix * 4) {
+            s->out_rgba.release();
+            HIP_TRY(hipMalloc(&s->out_rgba.p, npix * 4));
+            s->out_rgba.n = npix * 4;
+        }
+        out.rgba = s->out_rgba.p;
+    }
+    if (o.rgb32_device) {
+        out.rgb = static_cast<float *>(o.rgb32_device);
+    } else if (rgb_host) {
+        if (s->out_rgb.n < npix * 3) {
+            s->out_rgb.release();
+            HIP_TRY(hipMalloc(&s->out_rgb.p, npix * 3 * sizeof(float)));
+            s->out_rgb.n = npix * 3;
+        }
+        out.rgb = s->out_rgb.p;
+    }
+    CameraGPU cam = s->cam;
+    cam.frame_seed = o.frame_seed;
+    const SceneGPU g = scene_gpu(s);
+    const bool exact = (o.flags & RT_RENDER_EXACT) != 0;
+    const bool count = (o.flags & RT_RENDER_COUNT_WORK) != 0;
+
+    HIP_TRY(hipStreamWaitEvent(stream, s->ev_copied[s->active], 0));
+    HIP_TRY(hipMemsetAsync(s->counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
+    HIP_TRY(hipEventRecord(s->k_start, stream));
+    HIP_TRY(exact ? launch_render_exact(g, cam, out, count, s->counters, stream)
+                  : launch_render_fast(g, cam, out, count, s->counters, stream));
+    HIP_TRY(hipEventRecord(s->k_stop, stream));
+    HIP_TRY(hipEventRecord(s->ev_used[s->active], stream));
+    if (o.flags & RT_RENDER_NO_SYNC) {
+        if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; }
+        return RT_OK;
+    }
+    HIP_TRY(hipMemcpyAsync(s->counters_host, s->counters, CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipStreamSynchronize(stream));
+    if (rgba_host) HIP_TRY(hipMemcpy(rgba_host, out.rgba, npix * 4, hipMemcpyDeviceToHost));
+    if (rgb_host) HIP_TRY(hipMemcpy(rgb_host, out.rgb, npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
+    if (stats) {
+        float kms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&kms, s->k_start, s->k_stop));
+        const unsigned long long *c = s->counters_host;
+        stats->rays = c[CNT_RAYS];
+        stats->pixels = c[CNT_PIXELS];
+        stats->aabb_tests = 2ull * c[CNT_PAIRS];
+        stats->triangle_tests = c[CNT_TRI];
+        stats->sphere_quad_tests = c[CNT_SPHQUAD];
+        stats->quad_tests = c[CNT_QUAD];
+        stats->instance_visits = c[CNT_INST];
+        stats->hits = c[CNT_HITS];
+        stats->kernel_ms = kms;
+        stats->update_ms = update_ms;
+        stats->frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    if (count && s->counters_host[CNT_OVERFLOW] != 0)
+        return fail(RT_ERR_UNSUPPORTED, "traversal stack overflow (tree deeper than 64 levels)");
+    return RT_OK;
+}
+
+rt_status rt_assemble_tiles(rt_scene *s, const void *gathered, uint32_t slab_tiles, uint32_t tw, uint32_t th,
+                            uint32_t tile_count, void *frame, void *stream) {
+    if (!s || !gathered || !frame) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
+    if (!s->cam_ok) return fail(RT_ERR_STATE, "rt_camera_set has not been called");
+    if (tw == 0 || th == 0 || tile_count == 0) return fail(RT_ERR_INVALID_ARGUMENT, "bad tile geometry");
+    HIP_TRY(hipSetDevice(s->device));
+    hipStream_t st = stream ? static_cast<hipStream_t>(stream) : s->stream;
+    HIP_TRY(launch_assemble(gathered, slab_tiles, tw, th, tile_count, s->width, s->height, frame, st));
+    return RT_OK;
+}
+
+rt_status rt_trace_rays(rt_scene *s, const float *rays, size_t n, uint32_t flags, rt_hit *hits) {
+    if (!s || (n && (!rays || !hits))) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
+    if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
+    if (n == 0) return RT_OK;
+    if (n > 0xFFFFFFFFull) return fail(RT_ERR_INVALID_ARGUMENT, "too many rays");
+    HIP_TRY(hipSetDevice(s->device));
+    float *d_rays = nullptr;
+    rt_hit *d_hits = nullptr;
+    HIP_TRY(hipMalloc(&d_rays, n * 6 * sizeof(float)));
+    hipError_t e = hipMalloc(&d_hits, n * sizeof(rt_hit));
+    if (e != hipSuccess) { (void)hipFree(d_rays); return fail(RT_ERR_OUT_OF_MEMORY, "hipMalloc hits"); }
+    const SceneGPU g = scene_gpu(s);
+    e = hipMemcpyAsync(d_rays, rays, n * 6 * sizeof(float), hipMemcpyHostToDevice, s->stream);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s->stream, s->ev_copied[s->active], 0);
+    if (e == hipSuccess)
+        e = (flags & RT_RENDER_EXACT) ? launch_trace_rays_exact(g, d_rays, (uint32_t)n, d_hits, s->stream)
+                                      : launch_trace_rays_fast(g, d_rays, (uint32_t)n, d_hits, s->stream);
+    if (e == hipSuccess) e = hipEventRecord(s->ev_used[s->active], s->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
+    if (e == hipSuccess) e = hipMemcpy(hits, d_hits, n * sizeof(rt_hit), hipMemcpyDeviceToHost);
+    (void)hipFree(d_rays);
+    (void)hipFree(d_hits);
+    if (e != hipSuccess) return fail(RT_ERR_DEVICE, std::string("rt_trace_rays: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+rt_status rt_synchronize(rt_scene *s) {
+    if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
+    HIP_TRY(hipSetDevice(s->device));
+    if (s->stream) HIP_TRY(hipStreamSynchronize(s->stream));
+    return RT_OK;
+}
+
+void rt_scene_destroy(rt_scene *s) { delete s; }
+
+rt_status rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
+    if (!s || !info) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
+    std::memset(info, 0, sizeof *info);
+    info->blas_count = s->blas.size();
+    info->blas_node_pairs = s->blas_pair_count;
+    info->blas_leaves = s->blas_leaf_count;
+    info->tlas_node_pairs = s->tlas_flat.pairs.size();
+    info->device_bytes = s->blas_pairs.n * sizeof(NodePair) + s->tri_hot.n * sizeof(TriHot) + s->tri_cold.n * sizeof(TriCold) +
+                         s->sph_hot.n * sizeof(SphereHot) + s->sph_cold.n * sizeof(PrimCold) +
+                         s->quad_hot.n * sizeof(QuadHot) + s->quad_cold.n * sizeof(PrimCold) +
+                         s->materials.n * sizeof(float) + 2 * s->frame_block + s->out_rgba.n + s->out_rgb.n * sizeof(float);
+    info->width = s->width; info->height = s->height;
+    info->sqrt_sample_count = s->cam.sqrt_s;
+    info->ray_trace_depth = s->cam.depth;
+    return RT_OK;
+}
+
+static void export_tree(const Tree &t, float *boxes, uint32_t *ci) {
+    for (size_t i = 0; i < t.nodes.size(); i++) {
+        if (boxes) t.nodes[i].box.store(boxes + 6 * i);
+        if (ci) { ci[2 * i] = t.nodes[i].count; ci[2 * i + 1] = t.nodes[i].index; }
+    }
+}
+
+rt_status rt_scene_export_blas(const rt_scene *s, uint32_t b, float *boxes, uint32_t *ci, uint32_t *refs,
+                               uint32_t *n_nodes, uint32_t *n_prims) {
+    if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
+    if (!s->built || b >= s->blas.size()) return fail(RT_ERR_INVALID_ARGUMENT, "no such BLAS");
+    const Tree &t = s->blas[b].tree;
+    if (n_nodes) *n_nodes = (uint32_t)t.nodes.size();
+    if (n_prims) *n_prims = (uint32_t)t.refs.size();
+    export_tree(t, boxes, ci);
+    if (refs) std::memcpy(refs, t.refs.data(), t.refs.size() * sizeof(uint32_t));
+    return RT_OK;
+}
+
+rt_status rt_scene_export_tlas(const rt_scene *s, float *boxes, uint32_t *ci, uint32_t *refs, uint32_t *n_nodes,
+                               uint32_t *n_refs) {
+    if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
+    if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
+    if (n_nodes) *n_nodes = (uint32_t)s->tlas.nodes.size();
+    if (n_refs) *n_refs = (uint32_t)s->tlas.refs.size();
+    export_tree(s->tlas, boxes, ci);
+    if (refs) std::memcpy(refs, s->tlas.refs.data(), s->tlas.refs.size() * sizeof(uint32_t));
+    return RT_OK;
+}
+
+// updateInstance (src/Global/Main.cu:6-42)
+void rt_demo_update(void *user, rt_xform *x, size_t n, uint64_t frame) {
+    (void)user;
+    const float ic[3] = {0.0f, 2.0f, 0.0f};
+    const float radius = 2.0f, speed = 0.02f;
+    const float angle = (float)frame * speed;
+    const float c1[3] = {ic[0] + radius * std::cos(angle) * 1.5f, ic[1] + radius * std::sin(angle) * std::cos(angle),
+                         ic[2] + radius * std::sin(angle) * 1.5f};
+    const float c2[3] = {-c1[0], c1[1], -c1[2]};
+    const float c3[3] = {-c1[0], c1[1] + 5.0f, c1[2]};
+    const float rot = (float)frame * 0.4f;
+    const rt_xform t[5] = {
+        {{0.0f, -1000.0f, 0.0f}, {0.0f, 0.0f, 0.0f}, {1.0f, 1.0f, 1.0f}},
+        {{c1[0], c1[1], c1[2]}, {0.0f, 0.0f, 0.0f}, {1.0f, 1.0f, 1.0f}},
+        {{-5.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f}, {1.0f, 1.0f, 1.0f}},
+        {{c2[0], c2[1], c2[2]}, {rot, rot, rot}, {3.0f, 3.0f, 3.0f}},
+        {{c3[0], c3[1], c3[2]}, {0.0f, 0.0f, 0.0f}, {1.0f, 1.0f, 1.0f}},
+    };
+    for (size_t i = 0; i < n && i < 5; i++) x[i] = t[i];
+}
+
+}  // extern "C"

@@ -1,0 +1,576 @@
+// trace_kernel.hip — the hot path on gfx950: camera ray -> two-level BVH traversal
+// (TLAS -> instance -> BLAS) -> sphere / parallelogram / Moller-Trumbore intersection ->
+// Rough/Metal scatter loop -> average -> gamma-2 quantise -> framebuffer write.
+//
+// Restates the reference kernel `render` (src/Global/Kernel.cu:105-147) and its device
+// callees: rayColor (Kernel.cu:6-103), TLAS::hit (src/AS/TLAS.cu:131-201), Instance::hit
+// (src/AS/Instance.cu:19-50), BLAS::hit (src/AS/BLAS.cu:119-206), BoundingBox::hit
+// (src/AS/BoundingBox.cu:34-72), Sphere/Parallelogram/Triangle::hit (src/Geometry/*.cu),
+// Rough/Metal::scatter (include/Material/*.cuh), Color3::castToUchar4 (Color3.cuh:99-114).
+//
+// This file is compiled twice:
+//   RT_EXACT=1, -ffp-contract=off : every float operation in the reference's order with IEEE
+//       division — bit-faithful to the oracle on identical trees (parity mode);
+//   RT_EXACT=0, -ffp-contract=fast: reciprocal-direction slab tests (one FMA per plane),
+//       reciprocal determinant, FMA-contracted transforms (performance mode; parity within
+//       the stated tolerance).
+//
+// Traversal keeps the reference's visit order exactly: node pairs test both children of an
+// interior node (BLAS.cu:180-202), the near child (smaller entry t; ties -> left) is visited
+// next and the far child is pushed with its entry t; a popped entry is culled iff its entry t
+// >= the current tmax, which is exactly when the reference's re-test of the popped node box
+// (BLAS.cu:145) fails.  TLAS leaves with two instances push a non-cullable "resume" entry, as
+// the reference loops over a leaf's instances without re-testing the leaf box (TLAS.cu:157-173).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "layout.hpp"
+#include "../../include/rt.h"
+
+#ifndef RT_EXACT
+#error "compile with -DRT_EXACT=0 or 1"
+#endif
+
+#if RT_EXACT
+#define RT_SUFFIX(n) n##_exact
+#else
+#define RT_SUFFIX(n) n##_fast
+#endif
+
+namespace rtamd {
+namespace RT_SUFFIX(dev) {
+
+constexpr float FZERO = 1e-6f;          // FLOAT_ZERO_VALUE (Global.cuh:147)
+constexpr float TMIN = 0.001f;          // Kernel.cu:66
+constexpr int BLOCK = 256;              // 4 waves; each wave owns one 8x8 pixel unit
+constexpr int LDS_DEPTH = 16;           // per-lane stack entries kept in LDS
+constexpr int SPILL_DEPTH = 48;         // overflow entries in scratch (max depth 64 = reference)
+
+struct f3 { float x, y, z; };
+__device__ __forceinline__ f3 mk(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ f3 ld3(const float *p) { return mk(p[0], p[1], p[2]); }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 scl(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ f3 neg(f3 a) { return mk(-a.x, -a.y, -a.z); }
+__device__ __forceinline__ f3 mul(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ float dot(f3 a, f3 b) {          // Vec3.cuh:113-119
+    float s = 0.0f; s += a.x * b.x; s += a.y * b.y; s += a.z * b.z; return s;
+}
+__device__ __forceinline__ f3 cross(f3 a, f3 b) {           // Vec3.cuh:120-126
+    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ f3 unit(f3 a) {                   // Vec3.cuh:129-137
+    const float f = 1.0f / sqrtf(dot(a, a));
+    return mk(a.x * f, a.y * f, a.z * f);
+}
+__device__ __forceinline__ float comp(f3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+
+__device__ __forceinline__ bool f_eq(float a, float b) { return fabsf(a - b) < FZERO; }
+__device__ __forceinline__ bool in_range(float v, float mn, float mx) {      // Range.cuh:33-43
+    return f_eq(v, mn) || f_eq(v, mx) || (v > mn && v < mx);
+}
+
+// ---- pinned RNG contract (replaces curand XORWOW, Kernel.cu:114) ----------
+constexpr uint64_t GOLDEN64 = 0x9E3779B97F4A7C15ull;
+constexpr uint64_t SUBMUL64 = 0xD1B54A32D192ED03ull;
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+struct Rng {
+    uint64_t s;
+    __device__ __forceinline__ void init(uint64_t seed, uint64_t sub) { s = mix64((seed * GOLDEN64) ^ ((sub + 1ull) * SUBMUL64)); }
+    __device__ __forceinline__ float uniform() {                             // (0, 1]
+        s += GOLDEN64;
+        const uint64_t x = mix64(s);
+        return (float)((uint32_t)(x >> 40) + 1u) * 0x1p-24f;
+    }
+    __device__ __forceinline__ float range(float mn, float mx) { return mn + (mx - mn) * uniform(); }   // Global.cuh:209-211
+};
+__device__ __forceinline__ f3 random_space_vector(Rng &r) {   // Vec3.cu:54-65 (length 1)
+    f3 v; float l2;
+    do {
+        v.x = r.range(-1.0f, 1.0f);
+        v.y = r.range(-1.0f, 1.0f);
+        v.z = r.range(-1.0f, 1.0f);
+        l2 = dot(v, v);
+    } while (l2 < FZERO * FZERO);
+    return scl(unit(v), 1.0f);
+}
+__device__ __forceinline__ f3 random_plane_vector(Rng &r, float maxlen) {   // Vec3.cu:29-36
+    float x, y;
+    do {
+        x = r.range(-1.0f, 1.0f);
+        y = r.range(-1.0f, 1.0f);
+    } while (x * x + y * y > maxlen * maxlen);
+    return mk(x, y, 0.0f);
+}
+
+// ---- rays ---------------------------------------------------------------------------
+struct RayP {
+    f3 o, d;
+#if !RT_EXACT
+    f3 inv, oinv;      // 1/d and o/d for one-FMA slab planes
+    bool tiny;         // some |d_axis| < 1e-6: use the reference's parallel-axis branch
+#endif
+};
+__device__ __forceinline__ void prep(RayP &r) {
+#if !RT_EXACT
+    r.tiny = fabsf(r.d.x) < FZERO || fabsf(r.d.y) < FZERO || fabsf(r.d.z) < FZERO;
+    r.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    r.oinv = mk(r.o.x * r.inv.x, r.o.y * r.inv.y, r.o.z * r.inv.z);
+#else
+    (void)r;
+#endif
+}
+
+// BoundingBox::hit (BoundingBox.cu:34-72), reference arithmetic.  b = {xmin,xmax,ymin,ymax,zmin,zmax}
+__device__ __forceinline__ bool slab_ref(const float *b, const f3 &o, const f3 &d, float tmin, float tmax, float &te) {
+    float cmin = tmin, cmax = tmax;
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        const float q = comp(o, a), dd = comp(d, a), mn = b[2 * a], mx = b[2 * a + 1];
+        if (fabsf(dd) < FZERO) {
+            if (q < mn || q > mx) return false;
+            continue;
+        }
+        const float t1 = (mn - q) / dd;
+        const float t2 = (mx - q) / dd;
+        if (t1 < t2) {
+            if (t1 > cmin) cmin = t1;
+            if (t2 < cmax) cmax = t2;
+        } else {
+            if (t2 > cmin) cmin = t2;
+            if (t1 < cmax) cmax = t1;
+        }
+        if (cmin >= cmax) return false;
+    }
+    te = cmin;
+    return true;
+}
+
+__device__ __forceinline__ bool slab(const float *b, const RayP &r, float tmin, float tmax, float &te) {
+#if RT_EXACT
+    return slab_ref(b, r.o, r.d, tmin, tmax, te);
+#else
+    if (r.tiny) return slab_ref(b, r.o, r.d, tmin, tmax, te);
+    const float tx1 = fmaf(b[0], r.inv.x, -r.oinv.x), tx2 = fmaf(b[1], r.inv.x, -r.oinv.x);
+    const float ty1 = fmaf(b[2], r.inv.y, -r.oinv.y), ty2 = fmaf(b[3], r.inv.y, -r.oinv.y);
+    const float tz1 = fmaf(b[4], r.inv.z, -r.oinv.z), tz2 = fmaf(b[5], r.inv.z, -r.oinv.z);
+    const float lo = fmaxf(fmaxf(tmin, fminf(tx1, tx2)), fmaxf(fminf(ty1, ty2), fminf(tz1, tz2)));
+    const float hi = fminf(fminf(tmax, fmaxf(tx1, tx2)), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
+    te = lo;
+    return lo < hi;
+#endif
+}
+
+// ---- primitives (local space) ---------------------------------------------------------
+__device__ __forceinline__ bool tri_test(const TriHot &T, const RayP &r, float tmin, float tmax,
+                                         float &t, float &u, float &v) {      // Triangle.cu:4-44
+    const f3 e1 = ld3(T.e1), e2 = ld3(T.e2), v0 = ld3(T.v0);
+    const f3 h = cross(r.d, e2);
+    const float det = dot(e1, h);
+    if (fabsf(det) < FZERO) return false;
+    const f3 s = sub(r.o, v0);
+#if RT_EXACT
+    u = dot(s, h) / det;
+    if (!in_range(u, 0.0f, 1.0f)) return false;
+    const f3 q = cross(s, e1);
+    v = dot(r.d, q) / det;
+    if (!in_range(v, 0.0f, 1.0f) || u + v > 1.0f) return false;
+    t = dot(e2, q) / det;
+    return in_range(t, tmin, tmax);
+#else
+    const float inv = __builtin_amdgcn_rcpf(det);
+    const f3 q = cross(s, e1);
+    u = dot(s, h) * inv;
+    v = dot(r.d, q) * inv;
+    t = dot(e2, q) * inv;
+    return in_range(u, 0.0f, 1.0f) && in_range(v, 0.0f, 1.0f) && !(u + v > 1.0f) && in_range(t, tmin, tmax);
+#endif
+}
+
+__device__ __forceinline__ bool sphere_test(const SphereHot &S, const RayP &r, float tmin, float tmax, float &t) {
+    const f3 c = ld3(S.center);                                               // Sphere.cu:4-28
+    const f3 cq = sub(c, r.o);
+    const float a = dot(r.d, r.d);
+    const float b = -2.0f * dot(cq, r.d);
+    const float cc = dot(cq, cq) - S.radius * S.radius;
+    float delta = b * b - 4.0f * a * cc;
+    if (delta < 0.0f) return false;
+    delta = sqrtf(delta);
+    const float root1 = (-b - delta) / (a * 2.0f);
+    const float root2 = (-b + delta) / (a * 2.0f);
+    if (in_range(root1, tmin, tmax)) { t = root1; return true; }
+    if (in_range(root2, tmin, tmax)) { t = root2; return true; }
+    return false;
+}
+
+__device__ __forceinline__ bool quad_test(const QuadHot &Q, const RayP &r, float tmin, float tmax,
+                                          float &t, float &al, float &be) {   // Parallelogram.cu:4-36
+    const f3 n = ld3(Q.n);
+    const float ndd = dot(n, r.d);
+    if (fabsf(ndd) < FZERO) return false;
+    float ndp = 0.0f;
+    ndp += n.x * r.o.x; ndp += n.y * r.o.y; ndp += n.z * r.o.z;
+    const float tt = (Q.d - ndp) / ndd;
+    if (!in_range(tt, tmin, tmax)) return false;
+    const f3 inter = add(r.o, scl(r.d, tt));
+    const f3 p = sub(inter, ld3(Q.q));
+    const f3 nx = ld3(Q.nx);
+    if (fabsf(Q.den) < FZERO) return false;
+    al = dot(cross(p, ld3(Q.v)), nx) / Q.den;
+    be = dot(cross(ld3(Q.u), p), nx) / Q.den;
+    if (!in_range(al, 0.0f, 1.0f) || !in_range(be, 0.0f, 1.0f)) return false;
+    t = tt;
+    return true;
+}
+
+// (M * toMatrix(Point3)).toPoint() / (M * toMatrix(Vec3)).toVector() over rows 1..3 of a 4x4
+// (Matrix.cu:71-86); m = 12 floats (3 rows x 4 cols).
+__device__ __forceinline__ f3 xf_point(const float *m, f3 p) {
+    f3 r;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        float s = 0.0f;
+        s += m[4 * i] * p.x; s += m[4 * i + 1] * p.y; s += m[4 * i + 2] * p.z; s += m[4 * i + 3] * 1.0f;
+        if (i == 0) r.x = s; else if (i == 1) r.y = s; else r.z = s;
+    }
+    return r;
+}
+__device__ __forceinline__ f3 xf_vector(const float *m, f3 v) {
+    f3 r;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        float s = 0.0f;
+        s += m[4 * i] * v.x; s += m[4 * i + 1] * v.y; s += m[4 * i + 2] * v.z;
+#if RT_EXACT
+        s += m[4 * i + 3] * 0.0f;     // keeps the sign-of-zero behaviour of the 4x4 product
+#endif
+        if (i == 0) r.x = s; else if (i == 1) r.y = s; else r.z = s;
+    }
+    return r;
+}
+
+// ---- closest hit -----------------------------------------------------------------------
+struct Hit {
+    float t;
+    uint32_t inst;     // instance index
+    uint32_t ptype;    // primitive type
+    uint32_t slot;     // leaf-ordered slot in the type's array
+    float u, v;
+};
+
+struct LaneCount { uint32_t pairs, tri, sq, quad, inst, hits, overflow; };
+
+struct Stack {
+    uint2 (*lds)[BLOCK];   // [LDS_DEPTH][BLOCK]
+    uint2 spill[SPILL_DEPTH];
+    int sp;
+    int tid;
+    __device__ __forceinline__ void push(uint32_t ref, float tn, LaneCount &c) {
+        const uint2 e = make_uint2(ref, __float_as_uint(tn));
+        if (sp < LDS_DEPTH) lds[sp][tid] = e;
+        else if (sp < LDS_DEPTH + SPILL_DEPTH) spill[sp - LDS_DEPTH] = e;
+        else { c.overflow++; return; }       // the reference's 64-entry stack would overflow here
+        sp++;
+    }
+    __device__ __forceinline__ uint2 pop() {
+        --sp;
+        return sp < LDS_DEPTH ? lds[sp][tid] : spill[sp - LDS_DEPTH];
+    }
+};
+
+template <bool COUNT>
+__device__ bool trace(const SceneGPU &sc, const f3 &o, const f3 &d, Hit &hit, Stack &stk, LaneCount &cnt) {
+    RayP wr; wr.o = o; wr.d = d; prep(wr);
+    RayP lr = wr;
+    float tmax = __builtin_huge_valf();
+    bool found = false;
+    float te;
+    stk.sp = 0;
+    if (!slab(sc.tlas_root_box, wr, TMIN, tmax, te)) return false;     // root pop test (TLAS.cu:150)
+    uint32_t cur = sc.tlas_root_ref;
+    uint32_t cur_inst = 0;
+    for (;;) {
+        if (!(cur & REF_LEAF)) {
+            // interior node pair: test both children (TLAS.cu:175-197 / BLAS.cu:178-202)
+            const bool blas = (cur & REF_BLAS) != 0;
+            const NodePair *P = (blas ? sc.blas_pairs : sc.tlas_pairs) + (cur & REF_INDEX_MASK);
+            const float4 *P4 = reinterpret_cast<const float4 *>(P);
+            const float4 A = P4[0], B = P4[1], Cc = P4[2];
+            const uint4 D = reinterpret_cast<const uint4 *>(P)[3];
+            const float b0[6] = {A.x, A.y, A.z, A.w, B.x, B.y};
+            const float b1[6] = {B.z, B.w, Cc.x, Cc.y, Cc.z, Cc.w};
+            if (COUNT) cnt.pairs++;
+            float e0 = 0.0f, e1 = 0.0f;
+            const RayP &r = blas ? lr : wr;
+            const bool h0 = slab(b0, r, TMIN, tmax, e0);
+            const bool h1 = slab(b1, r, TMIN, tmax, e1);
+            if (h0 && h1) {
+                // reference: tLeft > tRight -> push left then right (right popped first)
+                const bool right_near = e0 > e1;
+                stk.push(right_near ? D.x : D.y, right_near ? e0 : e1, cnt);
+                cur = right_near ? D.y : D.x;
+                continue;
+            }
+            if (h0) { cur = D.x; continue; }
+            if (h1) { cur = D.y; continue; }
+        } else if (!(cur & REF_BLAS)) {
+            // TLAS leaf: its instances in order (TLAS.cu:157-173)
+            const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur);
+            if (count > 1) stk.push(make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
+            cur_inst = sc.tlas_slots[start];
+            const InstHot &I = sc.inst_hot[cur_inst];
+            if (COUNT) cnt.inst++;
+            // Instance::hit: ray into local space, d' not renormalised (Instance.cu:26-27)
+            lr.o = xf_point(I.inv, wr.o);
+            lr.d = xf_vector(I.inv, wr.d);
+            prep(lr);
+            if (slab(I.root_box, lr, TMIN, tmax, te)) { cur = I.root_ref; continue; }   // BLAS root pop test
+        } else {
+            // BLAS leaf: primitives in leaf order (BLAS.cu:153-176)
+            const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur), type = ref_leaf_type(cur);
+            for (uint32_t k = 0; k < count; k++) {
+                const uint32_t slot = start + k;
+                float t = 0.0f, u = 0.0f, v = 0.0f;
+                bool h;
+                if (type == RT_PRIM_TRIANGLE) {
+                    if (COUNT) cnt.tri++;
+                    h = tri_test(sc.tri_hot[slot], lr, TMIN, tmax, t, u, v);
+                } else if (type == RT_PRIM_SPHERE) {
+                    if (COUNT) cnt.sq++;
+                    h = sphere_test(sc.sph_hot[slot], lr, TMIN, tmax, t);
+                } else {
+                    if (COUNT) { cnt.sq++; cnt.quad++; }
+                    h = quad_test(sc.quad_hot[slot], lr, TMIN, tmax, t, u, v);
+                }
+                if (h) {
+                    found = true; tmax = t;
+                    hit.t = t; hit.inst = cur_inst; hit.ptype = type; hit.slot = slot; hit.u = u; hit.v = v;
+                }
+            }
+        }
+        // pop until an entry survives the re-test (entry t < tmax)
+        bool got = false;
+        while (stk.sp > 0) {
+            const uint2 e = stk.pop();
+            if (__uint_as_float(e.y) < tmax) { cur = e.x; got = true; break; }
+        }
+        if (!got) break;
+    }
+    return found;
+}
+
+// Record fields the shading needs (HitRecord, BasicTypes.cuh:19-31), world space.
+struct Surface { f3 p, n; uint32_t material; uint32_t orig; };
+
+// Recompute the hit point / normal of the closest hit exactly as the primitive hit function and
+// Instance::hit (Instance.cu:41-45) would have stored them.
+__device__ __forceinline__ Surface finalize(const SceneGPU &sc, const f3 &wo, const f3 &wd, const Hit &h) {
+    const InstHot &I = sc.inst_hot[h.inst];
+    const InstCold &IC = sc.inst_cold[h.inst];
+    const f3 lo = xf_point(I.inv, wo), ld = xf_vector(I.inv, wd);
+    const f3 p = add(lo, scl(ld, h.t));                                        // Ray::at (Ray.cuh:18-20)
+    f3 n;
+    Surface s;
+    if (h.ptype == RT_PRIM_TRIANGLE) {                                         // Triangle.cu:40-42
+        const TriCold &T = sc.tri_cold[h.slot];
+        const f3 nn = unit(add(add(scl(ld3(T.n0), (1.0f - h.u) - h.v), scl(ld3(T.n1), h.u)), scl(ld3(T.n2), h.v)));
+        n = dot(ld, nn) < 0.0f ? nn : neg(nn);
+        s.material = T.material; s.orig = T.orig_index;
+    } else if (h.ptype == RT_PRIM_SPHERE) {                                    // Sphere.cu:37-39
+        const SphereHot &S = sc.sph_hot[h.slot];
+        const f3 outward = unit(sub(p, ld3(S.center)));
+        n = dot(ld, outward) < 0.0f ? outward : neg(outward);
+        s.material = sc.sph_cold[h.slot].material; s.orig = sc.sph_cold[h.slot].orig_index;
+    } else {                                                                   // Parallelogram.cu:42-43
+        const QuadHot &Q = sc.quad_hot[h.slot];
+        const f3 qn = ld3(Q.n);
+        n = dot(ld, qn) < 0.0f ? qn : neg(qn);
+        s.material = sc.quad_cold[h.slot].material; s.orig = sc.quad_cold[h.slot].orig_index;
+    }
+    s.p = xf_point(IC.fwd, p);
+    s.n = unit(xf_vector(IC.nrm, n));
+    return s;
+}
+
+template <bool COUNT>
+__device__ f3 ray_color(const SceneGPU &sc, const CameraGPU &cam, f3 o, f3 d, Rng &rng, Stack &stk,
+                        LaneCount &cnt, uint32_t &rays) {                      // Kernel.cu:6-103
+    f3 result = mk(1.0f, 1.0f, 1.0f);
+    for (uint32_t depth = 0; depth < cam.depth; depth++) {
+        Hit h;
+        rays++;
+        if (trace<COUNT>(sc, o, d, h, stk, cnt)) {
+            if (COUNT) cnt.hits++;
+            const Surface s = finalize(sc, o, d, h);
+            const float4 m = reinterpret_cast<const float4 *>(sc.materials)[s.material & ~MAT_METAL_BIT];
+            const f3 albedo = mk(m.x, m.y, m.z);
+            f3 out;
+            if (!(s.material & MAT_METAL_BIT)) {                               // Rough.cuh:14-29
+                out = add(s.n, random_space_vector(rng));
+                if (f_eq(dot(out, out), FZERO * FZERO)) out = s.n;
+            } else {                                                           // Metal.cuh:15-32
+                out = unit(sub(d, scl(s.n, 2.0f * dot(d, s.n))));
+                if (m.w > 0.0f) out = add(out, scl(random_space_vector(rng), m.w));
+                if (!(dot(out, s.n) > 0.0f)) return result;                    // absorbed: throughput (Kernel.cu:85-87)
+            }
+            o = s.p; d = out;
+            result = mul(result, albedo);
+        } else {
+            result = mul(result, ld3(cam.background));
+            break;
+        }
+    }
+    return result;
+}
+
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void render_kernel(SceneGPU sc, CameraGPU cam, OutputGPU out,
+                                                       unsigned long long *counters) {
+    __shared__ uint2 lds_stack[LDS_DEPTH][BLOCK];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t wunit = blockIdx.x * (BLOCK / 64) + (tid >> 6);
+    if (wunit >= out.units) return;                       // wave-uniform
+
+    // 8x8 pixel unit -> pixel + output index
+    uint32_t px, py, oi;
+    if (out.tile_count == 0) {
+        const uint32_t ux = wunit % out.units_x, uy = wunit / out.units_x;
+        px = ux * 8 + (lane & 7); py = uy * 8 + (lane >> 3);
+        oi = py * cam.width + px;
+    } else {
+        const uint32_t upr = out.tile_w / 8, upt = upr * (out.tile_h / 8);
+        const uint32_t k = wunit / upt, r = wunit % upt;
+        const uint32_t t = out.tile_rank + k * out.tile_count;
+        const uint32_t lx = (r % upr) * 8 + (lane & 7), ly = (r / upr) * 8 + (lane >> 3);
+        px = (t % out.tiles_x) * out.tile_w + lx;
+        py = (t / out.tiles_x) * out.tile_h + ly;
+        oi = k * out.tile_w * out.tile_h + ly * out.tile_w + lx;
+    }
+    const bool valid = px < cam.width && py < cam.height;
+
+    Stack stk;
+    stk.lds = lds_stack;
+    stk.tid = tid;
+    stk.sp = 0;
+    LaneCount cnt = {0, 0, 0, 0, 0, 0, 0};
+    uint32_t rays = 0;
+
+    if (valid) {
+        const uint32_t pixel = cam.pitch * py + px;                            // Kernel.cu:109
+        Rng rng;
+        rng.init((uint64_t)pixel ^ cam.frame_seed, pixel);                      // Kernel.cu:114
+        f3 result = mk(0.0f, 0.0f, 0.0f);
+        const f3 po = ld3(cam.pixel_origin), dx = ld3(cam.dx), dy = ld3(cam.dy), cc = ld3(cam.center);
+        for (uint32_t si = 0; si < cam.sqrt_s; si++) {
+            for (uint32_t sj = 0; sj < cam.sqrt_s; sj++) {                      // Kernel.cu:119-139
+                const float ox = (((float)sj + rng.uniform()) * cam.recip_sqrt) - 0.5f;
+                const float oy = (((float)si + rng.uniform()) * cam.recip_sqrt) - 0.5f;
+                const f3 sp = add(add(po, scl(dx, (float)px + ox)), scl(dy, (float)py + oy));
+                f3 origin = cc;
+                if (cam.focus_radius > 0.0f) {
+                    const f3 dv = random_plane_vector(rng, cam.focus_radius);
+                    origin = add(add(cc, scl(ld3(cam.cu), dv.x)), scl(ld3(cam.cv), dv.y));
+                }
+                const f3 dir = unit(sub(sp, origin));
+                result = add(result, ray_color<COUNT>(sc, cam, origin, dir, rng, stk, cnt, rays));
+            }
+        }
+        result = scl(result, cam.recip_sqrt * cam.recip_sqrt);                  // Kernel.cu:143
+        if (out.rgb) {
+            out.rgb[3 * (size_t)oi + 0] = result.x;
+            out.rgb[3 * (size_t)oi + 1] = result.y;
+            out.rgb[3 * (size_t)oi + 2] = result.z;
+        }
+        // Color3::castToUchar4, gamma 2 (Color3.cuh:99-114)
+        const float cr = fminf(fmaxf(sqrtf(result.x), 0.0f), 0.999f);
+        const float cg = fminf(fmaxf(sqrtf(result.y), 0.0f), 0.999f);
+        const float cb = fminf(fmaxf(sqrtf(result.z), 0.0f), 0.999f);
+        const uint32_t packed = (uint32_t)(uint8_t)(256.0f * cr) | ((uint32_t)(uint8_t)(256.0f * cg) << 8) |
+                                ((uint32_t)(uint8_t)(256.0f * cb) << 16) | (255u << 24);
+        reinterpret_cast<uint32_t *>(out.rgba)[oi] = packed;
+    }
+
+    // one atomic per wave per counter
+    const uint32_t wr = wave_sum(rays);
+    const uint32_t wp = wave_sum(valid ? 1u : 0u);
+    if (COUNT) {
+        const uint32_t a = wave_sum(cnt.pairs), b = wave_sum(cnt.tri), c = wave_sum(cnt.sq), d = wave_sum(cnt.inst),
+                       e = wave_sum(cnt.overflow), f = wave_sum(cnt.quad), g = wave_sum(cnt.hits);
+        if (lane == 0) {
+            atomicAdd(&counters[CNT_PAIRS], (unsigned long long)a);
+            atomicAdd(&counters[CNT_TRI], (unsigned long long)b);
+            atomicAdd(&counters[CNT_SPHQUAD], (unsigned long long)c);
+            atomicAdd(&counters[CNT_INST], (unsigned long long)d);
+            atomicAdd(&counters[CNT_OVERFLOW], (unsigned long long)e);
+            atomicAdd(&counters[CNT_QUAD], (unsigned long long)f);
+            atomicAdd(&counters[CNT_HITS], (unsigned long long)g);
+        }
+    }
+    if (lane == 0) {
+        atomicAdd(&counters[CNT_RAYS], (unsigned long long)wr);
+        atomicAdd(&counters[CNT_PIXELS], (unsigned long long)wp);
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const float *rays, uint32_t n, rt_hit *hits) {
+    __shared__ uint2 lds_stack[LDS_DEPTH][BLOCK];
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    Stack stk;
+    stk.lds = lds_stack;
+    stk.tid = threadIdx.x;
+    stk.sp = 0;
+    LaneCount cnt = {0, 0, 0, 0, 0, 0, 0};
+    const f3 o = mk(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
+    const f3 d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
+    Hit h;
+    rt_hit r;
+    if (trace<false>(sc, o, d, h, stk, cnt)) {
+        const Surface s = finalize(sc, o, d, h);
+        r.t = h.t; r.instance = h.inst; r.primitive_type = h.ptype; r.primitive_index = s.orig;
+        r.point.x = s.p.x; r.point.y = s.p.y; r.point.z = s.p.z;
+        r.normal.x = s.n.x; r.normal.y = s.n.y; r.normal.z = s.n.z;
+        r.material_type = (s.material & MAT_METAL_BIT) ? RT_MAT_METAL : RT_MAT_ROUGH;
+        r.material_index = s.material & ~MAT_METAL_BIT;
+    } else {
+        r.t = __builtin_huge_valf(); r.instance = 0xFFFFFFFFu; r.primitive_type = 0; r.primitive_index = 0;
+        r.point.x = r.point.y = r.point.z = 0.0f; r.normal.x = r.normal.y = r.normal.z = 0.0f;
+        r.material_type = 0; r.material_index = 0;
+    }
+    hits[i] = r;
+}
+
+}  // namespace dev
+
+hipError_t RT_SUFFIX(launch_render)(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
+                                    unsigned long long *counters, hipStream_t stream) {
+    using namespace RT_SUFFIX(dev);
+    const uint32_t waves_per_block = BLOCK / 64;
+    const dim3 grid((out.units + waves_per_block - 1) / waves_per_block);
+    if (grid.x == 0) return hipSuccess;
+    if (count) hipLaunchKernelGGL(render_kernel<true>, grid, dim3(BLOCK), 0, stream, sc, cam, out, counters);
+    else hipLaunchKernelGGL(render_kernel<false>, grid, dim3(BLOCK), 0, stream, sc, cam, out, counters);
+    return hipGetLastError();
+}
+
+hipError_t RT_SUFFIX(launch_trace_rays)(const SceneGPU &sc, const float *rays, uint32_t n, rt_hit *hits,
+                                        hipStream_t stream) {
+    using namespace RT_SUFFIX(dev);
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(trace_rays_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, stream, sc, rays, n, hits);
+    return hipGetLastError();
+}
+
+}  // namespace rtamd

@@ -1,0 +1,146 @@
+"""Python mirror of the reference's host `Renderer` (include/Global/Renderer.cuh:109-146) over
+the C ABI of librtamd.so.  Method names follow the reference lifecycle:
+
+    commitGeometryData + commitMaterialData + configureInstances -> Renderer(scene)
+    buildAccelerationStructure                                   -> build_acceleration_structure()
+    configureCamera                                              -> configure_camera()
+    one iteration of startRender                                 -> render(frame)
+    cleanup                                                      -> cleanup()
+
+There is no CPU fallback: constructing a Renderer without librtamd.so or without a GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi
+
+
+class Renderer:
+    def __init__(self, scene, device: int = 0, update=None):
+        """update: None -> the scene's own animation (Main.cu updateInstance via the native
+        rt_demo_update when scene.animated), False -> static, or a Python callable
+        f(xforms: ctypes array of Xform, n, frame) (slow path, crosses into Python per frame)."""
+        self.lib = abi.load_library()
+        self.scene = scene
+        self._cb = None
+        if update is None:
+            fn = C.cast(self.lib.rt_demo_update, C.c_void_p) if scene.animated else None
+        elif update is False:
+            fn = None
+        else:
+            self._cb = abi.UPDATE_FN(lambda user, xs, n, frame: update(xs, n, frame))
+            fn = C.cast(self._cb, C.c_void_p)
+        self._desc = scene.desc(fn)
+        h = C.c_void_p()
+        abi.check(self.lib, self.lib.rt_scene_create(C.byref(self._desc), device, C.byref(h)))
+        self.h = h
+        self.device = device
+        self.width = self.height = 0
+
+    # ---- lifecycle ---------------------------------------------------------------------
+    def build_acceleration_structure(self, seed: int = 0):
+        abi.check(self.lib, self.lib.rt_scene_build(self.h, abi.RT_BUILD_COMPAT_MEDIAN, seed))
+        return self
+
+    def configure_camera(self, width: int, height: int, **camera):
+        ci = self.scene.camera_input(**camera)
+        abi.check(self.lib, self.lib.rt_camera_set(self.h, C.byref(ci), width, height))
+        self.width, self.height = width, height
+        return self
+
+    def update(self, frame: int):
+        abi.check(self.lib, self.lib.rt_scene_update(self.h, frame))
+
+    def render(self, frame: int = 0, frame_seed: int = 0x5EED, exact: bool = False, count_work: bool = False,
+               want_rgb: bool = False, want_rgba: bool = True, skip_update: bool = False,
+               tiles=None, rgba8_device=None, rgb32_device=None, stream=None, sync: bool = True):
+        """One frame.  Returns (rgba[H,W,4] uint8 | None, rgb[H,W,3] float32 | None, stats dict).
+        tiles = (tile_w, tile_h, rank, count) renders a tile shard into tile-compact outputs."""
+        o = abi.RenderOpts()
+        o.frame_seed = frame_seed
+        o.flags = (abi.RT_RENDER_EXACT if exact else 0) | (abi.RT_RENDER_COUNT_WORK if count_work else 0) | \
+                  (abi.RT_RENDER_SKIP_UPDATE if skip_update else 0) | (0 if sync else abi.RT_RENDER_NO_SYNC)
+        if tiles is not None:
+            o.tile_w, o.tile_h, o.tile_rank, o.tile_count = tiles
+            npix = self.tiles_for_rank(*tiles) * tiles[0] * tiles[1]
+            shape = (npix,)
+        else:
+            shape = (self.height, self.width)
+        o.rgba8_device = rgba8_device
+        o.rgb32_device = rgb32_device
+        o.stream = stream
+        rgba = np.zeros(shape + (4,), np.uint8) if (want_rgba and sync) else None
+        rgb = np.zeros(shape + (3,), np.float32) if (want_rgb and sync) else None
+        st = abi.Stats()
+        abi.check(self.lib, self.lib.rt_render(self.h, frame, C.byref(o),
+                                               rgba.ctypes.data if rgba is not None else None,
+                                               rgb.ctypes.data if rgb is not None else None, C.byref(st)))
+        stats = {k: getattr(st, k) for k, _ in abi.Stats._fields_}
+        return rgba, rgb, stats
+
+    def tiles_for_rank(self, tile_w, tile_h, rank, count):
+        return int(self.lib.rt_tiles_for_rank(self.h, tile_w, tile_h, rank, count))
+
+    def assemble_tiles(self, gathered_device, slab_tiles, tile_w, tile_h, tile_count, frame_device, stream=None):
+        abi.check(self.lib, self.lib.rt_assemble_tiles(self.h, gathered_device, slab_tiles, tile_w, tile_h,
+                                                       tile_count, frame_device, stream))
+
+    def trace_rays(self, rays, exact: bool = False):
+        rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+        n = rays.shape[0]
+        hits = (abi.Hit * max(1, n))()
+        abi.check(self.lib, self.lib.rt_trace_rays(self.h, rays.ctypes.data, n,
+                                                   abi.RT_RENDER_EXACT if exact else 0, hits))
+        out = np.zeros(n, dtype=[("t", np.float32), ("instance", np.uint32), ("ptype", np.uint32),
+                                 ("pindex", np.uint32), ("point", np.float32, 3), ("normal", np.float32, 3),
+                                 ("mtype", np.uint32), ("midx", np.uint32)])
+        out[:] = np.frombuffer(hits, dtype=out.dtype, count=n)
+        return out
+
+    def synchronize(self):
+        abi.check(self.lib, self.lib.rt_synchronize(self.h))
+
+    def info(self):
+        i = abi.SceneInfo()
+        abi.check(self.lib, self.lib.rt_scene_get_info(self.h, C.byref(i)))
+        return {k: getattr(i, k) for k, _ in abi.SceneInfo._fields_}
+
+    def export_blas(self, b: int):
+        nn, npr = C.c_uint32(), C.c_uint32()
+        abi.check(self.lib, self.lib.rt_scene_export_blas(self.h, b, None, None, None, C.byref(nn), C.byref(npr)))
+        boxes = np.zeros((nn.value, 6), np.float32)
+        ci = np.zeros((nn.value, 2), np.uint32)
+        refs = np.zeros(npr.value, np.uint32)
+        abi.check(self.lib, self.lib.rt_scene_export_blas(self.h, b, boxes.ctypes.data, ci.ctypes.data,
+                                                          refs.ctypes.data, C.byref(nn), C.byref(npr)))
+        return boxes, ci, refs
+
+    def export_tlas(self):
+        nn, npr = C.c_uint32(), C.c_uint32()
+        abi.check(self.lib, self.lib.rt_scene_export_tlas(self.h, None, None, None, C.byref(nn), C.byref(npr)))
+        boxes = np.zeros((nn.value, 6), np.float32)
+        ci = np.zeros((nn.value, 2), np.uint32)
+        refs = np.zeros(npr.value, np.uint32)
+        abi.check(self.lib, self.lib.rt_scene_export_tlas(self.h, boxes.ctypes.data, ci.ctypes.data,
+                                                          refs.ctypes.data, C.byref(nn), C.byref(npr)))
+        return boxes, ci, refs
+
+    def cleanup(self):
+        if getattr(self, "h", None):
+            self.lib.rt_scene_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.cleanup()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.cleanup()

@@ -1,0 +1,47 @@
+"""Test configuration: paths, the `gpu` marker, and build fixtures.
+
+`-m "not gpu"` tests run on CPU (oracle, host logic, ABI exports, gloo multi-process).
+`-m gpu` tests run the HIP path through the C ABI and compare it with the oracle.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "real-time-gpu-ray-tracer_amd")
+for p in (REPO, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through librtamd.so)")
+
+
+@pytest.fixture(scope="session")
+def oracle_lib():
+    from oracle import oracle
+    oracle.build()
+    return oracle
+
+
+@pytest.fixture(scope="session")
+def rtlib_path():
+    """Path of librtamd.so, building it if missing (hipcc cross-compiles without a GPU)."""
+    from rtamd import abi
+    if not os.path.exists(abi.LIB_PATH):
+        subprocess.run(["make", "-s", "-j4", "-C", os.path.join(PKG, "csrc")], check=True)
+    return abi.LIB_PATH
+
+
+@pytest.fixture(scope="session")
+def gpu_lib(rtlib_path):
+    """librtamd.so on a GPU box; fails loudly (never skips to a fallback) if no device is visible."""
+    import torch  # noqa: F401  (load torch's HIP runtime first so both share one runtime)
+    from rtamd import abi
+    lib = abi.load_library()
+    n = lib.rt_device_count()
+    assert n > 0, "gpu test collected but no HIP device is visible"
+    return lib
