@@ -103,6 +103,7 @@ struct SceneGPU {
     float tlas_root_box[6];
     uint32_t tlas_root_ref;
     uint32_t instance_count;
+    uint32_t rough_count;           // material slot of metal m = rough_count + m
 };
 
 struct CameraGPU {                  // Camera (RendererImpl.cuh:32-61), precomputed on host

@@ -246,6 +246,7 @@ SceneGPU scene_gpu(const rt_scene *s) {
     std::memcpy(g.tlas_root_box, s->tlas_root_box, sizeof g.tlas_root_box);
     g.tlas_root_ref = s->tlas_root_ref;
     g.instance_count = (uint32_t)s->inst.size();
+    g.rough_count = (uint32_t)s->roughs.size();
     return g;
 }
 

@@ -265,32 +265,61 @@ struct Hit {
 
 struct LaneCount { uint32_t pairs, tri, sq, quad, inst, hits, overflow; };
 
+// Per-lane traversal stack: a window of LDS_DEPTH entries in LDS (layout [depth][BLOCK]: a wave's
+// 64 lanes touch 64 consecutive uint2 at any depth -> bank-conflict-free ds_*_b64) backed by a
+// scratch array.  Push/pop only touch LDS; when the window fills, its bottom half is paged out to
+// scratch, and when it empties the most recent half-page is paged back in (rare: median-split
+// trees stay within 16 entries up to ~1k instances x 1k triangles).  Capacity LDS_DEPTH +
+// SPILL_DEPTH = 64 entries, the reference's stack size (BLAS.cu:129, TLAS.cu:138).
+typedef __attribute__((address_space(3))) uint2 LdsU2;
+constexpr int HALF = LDS_DEPTH / 2;
+
 struct Stack {
-    uint2 (*lds)[BLOCK];   // [LDS_DEPTH][BLOCK]
-    uint2 spill[SPILL_DEPTH];
-    int sp;
-    int tid;
-    __device__ __forceinline__ void push(uint32_t ref, float tn, LaneCount &c) {
-        const uint2 e = make_uint2(ref, __float_as_uint(tn));
-        if (sp < LDS_DEPTH) lds[sp][tid] = e;
-        else if (sp < LDS_DEPTH + SPILL_DEPTH) spill[sp - LDS_DEPTH] = e;
-        else { c.overflow++; return; }       // the reference's 64-entry stack would overflow here
-        sp++;
-    }
-    __device__ __forceinline__ uint2 pop() {
-        --sp;
-        return sp < LDS_DEPTH ? lds[sp][tid] : spill[sp - LDS_DEPTH];
-    }
+    LdsU2 *lds;            // &lds_stack[0][tid]; entry k at lds[k * BLOCK]
+    int sp;                // entries in the LDS window
+    int spilled;           // entries paged out to scratch
+    __device__ __forceinline__ bool empty() const { return sp == 0 && spilled == 0; }
 };
+
+__device__ __forceinline__ void stack_page_out(Stack &stk, uint2 *spill, LaneCount &c) {
+    if (stk.spilled + HALF > SPILL_DEPTH) {        // deeper than the reference's 64 entries
+        c.overflow++;
+        stk.spilled = SPILL_DEPTH - HALF;          // drop the oldest half-page (result flagged)
+    }
+#pragma unroll
+    for (int k = 0; k < HALF; k++) spill[stk.spilled + k] = stk.lds[k * BLOCK];
+#pragma unroll
+    for (int k = 0; k < HALF; k++) stk.lds[k * BLOCK] = stk.lds[(k + HALF) * BLOCK];
+    stk.sp = HALF;
+    stk.spilled += HALF;
+}
+__device__ __forceinline__ void stack_page_in(Stack &stk, const uint2 *spill) {
+    stk.spilled -= HALF;
+#pragma unroll
+    for (int k = 0; k < HALF; k++) stk.lds[k * BLOCK] = spill[stk.spilled + k];
+    stk.sp = HALF;
+}
+__device__ __forceinline__ void stack_push(Stack &stk, uint2 *spill, uint32_t ref, float tn, LaneCount &c) {
+    if (stk.sp == LDS_DEPTH) stack_page_out(stk, spill, c);
+    stk.lds[stk.sp * BLOCK] = make_uint2(ref, __float_as_uint(tn));
+    stk.sp++;
+}
+__device__ __forceinline__ uint2 stack_pop(Stack &stk, const uint2 *spill) {   // precondition: !empty()
+    if (stk.sp == 0) stack_page_in(stk, spill);
+    --stk.sp;
+    return stk.lds[stk.sp * BLOCK];
+}
 
 template <bool COUNT>
 __device__ bool trace(const SceneGPU &sc, const f3 &o, const f3 &d, Hit &hit, Stack &stk, LaneCount &cnt) {
+    uint2 spill[SPILL_DEPTH];
     RayP wr; wr.o = o; wr.d = d; prep(wr);
     RayP lr = wr;
     float tmax = __builtin_huge_valf();
     bool found = false;
     float te;
     stk.sp = 0;
+    stk.spilled = 0;
     if (!slab(sc.tlas_root_box, wr, TMIN, tmax, te)) return false;     // root pop test (TLAS.cu:150)
     uint32_t cur = sc.tlas_root_ref;
     uint32_t cur_inst = 0;
@@ -312,7 +341,7 @@ __device__ bool trace(const SceneGPU &sc, const f3 &o, const f3 &d, Hit &hit, St
             if (h0 && h1) {
                 // reference: tLeft > tRight -> push left then right (right popped first)
                 const bool right_near = e0 > e1;
-                stk.push(right_near ? D.x : D.y, right_near ? e0 : e1, cnt);
+                stack_push(stk, spill, right_near ? D.x : D.y, right_near ? e0 : e1, cnt);
                 cur = right_near ? D.y : D.x;
                 continue;
             }
@@ -321,7 +350,7 @@ __device__ bool trace(const SceneGPU &sc, const f3 &o, const f3 &d, Hit &hit, St
         } else if (!(cur & REF_BLAS)) {
             // TLAS leaf: its instances in order (TLAS.cu:157-173)
             const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur);
-            if (count > 1) stk.push(make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
+            if (count > 1) stack_push(stk, spill, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
             cur_inst = sc.tlas_slots[start];
             const InstHot &I = sc.inst_hot[cur_inst];
             if (COUNT) cnt.inst++;
@@ -355,8 +384,8 @@ __device__ bool trace(const SceneGPU &sc, const f3 &o, const f3 &d, Hit &hit, St
         }
         // pop until an entry survives the re-test (entry t < tmax)
         bool got = false;
-        while (stk.sp > 0) {
-            const uint2 e = stk.pop();
+        while (!stk.empty()) {
+            const uint2 e = stack_pop(stk, spill);
             if (__uint_as_float(e.y) < tmax) { cur = e.x; got = true; break; }
         }
         if (!got) break;
@@ -461,9 +490,9 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(SceneGPU sc, CameraGPU ca
     const bool valid = px < cam.width && py < cam.height;
 
     Stack stk;
-    stk.lds = lds_stack;
-    stk.tid = tid;
+    stk.lds = (LdsU2 *)&lds_stack[0][tid];
     stk.sp = 0;
+    stk.spilled = 0;
     LaneCount cnt = {0, 0, 0, 0, 0, 0, 0};
     uint32_t rays = 0;
 
@@ -529,9 +558,9 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const fl
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     Stack stk;
-    stk.lds = lds_stack;
-    stk.tid = threadIdx.x;
+    stk.lds = (LdsU2 *)&lds_stack[0][threadIdx.x];
     stk.sp = 0;
+    stk.spilled = 0;
     LaneCount cnt = {0, 0, 0, 0, 0, 0, 0};
     const f3 o = mk(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
     const f3 d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
@@ -542,8 +571,9 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const fl
         r.t = h.t; r.instance = h.inst; r.primitive_type = h.ptype; r.primitive_index = s.orig;
         r.point.x = s.p.x; r.point.y = s.p.y; r.point.z = s.p.z;
         r.normal.x = s.n.x; r.normal.y = s.n.y; r.normal.z = s.n.z;
-        r.material_type = (s.material & MAT_METAL_BIT) ? RT_MAT_METAL : RT_MAT_ROUGH;
-        r.material_index = s.material & ~MAT_METAL_BIT;
+        const bool metal = (s.material & MAT_METAL_BIT) != 0;
+        r.material_type = metal ? RT_MAT_METAL : RT_MAT_ROUGH;
+        r.material_index = (s.material & ~MAT_METAL_BIT) - (metal ? sc.rough_count : 0u);
     } else {
         r.t = __builtin_huge_valf(); r.instance = 0xFFFFFFFFu; r.primitive_type = 0; r.primitive_index = 0;
         r.point.x = r.point.y = r.point.z = 0.0f; r.normal.x = r.normal.y = r.normal.z = 0.0f;
