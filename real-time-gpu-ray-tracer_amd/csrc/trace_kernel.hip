@@ -266,12 +266,16 @@ struct Hit {
 struct LaneCount { uint32_t pairs, tri, sq, quad, inst, hits, overflow; };
 
 // Per-lane traversal stack: a window of LDS_DEPTH entries in LDS (layout [depth][BLOCK]: a wave's
-// 64 lanes touch 64 consecutive uint2 at any depth -> bank-conflict-free ds_*_b64) backed by a
+// 64 lanes touch 64 consecutive u64 at any depth -> bank-conflict-free ds_*_b64) backed by a
 // scratch array.  Push/pop only touch LDS; when the window fills, its bottom half is paged out to
 // scratch, and when it empties the most recent half-page is paged back in (rare: median-split
 // trees stay within 16 entries up to ~1k instances x 1k triangles).  Capacity LDS_DEPTH +
 // SPILL_DEPTH = 64 entries, the reference's stack size (BLAS.cu:129, TLAS.cu:138).
-typedef __attribute__((address_space(3))) uint2 LdsU2;
+struct SEnt { uint32_t ref; uint32_t tn; };   // node ref, entry t (float bits)
+// LDS entries are stored packed as u64 (low = ref, high = entry t bits)
+typedef __attribute__((address_space(3))) unsigned long long LdsU2;
+__device__ __forceinline__ unsigned long long pack(SEnt e) { return (unsigned long long)e.ref | ((unsigned long long)e.tn << 32); }
+__device__ __forceinline__ SEnt unpack(unsigned long long v) { SEnt e; e.ref = (uint32_t)v; e.tn = (uint32_t)(v >> 32); return e; }
 constexpr int HALF = LDS_DEPTH / 2;
 
 struct Stack {
@@ -281,38 +285,41 @@ struct Stack {
     __device__ __forceinline__ bool empty() const { return sp == 0 && spilled == 0; }
 };
 
-__device__ __forceinline__ void stack_page_out(Stack &stk, uint2 *spill, LaneCount &c) {
+__device__ __forceinline__ void stack_page_out(Stack &stk, SEnt *spill, LaneCount &c) {
     if (stk.spilled + HALF > SPILL_DEPTH) {        // deeper than the reference's 64 entries
         c.overflow++;
         stk.spilled = SPILL_DEPTH - HALF;          // drop the oldest half-page (result flagged)
     }
 #pragma unroll
-    for (int k = 0; k < HALF; k++) spill[stk.spilled + k] = stk.lds[k * BLOCK];
+    for (int k = 0; k < HALF; k++) spill[stk.spilled + k] = unpack(stk.lds[k * BLOCK]);
 #pragma unroll
     for (int k = 0; k < HALF; k++) stk.lds[k * BLOCK] = stk.lds[(k + HALF) * BLOCK];
     stk.sp = HALF;
     stk.spilled += HALF;
 }
-__device__ __forceinline__ void stack_page_in(Stack &stk, const uint2 *spill) {
+__device__ __forceinline__ void stack_page_in(Stack &stk, const SEnt *spill) {
     stk.spilled -= HALF;
 #pragma unroll
-    for (int k = 0; k < HALF; k++) stk.lds[k * BLOCK] = spill[stk.spilled + k];
+    for (int k = 0; k < HALF; k++) stk.lds[k * BLOCK] = pack(spill[stk.spilled + k]);
     stk.sp = HALF;
 }
-__device__ __forceinline__ void stack_push(Stack &stk, uint2 *spill, uint32_t ref, float tn, LaneCount &c) {
+__device__ __forceinline__ void stack_push(Stack &stk, SEnt *spill, uint32_t ref, float tn, LaneCount &c) {
     if (stk.sp == LDS_DEPTH) stack_page_out(stk, spill, c);
-    stk.lds[stk.sp * BLOCK] = make_uint2(ref, __float_as_uint(tn));
+    SEnt e;
+    e.ref = ref;
+    e.tn = __float_as_uint(tn);
+    stk.lds[stk.sp * BLOCK] = pack(e);
     stk.sp++;
 }
-__device__ __forceinline__ uint2 stack_pop(Stack &stk, const uint2 *spill) {   // precondition: !empty()
+__device__ __forceinline__ SEnt stack_pop(Stack &stk, const SEnt *spill) {   // precondition: !empty()
     if (stk.sp == 0) stack_page_in(stk, spill);
     --stk.sp;
-    return stk.lds[stk.sp * BLOCK];
+    return unpack(stk.lds[stk.sp * BLOCK]);
 }
 
 template <bool COUNT>
 __device__ bool trace(const SceneGPU &sc, const f3 &o, const f3 &d, Hit &hit, Stack &stk, LaneCount &cnt) {
-    uint2 spill[SPILL_DEPTH];
+    SEnt spill[SPILL_DEPTH];
     RayP wr; wr.o = o; wr.d = d; prep(wr);
     RayP lr = wr;
     float tmax = __builtin_huge_valf();
@@ -385,8 +392,8 @@ __device__ bool trace(const SceneGPU &sc, const f3 &o, const f3 &d, Hit &hit, St
         // pop until an entry survives the re-test (entry t < tmax)
         bool got = false;
         while (!stk.empty()) {
-            const uint2 e = stack_pop(stk, spill);
-            if (__uint_as_float(e.y) < tmax) { cur = e.x; got = true; break; }
+            const SEnt e = stack_pop(stk, spill);
+            if (__uint_as_float(e.tn) < tmax) { cur = e.ref; got = true; break; }
         }
         if (!got) break;
     }
@@ -466,7 +473,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v) {
 template <bool COUNT>
 __global__ __launch_bounds__(BLOCK) void render_kernel(SceneGPU sc, CameraGPU cam, OutputGPU out,
                                                        unsigned long long *counters) {
-    __shared__ uint2 lds_stack[LDS_DEPTH][BLOCK];
+    __shared__ unsigned long long lds_stack[LDS_DEPTH][BLOCK];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const uint32_t wunit = blockIdx.x * (BLOCK / 64) + (tid >> 6);
@@ -554,7 +561,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(SceneGPU sc, CameraGPU ca
 }
 
 __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const float *rays, uint32_t n, rt_hit *hits) {
-    __shared__ uint2 lds_stack[LDS_DEPTH][BLOCK];
+    __shared__ unsigned long long lds_stack[LDS_DEPTH][BLOCK];
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
     Stack stk;
