@@ -1,0 +1,80 @@
+"""World-size-2 gloo test of the multi-GPU frame protocol on CPU.
+
+Each rank renders only its interleaved screen tiles (here with the oracle, per tile region),
+packs them into a padded tile-compact slab, the slabs are gathered to rank 0 exactly as
+bench.py does with RCCL, and rank 0 assembles the frame.  The result must be byte-identical to
+a single-rank full-frame render: the RNG is keyed by the global padded pixel index.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from rtamd import scenes, tiles
+
+W, H, TW, TH = 200, 120, 64, 32
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _render_slab(o, rank, count):
+    st = tiles.slab_tiles(W, H, TW, TH, count)
+    slab = np.zeros((st * TW * TH, 4), np.uint8)
+    for k, t in enumerate(tiles.rank_tiles(W, H, TW, TH, rank, count)):
+        x0, y0 = tiles.tile_origin(t, W, TW, TH)
+        w, h = min(TW, W - x0), min(TH, H - y0)
+        _, rgba, _ = o.render(region=(x0, y0, w, h), threads=2, want_rgb=False)
+        tile = np.zeros((TH, TW, 4), np.uint8)
+        tile[:h, :w] = rgba
+        slab[k * TW * TH:(k + 1) * TW * TH] = tile.reshape(-1, 4)
+    return slab
+
+
+def _worker(rank, world, port, result_path):
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "real-time-gpu-ray-tracer_amd")]
+    from oracle.oracle import OracleScene
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    o = OracleScene(scenes.demo_with_particles(4), build_seed=2)
+    o.camera(W, H, ray_trace_depth=2)
+    o.update(5)
+    slab = torch.from_numpy(_render_slab(o, rank, world))
+    gather = [torch.zeros_like(slab) for _ in range(world)] if rank == 0 else None
+    dist.gather(slab, gather, dst=0)
+    if rank == 0:
+        g = torch.stack(gather).numpy()
+        frame = tiles.assemble(g, W, H, TW, TH, world)
+        _, full, _ = o.render(threads=2, want_rgb=False)
+        np.save(result_path, np.stack([frame, full]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_tile_gather_assemble_gloo(tmp_path, world):
+    out = str(tmp_path / "res.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    frame, full = np.load(out)
+    assert np.array_equal(frame, full)
+
+
+def test_tile_bookkeeping_covers_frame_once():
+    for count in (1, 2, 3, 8):
+        seen = np.zeros(tiles.tiles_xy(W, H, TW, TH), int).T.ravel()
+        for r in range(count):
+            for t in tiles.rank_tiles(W, H, TW, TH, r, count):
+                seen[t] += 1
+        assert (seen == 1).all()
+        assert sum(tiles.tiles_for_rank(W, H, TW, TH, r, count) for r in range(count)) == seen.size
