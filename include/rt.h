@@ -254,6 +254,12 @@ uint32_t rt_tiles_for_rank(const rt_scene *scene, uint32_t tile_w, uint32_t tile
 rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_count,
                         uint32_t flags, rt_hit *hits_host);
 
+/* Tuning knobs (defaults are the tuned values):
+ *   "kernel"    : 0 = one-thread-per-pixel grid kernel, 1 = persistent-wave megakernel (default)
+ *   "threshold" : persistent kernel — lanes that must be waiting before a wave leaves the
+ *                 traversal loop to shade / regenerate (1..64)                                  */
+rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
+
 /* Blocks until all work the scene enqueued has finished. */
 rt_status rt_synchronize(rt_scene *scene);
 

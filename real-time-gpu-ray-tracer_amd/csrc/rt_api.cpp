@@ -11,6 +11,7 @@
 
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -26,6 +27,12 @@ hipError_t launch_render_fast(const SceneGPU &, const CameraGPU &, const OutputG
 hipError_t launch_trace_rays_exact(const SceneGPU &, const float *, uint32_t, rt_hit *, hipStream_t);
 hipError_t launch_trace_rays_fast(const SceneGPU &, const float *, uint32_t, rt_hit *, hipStream_t);
 hipError_t launch_assemble(const void *, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, void *, hipStream_t);
+hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
+                                          uint32_t *, uint32_t, uint32_t, hipStream_t);
+hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
+                                         uint32_t *, uint32_t, uint32_t, hipStream_t);
+uint32_t persistent_blocks_per_cu_exact();
+uint32_t persistent_blocks_per_cu_fast();
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -121,6 +128,11 @@ struct rt_scene {
 
     hipStream_t stream = nullptr;
     hipEvent_t k_start = nullptr, k_stop = nullptr;
+    // persistent megakernel: work-queue head, grid size (#CUs x resident blocks), refill threshold
+    uint32_t *queue = nullptr;
+    uint32_t persist_blocks_exact = 0, persist_blocks_fast = 0;
+    uint32_t threshold = 16;
+    bool use_persistent = true;
     unsigned long long *counters = nullptr;       // HBM CNT_NUM
     unsigned long long *counters_host = nullptr;  // pinned
 
@@ -145,6 +157,7 @@ struct rt_scene {
             if (ev_used[b]) (void)hipEventDestroy(ev_used[b]);
         }
         if (counters) (void)hipFree(counters);
+        if (queue) (void)hipFree(queue);
         if (counters_host) (void)hipHostFree(counters_host);
         if (k_start) (void)hipEventDestroy(k_start);
         if (k_stop) (void)hipEventDestroy(k_stop);
@@ -452,6 +465,19 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     if (!s->k_start) HIP_TRY(hipEventCreate(&s->k_start));
     if (!s->k_stop) HIP_TRY(hipEventCreate(&s->k_stop));
     if (!s->counters) HIP_TRY(hipMalloc(&s->counters, CNT_NUM * sizeof(unsigned long long)));
+    if (!s->queue) HIP_TRY(hipMalloc(&s->queue, 16));
+    {
+        hipDeviceProp_t prop;
+        HIP_TRY(hipGetDeviceProperties(&prop, s->device));
+        const uint32_t cus = (uint32_t)prop.multiProcessorCount;
+        s->persist_blocks_exact = cus * persistent_blocks_per_cu_exact();
+        s->persist_blocks_fast = cus * persistent_blocks_per_cu_fast();
+        if (const char *k = std::getenv("RTAMD_KERNEL")) s->use_persistent = std::string(k) != "grid";
+        if (const char *t = std::getenv("RTAMD_THRESHOLD")) {
+            const long v = std::strtol(t, nullptr, 10);
+            if (v >= 1 && v <= 64) s->threshold = (uint32_t)v;
+        }
+    }
     if (!s->counters_host)
         HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->counters_host), CNT_NUM * sizeof(unsigned long long), hipHostMallocDefault));
     s->active = -1;
@@ -573,8 +599,14 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     HIP_TRY(hipStreamWaitEvent(stream, s->ev_copied[s->active], 0));
     HIP_TRY(hipMemsetAsync(s->counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
     HIP_TRY(hipEventRecord(s->k_start, stream));
-    HIP_TRY(exact ? launch_render_exact(g, cam, out, count, s->counters, stream)
-                  : launch_render_fast(g, cam, out, count, s->counters, stream));
+    if (s->use_persistent)
+        HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, s->counters, s->queue, s->persist_blocks_exact,
+                                                       s->threshold, stream)
+                      : launch_render_persistent_fast(g, cam, out, count, s->counters, s->queue, s->persist_blocks_fast,
+                                                      s->threshold, stream));
+    else
+        HIP_TRY(exact ? launch_render_exact(g, cam, out, count, s->counters, stream)
+                      : launch_render_fast(g, cam, out, count, s->counters, stream));
     HIP_TRY(hipEventRecord(s->k_stop, stream));
     HIP_TRY(hipEventRecord(s->ev_used[s->active], stream));
     if (o.flags & RT_RENDER_NO_SYNC) {
@@ -640,6 +672,21 @@ rt_status rt_trace_rays(rt_scene *s, const float *rays, size_t n, uint32_t flags
     (void)hipFree(d_rays);
     (void)hipFree(d_hits);
     if (e != hipSuccess) return fail(RT_ERR_DEVICE, std::string("rt_trace_rays: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
+rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
+    if (!s || !key) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
+    const std::string k(key);
+    if (k == "kernel") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "kernel must be 0 or 1");
+        s->use_persistent = value == 1;
+    } else if (k == "threshold") {
+        if (value < 1 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "threshold must be in 1..64");
+        s->threshold = (uint32_t)value;
+    } else {
+        return fail(RT_ERR_INVALID_ARGUMENT, "unknown option " + k);
+    }
     return RT_OK;
 }
 

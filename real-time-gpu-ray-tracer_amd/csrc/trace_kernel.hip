@@ -317,87 +317,111 @@ __device__ __forceinline__ SEnt stack_pop(Stack &stk, const SEnt *spill) {   // 
     return unpack(stk.lds[stk.sp * BLOCK]);
 }
 
-template <bool COUNT>
-__device__ bool trace(const SceneGPU &sc, const f3 &o, const f3 &d, Hit &hit, Stack &stk, LaneCount &cnt) {
-    SEnt spill[SPILL_DEPTH];
-    RayP wr; wr.o = o; wr.d = d; prep(wr);
-    RayP lr = wr;
-    float tmax = __builtin_huge_valf();
-    bool found = false;
+// Resumable per-lane traversal state: TLAS::hit (TLAS.cu:131-201) as a state machine so that a
+// persistent wave can interleave traversal steps with shading / ray regeneration of other lanes.
+struct Trav {
+    RayP wr, lr;           // world-space ray, instance-space ray of cur_inst
+    float tmax;            // currentRange.max
+    uint32_t cur;          // node to process next
+    uint32_t cur_inst;
+    Hit hit;
+    bool found;
+    bool tracing;
+    Stack stk;
+};
+
+__device__ __forceinline__ void trav_init(Trav &T, const SceneGPU &sc, const f3 &o, const f3 &d) {
+    T.wr.o = o; T.wr.d = d; prep(T.wr);
+    T.lr = T.wr;
+    T.tmax = __builtin_huge_valf();
+    T.found = false;
+    T.stk.sp = 0;
+    T.stk.spilled = 0;
+    T.cur = sc.tlas_root_ref;
+    T.cur_inst = 0;
     float te;
-    stk.sp = 0;
-    stk.spilled = 0;
-    if (!slab(sc.tlas_root_box, wr, TMIN, tmax, te)) return false;     // root pop test (TLAS.cu:150)
-    uint32_t cur = sc.tlas_root_ref;
-    uint32_t cur_inst = 0;
-    for (;;) {
-        if (!(cur & REF_LEAF)) {
-            // interior node pair: test both children (TLAS.cu:175-197 / BLAS.cu:178-202)
-            const bool blas = (cur & REF_BLAS) != 0;
-            const NodePair *P = (blas ? sc.blas_pairs : sc.tlas_pairs) + (cur & REF_INDEX_MASK);
-            const float4 *P4 = reinterpret_cast<const float4 *>(P);
-            const float4 A = P4[0], B = P4[1], Cc = P4[2];
-            const uint4 D = reinterpret_cast<const uint4 *>(P)[3];
-            const float b0[6] = {A.x, A.y, A.z, A.w, B.x, B.y};
-            const float b1[6] = {B.z, B.w, Cc.x, Cc.y, Cc.z, Cc.w};
-            if (COUNT) cnt.pairs++;
-            float e0 = 0.0f, e1 = 0.0f;
-            const RayP &r = blas ? lr : wr;
-            const bool h0 = slab(b0, r, TMIN, tmax, e0);
-            const bool h1 = slab(b1, r, TMIN, tmax, e1);
-            if (h0 && h1) {
-                // reference: tLeft > tRight -> push left then right (right popped first)
-                const bool right_near = e0 > e1;
-                stack_push(stk, spill, right_near ? D.x : D.y, right_near ? e0 : e1, cnt);
-                cur = right_near ? D.y : D.x;
-                continue;
+    T.tracing = slab(sc.tlas_root_box, T.wr, TMIN, T.tmax, te);          // root pop test (TLAS.cu:150)
+}
+
+// Process T.cur (one node pair, one TLAS leaf instance or one BLAS leaf), then choose the next node:
+// the near child, or a popped entry surviving the re-test; clears T.tracing when the stack is dry.
+template <bool COUNT>
+__device__ __forceinline__ void trav_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
+    const uint32_t cur = T.cur;
+    if (!(cur & REF_LEAF)) {
+        // interior node pair: test both children (TLAS.cu:175-197 / BLAS.cu:178-202)
+        const bool blas = (cur & REF_BLAS) != 0;
+        const NodePair *P = (blas ? sc.blas_pairs : sc.tlas_pairs) + (cur & REF_INDEX_MASK);
+        const float4 *P4 = reinterpret_cast<const float4 *>(P);
+        const float4 A = P4[0], B = P4[1], Cc = P4[2];
+        const uint4 D = reinterpret_cast<const uint4 *>(P)[3];
+        const float b0[6] = {A.x, A.y, A.z, A.w, B.x, B.y};
+        const float b1[6] = {B.z, B.w, Cc.x, Cc.y, Cc.z, Cc.w};
+        if (COUNT) cnt.pairs++;
+        float e0 = 0.0f, e1 = 0.0f;
+        const RayP &r = blas ? T.lr : T.wr;
+        const bool h0 = slab(b0, r, TMIN, T.tmax, e0);
+        const bool h1 = slab(b1, r, TMIN, T.tmax, e1);
+        if (h0 && h1) {
+            // reference: tLeft > tRight -> push left then right (right popped first)
+            const bool right_near = e0 > e1;
+            stack_push(T.stk, spill, right_near ? D.x : D.y, right_near ? e0 : e1, cnt);
+            T.cur = right_near ? D.y : D.x;
+            return;
+        }
+        if (h0) { T.cur = D.x; return; }
+        if (h1) { T.cur = D.y; return; }
+    } else if (!(cur & REF_BLAS)) {
+        // TLAS leaf: its instances in order (TLAS.cu:157-173)
+        const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur);
+        if (count > 1) stack_push(T.stk, spill, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
+        T.cur_inst = sc.tlas_slots[start];
+        const InstHot &I = sc.inst_hot[T.cur_inst];
+        if (COUNT) cnt.inst++;
+        // Instance::hit: ray into local space, d' not renormalised (Instance.cu:26-27)
+        T.lr.o = xf_point(I.inv, T.wr.o);
+        T.lr.d = xf_vector(I.inv, T.wr.d);
+        prep(T.lr);
+        float te;
+        if (slab(I.root_box, T.lr, TMIN, T.tmax, te)) { T.cur = I.root_ref; return; }   // BLAS root pop test
+    } else {
+        // BLAS leaf: primitives in leaf order (BLAS.cu:153-176)
+        const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur), type = ref_leaf_type(cur);
+        for (uint32_t k = 0; k < count; k++) {
+            const uint32_t slot = start + k;
+            float t = 0.0f, u = 0.0f, v = 0.0f;
+            bool h;
+            if (type == RT_PRIM_TRIANGLE) {
+                if (COUNT) cnt.tri++;
+                h = tri_test(sc.tri_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
+            } else if (type == RT_PRIM_SPHERE) {
+                if (COUNT) cnt.sq++;
+                h = sphere_test(sc.sph_hot[slot], T.lr, TMIN, T.tmax, t);
+            } else {
+                if (COUNT) { cnt.sq++; cnt.quad++; }
+                h = quad_test(sc.quad_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
             }
-            if (h0) { cur = D.x; continue; }
-            if (h1) { cur = D.y; continue; }
-        } else if (!(cur & REF_BLAS)) {
-            // TLAS leaf: its instances in order (TLAS.cu:157-173)
-            const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur);
-            if (count > 1) stack_push(stk, spill, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
-            cur_inst = sc.tlas_slots[start];
-            const InstHot &I = sc.inst_hot[cur_inst];
-            if (COUNT) cnt.inst++;
-            // Instance::hit: ray into local space, d' not renormalised (Instance.cu:26-27)
-            lr.o = xf_point(I.inv, wr.o);
-            lr.d = xf_vector(I.inv, wr.d);
-            prep(lr);
-            if (slab(I.root_box, lr, TMIN, tmax, te)) { cur = I.root_ref; continue; }   // BLAS root pop test
-        } else {
-            // BLAS leaf: primitives in leaf order (BLAS.cu:153-176)
-            const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur), type = ref_leaf_type(cur);
-            for (uint32_t k = 0; k < count; k++) {
-                const uint32_t slot = start + k;
-                float t = 0.0f, u = 0.0f, v = 0.0f;
-                bool h;
-                if (type == RT_PRIM_TRIANGLE) {
-                    if (COUNT) cnt.tri++;
-                    h = tri_test(sc.tri_hot[slot], lr, TMIN, tmax, t, u, v);
-                } else if (type == RT_PRIM_SPHERE) {
-                    if (COUNT) cnt.sq++;
-                    h = sphere_test(sc.sph_hot[slot], lr, TMIN, tmax, t);
-                } else {
-                    if (COUNT) { cnt.sq++; cnt.quad++; }
-                    h = quad_test(sc.quad_hot[slot], lr, TMIN, tmax, t, u, v);
-                }
-                if (h) {
-                    found = true; tmax = t;
-                    hit.t = t; hit.inst = cur_inst; hit.ptype = type; hit.slot = slot; hit.u = u; hit.v = v;
-                }
+            if (h) {
+                T.found = true; T.tmax = t;
+                T.hit.t = t; T.hit.inst = T.cur_inst; T.hit.ptype = type; T.hit.slot = slot; T.hit.u = u; T.hit.v = v;
             }
         }
-        // pop until an entry survives the re-test (entry t < tmax)
-        bool got = false;
-        while (!stk.empty()) {
-            const SEnt e = stack_pop(stk, spill);
-            if (__uint_as_float(e.tn) < tmax) { cur = e.ref; got = true; break; }
-        }
-        if (!got) break;
     }
-    return found;
+    // pop until an entry survives the re-test (entry t < tmax)
+    while (!T.stk.empty()) {
+        const SEnt e = stack_pop(T.stk, spill);
+        if (__uint_as_float(e.tn) < T.tmax) { T.cur = e.ref; return; }
+    }
+    T.tracing = false;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ bool trace(const SceneGPU &sc, const f3 &o, const f3 &d, Hit &hit, Trav &T, SEnt *spill,
+                                      LaneCount &cnt) {
+    trav_init(T, sc, o, d);
+    while (T.tracing) trav_step<COUNT>(T, sc, spill, cnt);
+    hit = T.hit;
+    return T.found;
 }
 
 // Record fields the shading needs (HitRecord, BasicTypes.cuh:19-31), world space.
@@ -434,13 +458,13 @@ __device__ __forceinline__ Surface finalize(const SceneGPU &sc, const f3 &wo, co
 }
 
 template <bool COUNT>
-__device__ f3 ray_color(const SceneGPU &sc, const CameraGPU &cam, f3 o, f3 d, Rng &rng, Stack &stk,
+__device__ f3 ray_color(const SceneGPU &sc, const CameraGPU &cam, f3 o, f3 d, Rng &rng, Trav &T, SEnt *spill,
                         LaneCount &cnt, uint32_t &rays) {                      // Kernel.cu:6-103
     f3 result = mk(1.0f, 1.0f, 1.0f);
     for (uint32_t depth = 0; depth < cam.depth; depth++) {
         Hit h;
         rays++;
-        if (trace<COUNT>(sc, o, d, h, stk, cnt)) {
+        if (trace<COUNT>(sc, o, d, h, T, spill, cnt)) {
             if (COUNT) cnt.hits++;
             const Surface s = finalize(sc, o, d, h);
             const float4 m = reinterpret_cast<const float4 *>(sc.materials)[s.material & ~MAT_METAL_BIT];
@@ -496,10 +520,9 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(SceneGPU sc, CameraGPU ca
     }
     const bool valid = px < cam.width && py < cam.height;
 
-    Stack stk;
-    stk.lds = (LdsU2 *)&lds_stack[0][tid];
-    stk.sp = 0;
-    stk.spilled = 0;
+    Trav T;
+    T.stk.lds = (LdsU2 *)&lds_stack[0][tid];
+    SEnt spill[SPILL_DEPTH];
     LaneCount cnt = {0, 0, 0, 0, 0, 0, 0};
     uint32_t rays = 0;
 
@@ -520,7 +543,7 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(SceneGPU sc, CameraGPU ca
                     origin = add(add(cc, scl(ld3(cam.cu), dv.x)), scl(ld3(cam.cv), dv.y));
                 }
                 const f3 dir = unit(sub(sp, origin));
-                result = add(result, ray_color<COUNT>(sc, cam, origin, dir, rng, stk, cnt, rays));
+                result = add(result, ray_color<COUNT>(sc, cam, origin, dir, rng, T, spill, cnt, rays));
             }
         }
         result = scl(result, cam.recip_sqrt * cam.recip_sqrt);                  // Kernel.cu:143
@@ -560,20 +583,213 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(SceneGPU sc, CameraGPU ca
     }
 }
 
+// ---- persistent-wave megakernel ------------------------------------------------------------
+// One launch of (#CUs x resident blocks) workgroups.  Each lane owns one pixel at a time and runs its
+// whole path (samples x bounces) as a sequence of ray segments; a segment is traversed step by
+// step (trav_step).  A wave keeps stepping while most lanes are traversing; when `threshold` lanes
+// have finished their segment (or are idle), the wave leaves the traversal loop and shades those
+// lanes together (scatter -> next segment, or next sample, or pixel write + a new pixel from the
+// work queue).  Lanes are refilled from a per-wave pool of 64 consecutive work items claimed with
+// one atomic per pool (ballot-compacted lane refill).  Each pixel's RNG stream
+// is consumed in exactly the reference order, so the image equals the grid kernel's bit for bit.
+__device__ __forceinline__ bool map_item(const OutputGPU &out, const CameraGPU &cam, uint32_t item,
+                                         uint32_t &px, uint32_t &py, uint32_t &oi) {
+    const uint32_t wunit = item >> 6, l = item & 63u;
+    if (out.tile_count == 0) {
+        const uint32_t ux = wunit % out.units_x, uy = wunit / out.units_x;
+        px = ux * 8 + (l & 7); py = uy * 8 + (l >> 3);
+        oi = py * cam.width + px;
+    } else {
+        const uint32_t upr = out.tile_w / 8, upt = upr * (out.tile_h / 8);
+        const uint32_t k = wunit / upt, r = wunit % upt;
+        const uint32_t t = out.tile_rank + k * out.tile_count;
+        const uint32_t lx = (r % upr) * 8 + (l & 7), ly = (r / upr) * 8 + (l >> 3);
+        px = (t % out.tiles_x) * out.tile_w + lx;
+        py = (t / out.tiles_x) * out.tile_h + ly;
+        oi = k * out.tile_w * out.tile_h + ly * out.tile_w + lx;
+    }
+    return px < cam.width && py < cam.height;
+}
+
+// Camera ray of sample `sample` of pixel (px, py) (Kernel.cu:119-135), consuming the pixel's RNG.
+__device__ __forceinline__ void camera_ray(const CameraGPU &cam, uint32_t px, uint32_t py, uint32_t sample, Rng &rng,
+                                           f3 &o, f3 &d) {
+    const uint32_t si = sample / cam.sqrt_s, sj = sample % cam.sqrt_s;
+    const float ox = (((float)sj + rng.uniform()) * cam.recip_sqrt) - 0.5f;
+    const float oy = (((float)si + rng.uniform()) * cam.recip_sqrt) - 0.5f;
+    const f3 sp = add(add(ld3(cam.pixel_origin), scl(ld3(cam.dx), (float)px + ox)), scl(ld3(cam.dy), (float)py + oy));
+    o = ld3(cam.center);
+    if (cam.focus_radius > 0.0f) {
+        const f3 dv = random_plane_vector(rng, cam.focus_radius);
+        o = add(add(o, scl(ld3(cam.cu), dv.x)), scl(ld3(cam.cv), dv.y));
+    }
+    d = unit(sub(sp, o));
+}
+
+__device__ __forceinline__ void write_pixel(const OutputGPU &out, uint32_t oi, f3 result) {
+    if (out.rgb) {
+        out.rgb[3 * (size_t)oi + 0] = result.x;
+        out.rgb[3 * (size_t)oi + 1] = result.y;
+        out.rgb[3 * (size_t)oi + 2] = result.z;
+    }
+    const float cr = fminf(fmaxf(sqrtf(result.x), 0.0f), 0.999f);       // Color3::castToUchar4
+    const float cg = fminf(fmaxf(sqrtf(result.y), 0.0f), 0.999f);
+    const float cb = fminf(fmaxf(sqrtf(result.z), 0.0f), 0.999f);
+    const uint32_t packed = (uint32_t)(uint8_t)(256.0f * cr) | ((uint32_t)(uint8_t)(256.0f * cg) << 8) |
+                            ((uint32_t)(uint8_t)(256.0f * cb) << 16) | (255u << 24);
+    reinterpret_cast<uint32_t *>(out.rgba)[oi] = packed;
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(BLOCK) void render_persistent_kernel(SceneGPU sc, CameraGPU cam, OutputGPU out,
+                                                                   uint32_t *queue, uint32_t threshold,
+                                                                   unsigned long long *counters) {
+    __shared__ unsigned long long lds_stack[LDS_DEPTH][BLOCK];
+    const int tid = threadIdx.x;
+    const int lane = tid & 63;
+    const uint32_t total = out.units * 64u;
+
+    Trav T;
+    T.stk.lds = (LdsU2 *)&lds_stack[0][tid];
+    T.tracing = false;
+    T.found = false;
+    SEnt spill[SPILL_DEPTH];
+    LaneCount cnt = {0, 0, 0, 0, 0, 0, 0};
+    uint32_t rays = 0, pixels = 0;
+
+    bool has = false;                  // lane owns a pixel
+    uint32_t px = 0, py = 0, oi = 0, sample = 0, depth = 0;
+    Rng rng;
+    rng.s = 0;
+    f3 acc = mk(0.0f, 0.0f, 0.0f), thr = mk(1.0f, 1.0f, 1.0f), ro = acc, rd = acc;
+    uint32_t pool_next = 0, pool_end = 0;     // wave-uniform
+    bool exhausted = false;                   // wave-uniform
+    const uint32_t S2 = cam.sqrt_s * cam.sqrt_s;
+
+    for (;;) {
+        // ---- refill idle lanes from the wave's pool / the global queue
+        uint64_t need = __ballot(!has);
+        while (need && !exhausted) {
+            const uint32_t n_need = __popcll(need);
+            if (pool_next >= pool_end) {
+                uint32_t b = 0;
+                if (lane == 0) b = atomicAdd(queue, 64u);
+                b = __shfl(b, 0, 64);
+                if (b >= total) { exhausted = true; break; }
+                pool_next = b;
+                pool_end = min(b + 64u, total);
+            }
+            const uint32_t take = min(n_need, pool_end - pool_next);
+            const uint32_t rank = __popcll(need & ((1ull << lane) - 1ull));
+            if (!has && rank < take) {
+                const uint32_t item = pool_next + rank;
+                if (map_item(out, cam, item, px, py, oi)) {
+                    has = true;
+                    const uint32_t pixel = cam.pitch * py + px;                    // Kernel.cu:109
+                    rng.init((uint64_t)pixel ^ cam.frame_seed, pixel);              // Kernel.cu:114
+                    acc = mk(0.0f, 0.0f, 0.0f);
+                    thr = mk(1.0f, 1.0f, 1.0f);
+                    sample = 0; depth = 0;
+                    camera_ray(cam, px, py, 0, rng, ro, rd);
+                    trav_init(T, sc, ro, rd);
+                    pixels++;
+                }
+            }
+            pool_next += take;
+            need = __ballot(!has);          // lanes handed an out-of-frame item (edge units) retry
+        }
+        if (!__any(has)) {
+            if (exhausted) break;
+            continue;
+        }
+        // ---- traverse while enough lanes are busy
+        for (;;) {
+            const uint64_t tr = __ballot(T.tracing);
+            if (tr == 0) break;
+            const uint64_t want = __ballot(!T.tracing && (has || !exhausted));
+            if ((uint32_t)__popcll(want) >= threshold) break;
+            if (T.tracing) trav_step<COUNT>(T, sc, spill, cnt);
+        }
+        // ---- shade lanes whose segment finished (rayColor body, Kernel.cu:64-100)
+        if (has && !T.tracing) {
+            rays++;
+            bool path_done;
+            if (T.found) {
+                if (COUNT) cnt.hits++;
+                const Surface s = finalize(sc, ro, rd, T.hit);
+                const float4 m = reinterpret_cast<const float4 *>(sc.materials)[s.material & ~MAT_METAL_BIT];
+                f3 outd;
+                bool absorbed = false;
+                if (!(s.material & MAT_METAL_BIT)) {                         // Rough.cuh:14-29
+                    outd = add(s.n, random_space_vector(rng));
+                    if (f_eq(dot(outd, outd), FZERO * FZERO)) outd = s.n;
+                } else {                                                     // Metal.cuh:15-32
+                    outd = unit(sub(rd, scl(s.n, 2.0f * dot(rd, s.n))));
+                    if (m.w > 0.0f) outd = add(outd, scl(random_space_vector(rng), m.w));
+                    absorbed = !(dot(outd, s.n) > 0.0f);
+                }
+                if (absorbed) {
+                    path_done = true;                                        // throughput (Kernel.cu:85-87)
+                } else {
+                    thr = mul(thr, mk(m.x, m.y, m.z));
+                    ro = s.p; rd = outd;
+                    depth++;
+                    path_done = depth >= cam.depth;                          // throughput on exhaustion
+                }
+            } else {
+                thr = mul(thr, ld3(cam.background));
+                path_done = true;
+            }
+            if (path_done) {
+                acc = add(acc, thr);                                         // Kernel.cu:138
+                sample++;
+                if (sample < S2) {
+                    thr = mk(1.0f, 1.0f, 1.0f);
+                    depth = 0;
+                    camera_ray(cam, px, py, sample, rng, ro, rd);
+                } else {
+                    write_pixel(out, oi, scl(acc, cam.recip_sqrt * cam.recip_sqrt));   // Kernel.cu:143-146
+                    has = false;
+                }
+            }
+            if (has) trav_init(T, sc, ro, rd);
+        }
+    }
+
+    const uint32_t wr = wave_sum(rays);
+    const uint32_t wp = wave_sum(pixels);
+    if (COUNT) {
+        const uint32_t a = wave_sum(cnt.pairs), b = wave_sum(cnt.tri), c = wave_sum(cnt.sq), d = wave_sum(cnt.inst),
+                       e = wave_sum(cnt.overflow), f = wave_sum(cnt.quad), g = wave_sum(cnt.hits);
+        if (lane == 0) {
+            atomicAdd(&counters[CNT_PAIRS], (unsigned long long)a);
+            atomicAdd(&counters[CNT_TRI], (unsigned long long)b);
+            atomicAdd(&counters[CNT_SPHQUAD], (unsigned long long)c);
+            atomicAdd(&counters[CNT_INST], (unsigned long long)d);
+            atomicAdd(&counters[CNT_OVERFLOW], (unsigned long long)e);
+            atomicAdd(&counters[CNT_QUAD], (unsigned long long)f);
+            atomicAdd(&counters[CNT_HITS], (unsigned long long)g);
+        }
+    }
+    if (lane == 0) {
+        atomicAdd(&counters[CNT_RAYS], (unsigned long long)wr);
+        atomicAdd(&counters[CNT_PIXELS], (unsigned long long)wp);
+    }
+}
+
 __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const float *rays, uint32_t n, rt_hit *hits) {
     __shared__ unsigned long long lds_stack[LDS_DEPTH][BLOCK];
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
-    Stack stk;
-    stk.lds = (LdsU2 *)&lds_stack[0][threadIdx.x];
-    stk.sp = 0;
-    stk.spilled = 0;
+    Trav T;
+    T.stk.lds = (LdsU2 *)&lds_stack[0][threadIdx.x];
+    SEnt spill[SPILL_DEPTH];
     LaneCount cnt = {0, 0, 0, 0, 0, 0, 0};
     const f3 o = mk(rays[6 * i], rays[6 * i + 1], rays[6 * i + 2]);
     const f3 d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
     Hit h;
     rt_hit r;
-    if (trace<false>(sc, o, d, h, stk, cnt)) {
+    if (trace<false>(sc, o, d, h, T, spill, cnt)) {
         const Surface s = finalize(sc, o, d, h);
         r.t = h.t; r.instance = h.inst; r.primitive_type = h.ptype; r.primitive_index = s.orig;
         r.point.x = s.p.x; r.point.y = s.p.y; r.point.z = s.p.z;
@@ -600,6 +816,29 @@ hipError_t RT_SUFFIX(launch_render)(const SceneGPU &sc, const CameraGPU &cam, co
     if (count) hipLaunchKernelGGL(render_kernel<true>, grid, dim3(BLOCK), 0, stream, sc, cam, out, counters);
     else hipLaunchKernelGGL(render_kernel<false>, grid, dim3(BLOCK), 0, stream, sc, cam, out, counters);
     return hipGetLastError();
+}
+
+hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
+                                               unsigned long long *counters, uint32_t *queue, uint32_t blocks,
+                                               uint32_t threshold, hipStream_t stream) {
+    using namespace RT_SUFFIX(dev);
+    if (out.units == 0) return hipSuccess;
+    hipError_t e = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+    const uint32_t need = (out.units + (BLOCK / 64) - 1) / (BLOCK / 64);
+    const dim3 grid(blocks < need ? blocks : need);
+    if (count)
+        hipLaunchKernelGGL(render_persistent_kernel<true>, grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
+    else
+        hipLaunchKernelGGL(render_persistent_kernel<false>, grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
+    return hipGetLastError();
+}
+
+uint32_t RT_SUFFIX(persistent_blocks_per_cu)() {
+    using namespace RT_SUFFIX(dev);
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false>, BLOCK, 0) != hipSuccess) return 1;
+    return n > 0 ? (uint32_t)n : 1u;
 }
 
 hipError_t RT_SUFFIX(launch_trace_rays)(const SceneGPU &sc, const float *rays, uint32_t n, rt_hit *hits,

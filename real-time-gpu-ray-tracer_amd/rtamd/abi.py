@@ -128,7 +128,7 @@ EXPORTED_SYMBOLS = (
     "rt_abi_version", "rt_last_error", "rt_device_count", "rt_scene_create", "rt_scene_build",
     "rt_camera_set", "rt_scene_update", "rt_render", "rt_assemble_tiles", "rt_tiles_for_rank",
     "rt_trace_rays", "rt_synchronize", "rt_scene_destroy", "rt_scene_get_info",
-    "rt_scene_export_blas", "rt_scene_export_tlas", "rt_demo_update",
+    "rt_scene_export_blas", "rt_scene_export_tlas", "rt_demo_update", "rt_scene_set_option",
 )
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -166,6 +166,8 @@ def _declare(lib):
                  "rt_assemble_tiles", "rt_trace_rays", "rt_synchronize", "rt_scene_get_info",
                  "rt_scene_export_blas", "rt_scene_export_tlas"):
         getattr(lib, name).restype = C.c_int
+    lib.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
+    lib.rt_scene_set_option.restype = C.c_int
     lib.rt_demo_update.argtypes = [C.c_void_p, P(Xform), C.c_size_t, C.c_uint64]
     lib.rt_demo_update.restype = None
     return lib

@@ -51,6 +51,10 @@ class Renderer:
         self.width, self.height = width, height
         return self
 
+    def set_option(self, key: str, value: int):
+        abi.check(self.lib, self.lib.rt_scene_set_option(self.h, key.encode(), int(value)))
+        return self
+
     def update(self, frame: int):
         abi.check(self.lib, self.lib.rt_scene_update(self.h, frame))
 

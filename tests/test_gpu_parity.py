@@ -200,3 +200,22 @@ def test_stack_depth_of_large_blas(gpu_lib):
     orgb, _, ocnt = o.render(threads=THREADS)
     assert (rgb != orgb).any(axis=2).sum() == 0
     assert st["triangle_tests"] == ocnt["triangle_tests"]
+
+
+@pytest.mark.parametrize("exact", [True, False])
+def test_persistent_kernel_equals_grid_kernel(gpu_lib, exact):
+    """The persistent-wave megakernel (lane refill, interleaved shading) and the one-thread-per-
+    pixel grid kernel consume each pixel's RNG identically: same bytes, same ray count."""
+    s = scenes.demo_with_particles(10)
+    r = Renderer(s).build_acceleration_structure(2).configure_camera(320, 180, ray_trace_depth=3, sample_count=4)
+    out = {}
+    for kernel in (0, 1):
+        for thr in ((16,) if kernel == 0 else (1, 16, 48, 64)):
+            r.set_option("kernel", kernel).set_option("threshold", thr)
+            rgba, rgb, st = r.render(0, exact=exact, want_rgb=True, count_work=True)
+            out[(kernel, thr)] = (rgba, rgb, st)
+    ref = out[(0, 16)]
+    for key, (rgba, rgb, st) in out.items():
+        assert np.array_equal(rgb, ref[1]) and np.array_equal(rgba, ref[0]), key
+        for k in ("rays", "pixels", "triangle_tests", "instance_visits", "hits"):
+            assert st[k] == ref[2][k], (key, k)
