@@ -257,7 +257,9 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
 /* Tuning knobs (defaults are the tuned values):
  *   "kernel"    : 0 = one-thread-per-pixel grid kernel, 1 = persistent-wave megakernel (default)
  *   "threshold" : persistent kernel — lanes that must be waiting before a wave leaves the
- *                 traversal loop to shade / regenerate (1..64)                                  */
+ *                 traversal loop to shade / regenerate (1..64)
+ *   "variant"   : persistent kernel register budget: 0 = compiler's choice, 4 / 5 = at least
+ *                 4 / 5 waves per SIMD                                                          */
 rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
 
 /* Blocks until all work the scene enqueued has finished. */

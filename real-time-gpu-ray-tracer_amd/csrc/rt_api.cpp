@@ -28,11 +28,11 @@ hipError_t launch_trace_rays_exact(const SceneGPU &, const float *, uint32_t, rt
 hipError_t launch_trace_rays_fast(const SceneGPU &, const float *, uint32_t, rt_hit *, hipStream_t);
 hipError_t launch_assemble(const void *, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, void *, hipStream_t);
 hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
-                                          uint32_t *, uint32_t, uint32_t, hipStream_t);
+                                          uint32_t *, uint32_t, uint32_t, uint32_t, hipStream_t);
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
-                                         uint32_t *, uint32_t, uint32_t, hipStream_t);
-uint32_t persistent_blocks_per_cu_exact();
-uint32_t persistent_blocks_per_cu_fast();
+                                         uint32_t *, uint32_t, uint32_t, uint32_t, hipStream_t);
+uint32_t persistent_blocks_per_cu_exact(uint32_t variant);
+uint32_t persistent_blocks_per_cu_fast(uint32_t variant);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -130,8 +130,9 @@ struct rt_scene {
     hipEvent_t k_start = nullptr, k_stop = nullptr;
     // persistent megakernel: work-queue head, grid size (#CUs x resident blocks), refill threshold
     uint32_t *queue = nullptr;
-    uint32_t persist_blocks_exact = 0, persist_blocks_fast = 0;
+    uint32_t cus = 0;
     uint32_t threshold = 16;
+    uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4, 5)
     bool use_persistent = true;
     unsigned long long *counters = nullptr;       // HBM CNT_NUM
     unsigned long long *counters_host = nullptr;  // pinned
@@ -469,9 +470,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     {
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, s->device));
-        const uint32_t cus = (uint32_t)prop.multiProcessorCount;
-        s->persist_blocks_exact = cus * persistent_blocks_per_cu_exact();
-        s->persist_blocks_fast = cus * persistent_blocks_per_cu_fast();
+        s->cus = (uint32_t)prop.multiProcessorCount;
         if (const char *k = std::getenv("RTAMD_KERNEL")) s->use_persistent = std::string(k) != "grid";
         if (const char *t = std::getenv("RTAMD_THRESHOLD")) {
             const long v = std::strtol(t, nullptr, 10);
@@ -600,10 +599,12 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     HIP_TRY(hipMemsetAsync(s->counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
     HIP_TRY(hipEventRecord(s->k_start, stream));
     if (s->use_persistent)
-        HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, s->counters, s->queue, s->persist_blocks_exact,
-                                                       s->threshold, stream)
-                      : launch_render_persistent_fast(g, cam, out, count, s->counters, s->queue, s->persist_blocks_fast,
-                                                      s->threshold, stream));
+        HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, s->counters, s->queue,
+                                                       s->cus * persistent_blocks_per_cu_exact(s->variant), s->threshold,
+                                                       s->variant, stream)
+                      : launch_render_persistent_fast(g, cam, out, count, s->counters, s->queue,
+                                                      s->cus * persistent_blocks_per_cu_fast(s->variant), s->threshold,
+                                                      s->variant, stream));
     else
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, s->counters, stream)
                       : launch_render_fast(g, cam, out, count, s->counters, stream));
@@ -684,6 +685,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "threshold") {
         if (value < 1 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "threshold must be in 1..64");
         s->threshold = (uint32_t)value;
+    } else if (k == "variant") {
+        if (value != 0 && value != 4 && value != 5) return fail(RT_ERR_INVALID_ARGUMENT, "variant must be 0, 4 or 5");
+        s->variant = (uint32_t)value;
     } else {
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown option " + k);
     }

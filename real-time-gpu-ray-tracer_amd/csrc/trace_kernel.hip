@@ -60,8 +60,28 @@ __device__ __forceinline__ float dot(f3 a, f3 b) {          // Vec3.cuh:113-119
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {           // Vec3.cuh:120-126
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
+// FAST mode replaces IEEE division / 1/sqrt by the hardware v_rcp_f32 / v_rsq_f32 (1 ulp);
+// EXACT mode keeps the reference's correctly rounded operations.
+__device__ __forceinline__ float rcp(float x) {
+#if RT_EXACT
+    return 1.0f / x;
+#else
+    return __builtin_amdgcn_rcpf(x);
+#endif
+}
+__device__ __forceinline__ float fdiv(float a, float b) {
+#if RT_EXACT
+    return a / b;
+#else
+    return a * __builtin_amdgcn_rcpf(b);
+#endif
+}
 __device__ __forceinline__ f3 unit(f3 a) {                   // Vec3.cuh:129-137
+#if RT_EXACT
     const float f = 1.0f / sqrtf(dot(a, a));
+#else
+    const float f = __builtin_amdgcn_rsqf(dot(a, a));
+#endif
     return mk(a.x * f, a.y * f, a.z * f);
 }
 __device__ __forceinline__ float comp(f3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
@@ -119,7 +139,7 @@ struct RayP {
 __device__ __forceinline__ void prep(RayP &r) {
 #if !RT_EXACT
     r.tiny = fabsf(r.d.x) < FZERO || fabsf(r.d.y) < FZERO || fabsf(r.d.z) < FZERO;
-    r.inv = mk(1.0f / r.d.x, 1.0f / r.d.y, 1.0f / r.d.z);
+    r.inv = mk(rcp(r.d.x), rcp(r.d.y), rcp(r.d.z));
     r.oinv = mk(r.o.x * r.inv.x, r.o.y * r.inv.y, r.o.z * r.inv.z);
 #else
     (void)r;
@@ -136,8 +156,8 @@ __device__ __forceinline__ bool slab_ref(const float *b, const f3 &o, const f3 &
             if (q < mn || q > mx) return false;
             continue;
         }
-        const float t1 = (mn - q) / dd;
-        const float t2 = (mx - q) / dd;
+        const float t1 = fdiv(mn - q, dd);
+        const float t2 = fdiv(mx - q, dd);
         if (t1 < t2) {
             if (t1 > cmin) cmin = t1;
             if (t2 < cmax) cmax = t2;
@@ -201,8 +221,8 @@ __device__ __forceinline__ bool sphere_test(const SphereHot &S, const RayP &r, f
     float delta = b * b - 4.0f * a * cc;
     if (delta < 0.0f) return false;
     delta = sqrtf(delta);
-    const float root1 = (-b - delta) / (a * 2.0f);
-    const float root2 = (-b + delta) / (a * 2.0f);
+    const float root1 = fdiv(-b - delta, a * 2.0f);
+    const float root2 = fdiv(-b + delta, a * 2.0f);
     if (in_range(root1, tmin, tmax)) { t = root1; return true; }
     if (in_range(root2, tmin, tmax)) { t = root2; return true; }
     return false;
@@ -215,14 +235,14 @@ __device__ __forceinline__ bool quad_test(const QuadHot &Q, const RayP &r, float
     if (fabsf(ndd) < FZERO) return false;
     float ndp = 0.0f;
     ndp += n.x * r.o.x; ndp += n.y * r.o.y; ndp += n.z * r.o.z;
-    const float tt = (Q.d - ndp) / ndd;
+    const float tt = fdiv(Q.d - ndp, ndd);
     if (!in_range(tt, tmin, tmax)) return false;
     const f3 inter = add(r.o, scl(r.d, tt));
     const f3 p = sub(inter, ld3(Q.q));
     const f3 nx = ld3(Q.nx);
     if (fabsf(Q.den) < FZERO) return false;
-    al = dot(cross(p, ld3(Q.v)), nx) / Q.den;
-    be = dot(cross(ld3(Q.u), p), nx) / Q.den;
+    al = fdiv(dot(cross(p, ld3(Q.v)), nx), Q.den);
+    be = fdiv(dot(cross(ld3(Q.u), p), nx), Q.den);
     if (!in_range(al, 0.0f, 1.0f) || !in_range(be, 0.0f, 1.0f)) return false;
     t = tt;
     return true;
@@ -641,9 +661,9 @@ __device__ __forceinline__ void write_pixel(const OutputGPU &out, uint32_t oi, f
 }
 
 template <bool COUNT>
-__global__ __launch_bounds__(BLOCK) void render_persistent_kernel(SceneGPU sc, CameraGPU cam, OutputGPU out,
-                                                                   uint32_t *queue, uint32_t threshold,
-                                                                   unsigned long long *counters) {
+__device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out,
+                                                       uint32_t *queue, uint32_t threshold,
+                                                       unsigned long long *counters) {
     __shared__ unsigned long long lds_stack[LDS_DEPTH][BLOCK];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
@@ -658,10 +678,10 @@ __global__ __launch_bounds__(BLOCK) void render_persistent_kernel(SceneGPU sc, C
     uint32_t rays = 0, pixels = 0;
 
     bool has = false;                  // lane owns a pixel
-    uint32_t px = 0, py = 0, oi = 0, sample = 0, depth = 0;
+    uint32_t item = 0, sample = 0, depth = 0;
     Rng rng;
     rng.s = 0;
-    f3 acc = mk(0.0f, 0.0f, 0.0f), thr = mk(1.0f, 1.0f, 1.0f), ro = acc, rd = acc;
+    f3 acc = mk(0.0f, 0.0f, 0.0f), thr = mk(1.0f, 1.0f, 1.0f);
     uint32_t pool_next = 0, pool_end = 0;     // wave-uniform
     bool exhausted = false;                   // wave-uniform
     const uint32_t S2 = cam.sqrt_s * cam.sqrt_s;
@@ -682,7 +702,8 @@ __global__ __launch_bounds__(BLOCK) void render_persistent_kernel(SceneGPU sc, C
             const uint32_t take = min(n_need, pool_end - pool_next);
             const uint32_t rank = __popcll(need & ((1ull << lane) - 1ull));
             if (!has && rank < take) {
-                const uint32_t item = pool_next + rank;
+                uint32_t px, py, oi;
+                item = pool_next + rank;
                 if (map_item(out, cam, item, px, py, oi)) {
                     has = true;
                     const uint32_t pixel = cam.pitch * py + px;                    // Kernel.cu:109
@@ -690,8 +711,9 @@ __global__ __launch_bounds__(BLOCK) void render_persistent_kernel(SceneGPU sc, C
                     acc = mk(0.0f, 0.0f, 0.0f);
                     thr = mk(1.0f, 1.0f, 1.0f);
                     sample = 0; depth = 0;
-                    camera_ray(cam, px, py, 0, rng, ro, rd);
-                    trav_init(T, sc, ro, rd);
+                    f3 o, d;
+                    camera_ray(cam, px, py, 0, rng, o, d);
+                    trav_init(T, sc, o, d);
                     pixels++;
                 }
             }
@@ -714,25 +736,25 @@ __global__ __launch_bounds__(BLOCK) void render_persistent_kernel(SceneGPU sc, C
         if (has && !T.tracing) {
             rays++;
             bool path_done;
+            f3 no = T.wr.o, nd = T.wr.d;                                     // next segment
             if (T.found) {
                 if (COUNT) cnt.hits++;
-                const Surface s = finalize(sc, ro, rd, T.hit);
+                const Surface s = finalize(sc, T.wr.o, T.wr.d, T.hit);
                 const float4 m = reinterpret_cast<const float4 *>(sc.materials)[s.material & ~MAT_METAL_BIT];
-                f3 outd;
                 bool absorbed = false;
                 if (!(s.material & MAT_METAL_BIT)) {                         // Rough.cuh:14-29
-                    outd = add(s.n, random_space_vector(rng));
-                    if (f_eq(dot(outd, outd), FZERO * FZERO)) outd = s.n;
+                    nd = add(s.n, random_space_vector(rng));
+                    if (f_eq(dot(nd, nd), FZERO * FZERO)) nd = s.n;
                 } else {                                                     // Metal.cuh:15-32
-                    outd = unit(sub(rd, scl(s.n, 2.0f * dot(rd, s.n))));
-                    if (m.w > 0.0f) outd = add(outd, scl(random_space_vector(rng), m.w));
-                    absorbed = !(dot(outd, s.n) > 0.0f);
+                    nd = unit(sub(T.wr.d, scl(s.n, 2.0f * dot(T.wr.d, s.n))));
+                    if (m.w > 0.0f) nd = add(nd, scl(random_space_vector(rng), m.w));
+                    absorbed = !(dot(nd, s.n) > 0.0f);
                 }
                 if (absorbed) {
                     path_done = true;                                        // throughput (Kernel.cu:85-87)
                 } else {
                     thr = mul(thr, mk(m.x, m.y, m.z));
-                    ro = s.p; rd = outd;
+                    no = s.p;
                     depth++;
                     path_done = depth >= cam.depth;                          // throughput on exhaustion
                 }
@@ -743,16 +765,18 @@ __global__ __launch_bounds__(BLOCK) void render_persistent_kernel(SceneGPU sc, C
             if (path_done) {
                 acc = add(acc, thr);                                         // Kernel.cu:138
                 sample++;
+                uint32_t px, py, oi;
+                map_item(out, cam, item, px, py, oi);
                 if (sample < S2) {
                     thr = mk(1.0f, 1.0f, 1.0f);
                     depth = 0;
-                    camera_ray(cam, px, py, sample, rng, ro, rd);
+                    camera_ray(cam, px, py, sample, rng, no, nd);
                 } else {
                     write_pixel(out, oi, scl(acc, cam.recip_sqrt * cam.recip_sqrt));   // Kernel.cu:143-146
                     has = false;
                 }
             }
-            if (has) trav_init(T, sc, ro, rd);
+            if (has) trav_init(T, sc, no, nd);
         }
     }
 
@@ -775,6 +799,14 @@ __global__ __launch_bounds__(BLOCK) void render_persistent_kernel(SceneGPU sc, C
         atomicAdd(&counters[CNT_RAYS], (unsigned long long)wr);
         atomicAdd(&counters[CNT_PIXELS], (unsigned long long)wp);
     }
+}
+
+// Register budget variants: WPE = minimum waves per SIMD the compiler must allow (0 = its choice).
+template <bool COUNT, int WPE>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
+void render_persistent_kernel(SceneGPU sc, CameraGPU cam, OutputGPU out, uint32_t *queue, uint32_t threshold,
+                              unsigned long long *counters) {
+    render_persistent_body<COUNT>(sc, cam, out, queue, threshold, counters);
 }
 
 __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const float *rays, uint32_t n, rt_hit *hits) {
@@ -818,27 +850,45 @@ hipError_t RT_SUFFIX(launch_render)(const SceneGPU &sc, const CameraGPU &cam, co
     return hipGetLastError();
 }
 
+namespace {
+template <int WPE>
+hipError_t launch_persistent_wpe(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
+                                 unsigned long long *counters, uint32_t *queue, uint32_t blocks_per_cu_cus,
+                                 uint32_t threshold, hipStream_t stream) {
+    using namespace RT_SUFFIX(dev);
+    const uint32_t need = (out.units + (BLOCK / 64) - 1) / (BLOCK / 64);
+    const dim3 grid(blocks_per_cu_cus < need ? blocks_per_cu_cus : need);
+    if (count)
+        hipLaunchKernelGGL((render_persistent_kernel<true, WPE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
+    else
+        hipLaunchKernelGGL((render_persistent_kernel<false, WPE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
+    return hipGetLastError();
+}
+template <int WPE>
+uint32_t blocks_per_cu_wpe() {
+    using namespace RT_SUFFIX(dev);
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false, WPE>, BLOCK, 0) != hipSuccess) return 1;
+    return n > 0 ? (uint32_t)n : 1u;
+}
+}  // namespace
+
+// variant: 0 = compiler's register budget, 4 / 5 = at least 4 / 5 waves per SIMD
 hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
                                                unsigned long long *counters, uint32_t *queue, uint32_t blocks,
-                                               uint32_t threshold, hipStream_t stream) {
-    using namespace RT_SUFFIX(dev);
+                                               uint32_t threshold, uint32_t variant, hipStream_t stream) {
     if (out.units == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    const uint32_t need = (out.units + (BLOCK / 64) - 1) / (BLOCK / 64);
-    const dim3 grid(blocks < need ? blocks : need);
-    if (count)
-        hipLaunchKernelGGL(render_persistent_kernel<true>, grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
-    else
-        hipLaunchKernelGGL(render_persistent_kernel<false>, grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
-    return hipGetLastError();
+    if (variant == 4) return launch_persistent_wpe<4>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+    if (variant == 5) return launch_persistent_wpe<5>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+    return launch_persistent_wpe<0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
 }
 
-uint32_t RT_SUFFIX(persistent_blocks_per_cu)() {
-    using namespace RT_SUFFIX(dev);
-    int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false>, BLOCK, 0) != hipSuccess) return 1;
-    return n > 0 ? (uint32_t)n : 1u;
+uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant) {
+    if (variant == 4) return blocks_per_cu_wpe<4>();
+    if (variant == 5) return blocks_per_cu_wpe<5>();
+    return blocks_per_cu_wpe<0>();
 }
 
 hipError_t RT_SUFFIX(launch_trace_rays)(const SceneGPU &sc, const float *rays, uint32_t n, rt_hit *hits,
