@@ -43,6 +43,24 @@ def main():
         res["write_bytes_per_launch"] = avg["WRITE_SIZE"] * 1024.0
         res["hbm_bytes_per_launch"] = int(res["fetch_bytes_per_launch_corrected"] + res["write_bytes_per_launch"])
         res["note"] = "hbm_bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction)"
+    a = avg
+    if {"SQ_WAVE_CYCLES", "GRBM_GUI_ACTIVE"} <= a.keys():
+        # waves resident per CU: SQ_WAVE_CYCLES counts quad-cycles (MI355X_MICROARCH.md) over 256 CUs;
+        # GRBM_GUI_ACTIVE is summed over 8 XCDs
+        gui = a["GRBM_GUI_ACTIVE"] / 8.0
+        res["derived_waves_per_cu"] = 4.0 * a["SQ_WAVE_CYCLES"] / gui / 256.0
+    if {"SQ_WAIT_ANY", "SQ_WAVE_CYCLES"} <= a.keys():
+        res["derived_frac_wave_cycles_waiting"] = a["SQ_WAIT_ANY"] / a["SQ_WAVE_CYCLES"]
+    if {"SQ_ACTIVE_INST_VALU", "SQ_WAVE_CYCLES"} <= a.keys():
+        res["derived_frac_wave_cycles_valu"] = a["SQ_ACTIVE_INST_VALU"] / a["SQ_WAVE_CYCLES"]
+    if {"SQ_THREAD_CYCLES_VALU", "SQ_ACTIVE_INST_VALU"} <= a.keys():
+        res["derived_valu_lane_utilization"] = a["SQ_THREAD_CYCLES_VALU"] / (64.0 * a["SQ_ACTIVE_INST_VALU"])
+    if {"SQ_THREAD_CYCLES_VALU", "SQ_INSTS_VALU"} <= a.keys():
+        res["derived_active_lanes_per_valu_inst"] = a["SQ_THREAD_CYCLES_VALU"] / a["SQ_INSTS_VALU"]
+    if {"TCC_HIT_sum", "TCC_MISS_sum"} <= a.keys():
+        res["derived_l2_hit_rate"] = a["TCC_HIT_sum"] / max(1.0, a["TCC_HIT_sum"] + a["TCC_MISS_sum"])
+    if {"TCP_TCC_READ_REQ_LATENCY_sum", "TCP_TCC_READ_REQ_sum"} <= a.keys():
+        res["derived_l1_to_l2_read_latency_cycles"] = a["TCP_TCC_READ_REQ_LATENCY_sum"] / max(1.0, a["TCP_TCC_READ_REQ_sum"])
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))
