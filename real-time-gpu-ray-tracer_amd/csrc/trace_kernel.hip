@@ -339,10 +339,14 @@ __device__ __forceinline__ SEnt stack_pop(Stack &stk, const SEnt *spill) {   // 
 
 // Resumable per-lane traversal state: TLAS::hit (TLAS.cu:131-201) as a state machine so that a
 // persistent wave can interleave traversal steps with shading / ray regeneration of other lanes.
+constexpr uint32_t REF_NONE = 0xFFFFFFFFu;   // leaf bit + primitive type 3: never a real ref
+
 struct Trav {
     RayP wr, lr;           // world-space ray, instance-space ray of cur_inst
     float tmax;            // currentRange.max
-    uint32_t cur;          // node to process next
+    uint32_t cur;          // node to process next (REF_NONE: stack exhausted)
+    float curT;            // entry t of cur (speculative traversal re-checks it)
+    uint32_t pleaf;        // postponed leaf (speculative traversal), REF_NONE if none
     uint32_t cur_inst;
     Hit hit;
     bool found;
@@ -359,8 +363,10 @@ __device__ __forceinline__ void trav_init(Trav &T, const SceneGPU &sc, const f3 
     T.stk.spilled = 0;
     T.cur = sc.tlas_root_ref;
     T.cur_inst = 0;
-    float te;
+    T.pleaf = REF_NONE;
+    float te = 0.0f;
     T.tracing = slab(sc.tlas_root_box, T.wr, TMIN, T.tmax, te);          // root pop test (TLAS.cu:150)
+    T.curT = te;
 }
 
 // Process T.cur (one node pair, one TLAS leaf instance or one BLAS leaf), then choose the next node:
@@ -433,6 +439,123 @@ __device__ __forceinline__ void trav_step(Trav &T, const SceneGPU &sc, SEnt *spi
         if (__uint_as_float(e.tn) < T.tmax) { T.cur = e.ref; return; }
     }
     T.tracing = false;
+}
+
+// ---- speculative while-while traversal (Aila & Laine 2009), reference-order preserving ----------
+// Phase 1 (interior loop): every lane walks interior node pairs; the first leaf a lane reaches is
+// postponed (pleaf) and the lane keeps walking (speculatively) until it meets a second leaf; the
+// wave leaves the loop once every traversing lane holds a postponed leaf.  Phase 2 processes the
+// postponed leaves together.  The reference processes a leaf before the nodes that follow it, with
+// the tmax the leaf produced.  Speculative steps used the older (larger) tmax, so:
+//   * the postponed leaf itself passed its test with the current tmax (no leaf ran in between);
+//   * entries pushed speculatively are re-tested at pop (entry t < tmax), as always;
+//   * the node the lane stopped at (cur) is re-tested after the leaf: every node reached below a node
+//     N has entry t >= N's entry t (child boxes lie inside parent boxes and the slab entry is
+//     monotone in the box bounds), so cur fails its re-test whenever the reference would have culled
+//     N or any node on the way.
+// Hence leaves are processed in the reference order with the reference's tmax: same hits, same
+// primitive tests, same instance visits (only extra node-pair tests are speculative).
+__device__ __forceinline__ void pop_next(Trav &T, const SEnt *spill) {
+    while (!T.stk.empty()) {
+        const SEnt e = stack_pop(T.stk, spill);
+        const float tn = __uint_as_float(e.tn);
+        if (tn < T.tmax) { T.cur = e.ref; T.curT = tn; return; }
+    }
+    T.cur = REF_NONE;
+}
+
+// One interior-loop step of a lane whose cur is an interior node, or a leaf to postpone.
+template <bool COUNT>
+__device__ __forceinline__ void spec_interior_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
+    const uint32_t cur = T.cur;
+    if (!(cur & REF_LEAF)) {
+        const bool blas = (cur & REF_BLAS) != 0;
+        const NodePair *P = (blas ? sc.blas_pairs : sc.tlas_pairs) + (cur & REF_INDEX_MASK);
+        const float4 *P4 = reinterpret_cast<const float4 *>(P);
+        const float4 A = P4[0], B = P4[1], Cc = P4[2];
+        const uint4 D = reinterpret_cast<const uint4 *>(P)[3];
+        const float b0[6] = {A.x, A.y, A.z, A.w, B.x, B.y};
+        const float b1[6] = {B.z, B.w, Cc.x, Cc.y, Cc.z, Cc.w};
+        if (COUNT) cnt.pairs++;
+        float e0 = 0.0f, e1 = 0.0f;
+        const RayP &r = blas ? T.lr : T.wr;
+        const bool h0 = slab(b0, r, TMIN, T.tmax, e0);
+        const bool h1 = slab(b1, r, TMIN, T.tmax, e1);
+        if (h0 && h1) {
+            const bool right_near = e0 > e1;          // TLAS.cu:185-192 ordering
+            stack_push(T.stk, spill, right_near ? D.x : D.y, right_near ? e0 : e1, cnt);
+            T.cur = right_near ? D.y : D.x;
+            T.curT = right_near ? e1 : e0;
+            return;
+        }
+        if (h0 || h1) {
+            T.cur = h0 ? D.x : D.y;
+            T.curT = h0 ? e0 : e1;
+            return;
+        }
+        pop_next(T, spill);
+    } else {
+        T.pleaf = cur;                                // postpone, keep walking
+        pop_next(T, spill);
+    }
+}
+
+// Process the postponed leaf, then resume at cur (re-tested) — TLAS.cu:157-173 / BLAS.cu:153-176.
+template <bool COUNT>
+__device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
+    const uint32_t leaf = T.pleaf;
+    T.pleaf = REF_NONE;
+    if (!(leaf & REF_BLAS)) {
+        // TLAS leaf: enter the first instance's BLAS; the speculative successor and the leaf's
+        // remaining instances wait on the stack (popped in reference order).
+        const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf);
+        if (T.cur != REF_NONE) stack_push(T.stk, spill, T.cur, T.curT, cnt);
+        if (count > 1) stack_push(T.stk, spill, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
+        T.cur_inst = sc.tlas_slots[start];
+        const InstHot &I = sc.inst_hot[T.cur_inst];
+        if (COUNT) cnt.inst++;
+        T.lr.o = xf_point(I.inv, T.wr.o);                      // Instance.cu:26-27
+        T.lr.d = xf_vector(I.inv, T.wr.d);
+        prep(T.lr);
+        float te = 0.0f;
+        if (slab(I.root_box, T.lr, TMIN, T.tmax, te)) { T.cur = I.root_ref; T.curT = te; }
+        else pop_next(T, spill);
+    } else {
+        const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf), type = ref_leaf_type(leaf);
+        for (uint32_t k = 0; k < count; k++) {
+            const uint32_t slot = start + k;
+            float t = 0.0f, u = 0.0f, v = 0.0f;
+            bool h;
+            if (type == RT_PRIM_TRIANGLE) {
+                if (COUNT) cnt.tri++;
+                h = tri_test(sc.tri_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
+            } else if (type == RT_PRIM_SPHERE) {
+                if (COUNT) cnt.sq++;
+                h = sphere_test(sc.sph_hot[slot], T.lr, TMIN, T.tmax, t);
+            } else {
+                if (COUNT) { cnt.sq++; cnt.quad++; }
+                h = quad_test(sc.quad_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
+            }
+            if (h) {
+                T.found = true; T.tmax = t;
+                T.hit.t = t; T.hit.inst = T.cur_inst; T.hit.ptype = type; T.hit.slot = slot; T.hit.u = u; T.hit.v = v;
+            }
+        }
+        if (T.cur != REF_NONE && !(T.curT < T.tmax)) pop_next(T, spill);   // re-test the successor
+    }
+    if (T.cur == REF_NONE) T.tracing = false;
+}
+
+// One round: interior loop until every traversing lane holds a leaf, then the leaf phase.
+template <bool COUNT>
+__device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
+    for (;;) {
+        if (T.tracing && T.pleaf == REF_NONE && T.cur == REF_NONE) T.tracing = false;   // done, no leaf left
+        if (!__any(T.tracing && T.pleaf == REF_NONE)) break;
+        const bool active = T.tracing && T.cur != REF_NONE && (!(T.cur & REF_LEAF) || T.pleaf == REF_NONE);
+        if (active) spec_interior_step<COUNT>(T, sc, spill, cnt);
+    }
+    if (T.tracing) spec_leaf_phase<COUNT>(T, sc, spill, cnt);
 }
 
 template <bool COUNT>
@@ -730,7 +853,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             if (tr == 0) break;
             const uint64_t want = __ballot(!T.tracing && (has || !exhausted));
             if ((uint32_t)__popcll(want) >= threshold) break;
-            if (T.tracing) trav_step<COUNT>(T, sc, spill, cnt);
+            spec_round<COUNT>(T, sc, spill, cnt);
         }
         // ---- shade lanes whose segment finished (rayColor body, Kernel.cu:64-100)
         if (has && !T.tracing) {
