@@ -151,7 +151,10 @@ typedef struct rt_camera_input {
  * from std::mt19937(random_device); here the axis stream is a pinned function of `seed`
  * so builds are reproducible, and centroid ties are broken by primitive index. */
 typedef enum rt_build_mode {
-    RT_BUILD_COMPAT_MEDIAN = 0
+    RT_BUILD_COMPAT_MEDIAN = 0,
+    /* Surface-area-heuristic BLAS and per-frame TLAS (leaf <= 4 items).  Different trees than the
+     * reference: hits agree except where two surfaces tie within the 1e-6 window. */
+    RT_BUILD_SAH = 1
 } rt_build_mode;
 
 typedef enum rt_render_flags {

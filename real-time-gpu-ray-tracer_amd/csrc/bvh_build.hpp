@@ -80,6 +80,142 @@ inline Tree build_median_tree(std::vector<BuildItem> items, uint32_t leaf_cap, u
     return t;
 }
 
+// ---- SAH builder (RT_BUILD_SAH) ---------------------------------------------------------------
+// Top-down surface-area-heuristic build: for each node, the split minimising
+//   C = C_trav + (A_L / A) * N_L * C_isect + (A_R / A) * N_R * C_isect
+// over the centroid-sorted sweeps of all three axes (exact sweep up to `sweep_max` items, 32 binned
+// planes above that); a node becomes a leaf when it holds <= leaf_cap items and the leaf cost
+// N * C_isect is not worse than the best split.  Output uses the same node convention as the
+// median builder (children at index, index+1; leaves index a DFS-ordered item array), so the
+// flattening and the kernels are unchanged.  Trees differ from the reference's, so results differ
+// only where two surfaces tie within the 1e-6 window (FAST tolerance).
+inline float half_area(const hm::Box &b) {
+    const float dx = b.r[0].max - b.r[0].min, dy = b.r[1].max - b.r[1].min, dz = b.r[2].max - b.r[2].min;
+    return dx * dy + dy * dz + dz * dx;
+}
+
+inline Tree build_sah_tree(std::vector<BuildItem> items, uint32_t leaf_cap, float c_trav = 1.0f, float c_isect = 1.0f,
+                           uint32_t sweep_max = 4096) {
+    Tree t;
+    const uint32_t n = (uint32_t)items.size();
+    t.nodes.resize(n ? 2 * (size_t)n - 1 : 0);
+    t.refs.reserve(n);
+    if (n == 0) return t;
+    struct Task { uint32_t start, count, node; };
+    std::vector<Task> stack;
+    stack.push_back({0, n, 0});
+    uint32_t node_count = 1;
+    std::vector<float> right_area(n + 1);
+    while (!stack.empty()) {
+        const Task task = stack.back();
+        stack.pop_back();
+        TreeNode &node = t.nodes[task.node];
+        hm::Box bb = items[task.start].box;
+        hm::Box cb{{{items[task.start].centroid.x, items[task.start].centroid.x},
+                    {items[task.start].centroid.y, items[task.start].centroid.y},
+                    {items[task.start].centroid.z, items[task.start].centroid.z}}};
+        for (uint32_t i = task.start + 1; i < task.start + task.count; i++) {
+            bb = hm::Box::merge(bb, items[i].box);
+            for (int a = 0; a < 3; a++) {
+                cb.r[a].min = std::min(cb.r[a].min, items[i].centroid[a]);
+                cb.r[a].max = std::max(cb.r[a].max, items[i].centroid[a]);
+            }
+        }
+        node.box = bb;
+        const uint32_t cnt = task.count;
+        const float parent_area = std::max(half_area(bb), 1e-30f);
+        float best_cost = INFINITY;
+        int best_axis = -1;
+        uint32_t best_mid = 0;
+        float best_plane = 0.0f;
+        if (cnt > 1) {
+            for (int axis = 0; axis < 3; axis++) {
+                if (!(cb.r[axis].max > cb.r[axis].min)) continue;
+                if (cnt <= sweep_max) {
+                    std::sort(items.begin() + task.start, items.begin() + task.start + cnt,
+                              [axis](const BuildItem &a, const BuildItem &b) {
+                                  const float fa = a.centroid[axis], fb = b.centroid[axis];
+                                  return fa < fb || (!(fb < fa) && a.index < b.index);
+                              });
+                    hm::Box acc = items[task.start + cnt - 1].box;
+                    right_area[cnt - 1] = half_area(acc);
+                    for (int64_t i = (int64_t)cnt - 2; i >= 1; i--) {
+                        acc = hm::Box::merge(acc, items[task.start + i].box);
+                        right_area[i] = half_area(acc);
+                    }
+                    acc = items[task.start].box;
+                    for (uint32_t i = 1; i < cnt; i++) {          // left = [0, i), right = [i, cnt)
+                        const float c = c_trav + (half_area(acc) * i + right_area[i] * (cnt - i)) * c_isect / parent_area;
+                        if (c < best_cost) { best_cost = c; best_axis = axis; best_mid = i; }
+                        acc = hm::Box::merge(acc, items[task.start + i].box);
+                    }
+                } else {
+                    constexpr int NB = 32;
+                    hm::Box bbox[NB];
+                    uint32_t bcnt[NB] = {0};
+                    const float lo = cb.r[axis].min, ext = cb.r[axis].max - cb.r[axis].min;
+                    for (uint32_t i = task.start; i < task.start + cnt; i++) {
+                        int b = (int)((items[i].centroid[axis] - lo) / ext * NB);
+                        b = b < 0 ? 0 : (b >= NB ? NB - 1 : b);
+                        bbox[b] = bcnt[b] ? hm::Box::merge(bbox[b], items[i].box) : items[i].box;
+                        bcnt[b]++;
+                    }
+                    float ra[NB];
+                    uint32_t rc[NB];
+                    hm::Box acc{};
+                    uint32_t accn = 0;
+                    for (int b = NB - 1; b >= 1; b--) {
+                        if (bcnt[b]) { acc = accn ? hm::Box::merge(acc, bbox[b]) : bbox[b]; accn += bcnt[b]; }
+                        ra[b] = accn ? half_area(acc) : 0.0f;
+                        rc[b] = accn;
+                    }
+                    accn = 0;
+                    for (int b = 0; b < NB - 1; b++) {
+                        if (bcnt[b]) { acc = accn ? hm::Box::merge(acc, bbox[b]) : bbox[b]; accn += bcnt[b]; }
+                        if (accn == 0 || rc[b + 1] == 0) continue;
+                        const float c = c_trav + (half_area(acc) * accn + ra[b + 1] * rc[b + 1]) * c_isect / parent_area;
+                        if (c < best_cost) { best_cost = c; best_axis = axis; best_plane = lo + ext * (float)(b + 1) / NB; best_mid = accn; }
+                    }
+                }
+            }
+        }
+        const float leaf_cost = c_isect * cnt;
+        if (cnt <= leaf_cap && (best_axis < 0 || leaf_cost <= best_cost)) {
+            node.count = cnt;
+            node.index = (uint32_t)t.refs.size();
+            for (uint32_t i = 0; i < cnt; i++) t.refs.push_back(items[task.start + i].index);
+            continue;
+        }
+        uint32_t mid;
+        if (best_axis < 0) {
+            mid = cnt / 2;                                // all centroids equal: split the list
+        } else if (cnt <= sweep_max) {
+            const int axis = best_axis;
+            std::sort(items.begin() + task.start, items.begin() + task.start + cnt,
+                      [axis](const BuildItem &a, const BuildItem &b) {
+                          const float fa = a.centroid[axis], fb = b.centroid[axis];
+                          return fa < fb || (!(fb < fa) && a.index < b.index);
+                      });
+            mid = best_mid;
+        } else {
+            const int axis = best_axis;
+            const float plane = best_plane;
+            auto it = std::partition(items.begin() + task.start, items.begin() + task.start + cnt,
+                                     [axis, plane](const BuildItem &a) { return a.centroid[axis] < plane; });
+            mid = (uint32_t)(it - (items.begin() + task.start));
+            if (mid == 0 || mid == cnt) mid = cnt / 2;
+        }
+        const uint32_t left = node_count++, right = node_count++;
+        (void)right;
+        node.count = 0;
+        node.index = left;
+        stack.push_back({task.start + mid, cnt - mid, left + 1});
+        stack.push_back({task.start, mid, left});
+    }
+    t.nodes.resize(node_count);
+    return t;
+}
+
 // Flattened form of one tree in the node-pair layout.
 struct FlatTree {
     std::vector<NodePair> pairs;   // one per interior node

@@ -56,6 +56,7 @@ rt_status fail(rt_status s, const std::string &msg) {
 
 constexpr uint32_t BLAS_LEAF_CAP = 4;   // BLAS.cuh:17
 constexpr uint32_t TLAS_LEAF_CAP = 2;   // TLAS.cuh:22
+constexpr uint32_t SAH_LEAF_CAP = 4;    // RT_BUILD_SAH: <= 4 items per leaf (2-bit count in a leaf ref)
 
 struct InstState {
     uint32_t ptype, pindex, pcount, blas;
@@ -102,6 +103,7 @@ struct rt_scene {
     Tree tlas;
     FlatTree tlas_flat;
     uint64_t build_seed = 0;
+    rt_build_mode build_mode = RT_BUILD_COMPAT_MEDIAN;
     bool built = false;
     uint64_t frame = 0;
 
@@ -217,7 +219,8 @@ rt_status frame_update(rt_scene *s, uint64_t frame) {
     // TLAS::constructTLAS over transformed instance boxes (Renderer.cu:275, TLAS.cu:4-129)
     std::vector<BuildItem> items(s->inst.size());
     for (size_t i = 0; i < items.size(); i++) items[i] = {s->inst[i].tbox, s->inst[i].tcentroid, (uint32_t)i};
-    s->tlas = build_median_tree(std::move(items), TLAS_LEAF_CAP, hm::tlas_axis_state(s->build_seed, frame));
+    s->tlas = s->build_mode == RT_BUILD_SAH ? build_sah_tree(std::move(items), SAH_LEAF_CAP)
+                                            : build_median_tree(std::move(items), TLAS_LEAF_CAP, hm::tlas_axis_state(s->build_seed, frame));
     s->tlas_flat = flatten_tree(s->tlas, 0, 0, 0, false);
     s->tlas_root_ref = s->tlas_flat.root_ref;
     std::memcpy(s->tlas_root_box, s->tlas_flat.root_box, sizeof s->tlas_root_box);
@@ -329,9 +332,10 @@ rt_status rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
 
 rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
-    if (mode != RT_BUILD_COMPAT_MEDIAN) return fail(RT_ERR_UNSUPPORTED, "unsupported build mode");
+    if (mode != RT_BUILD_COMPAT_MEDIAN && mode != RT_BUILD_SAH) return fail(RT_ERR_UNSUPPORTED, "unsupported build mode");
     HIP_TRY(hipSetDevice(s->device));
     s->build_seed = seed;
+    s->build_mode = mode;
     s->inst.clear();
     s->blas.clear();
 
@@ -376,7 +380,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             std::vector<BuildItem> items(in.pcount);
             for (uint32_t k = 0; k < in.pcount; k++)
                 items[k] = {prim_box(s, in.ptype, in.pindex + k), prim_centroid(s, in.ptype, in.pindex + k), in.pindex + k};
-            bh.tree = build_median_tree(std::move(items), BLAS_LEAF_CAP, hm::blas_axis_state(seed, in.blas));
+            bh.tree = mode == RT_BUILD_SAH ? build_sah_tree(std::move(items), SAH_LEAF_CAP)
+                                           : build_median_tree(std::move(items), BLAS_LEAF_CAP, hm::blas_axis_state(seed, in.blas));
             bh.pair_base = pair_base;
             bh.slot_base = slot_base[in.ptype];
             if ((uint64_t)slot_base[in.ptype] + in.pcount >= MAX_LEAF_SLOTS)

@@ -21,6 +21,7 @@ SPHERE, PARALLELOGRAM, TRIANGLE = 0, 1, 2
 ROUGH, METAL = 0, 1
 
 RT_BUILD_COMPAT_MEDIAN = 0
+RT_BUILD_SAH = 1
 
 RT_RENDER_EXACT = 1 << 0
 RT_RENDER_COUNT_WORK = 1 << 1

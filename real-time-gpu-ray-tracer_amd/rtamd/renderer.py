@@ -41,8 +41,10 @@ class Renderer:
         self.width = self.height = 0
 
     # ---- lifecycle ---------------------------------------------------------------------
-    def build_acceleration_structure(self, seed: int = 0):
-        abi.check(self.lib, self.lib.rt_scene_build(self.h, abi.RT_BUILD_COMPAT_MEDIAN, seed))
+    def build_acceleration_structure(self, seed: int = 0, mode: str = "compat"):
+        """mode "compat": the reference's random-axis median split (pinned seed); "sah": SAH trees."""
+        m = {"compat": abi.RT_BUILD_COMPAT_MEDIAN, "sah": abi.RT_BUILD_SAH}[mode]
+        abi.check(self.lib, self.lib.rt_scene_build(self.h, m, seed))
         return self
 
     def configure_camera(self, width: int, height: int, **camera):

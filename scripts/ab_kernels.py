@@ -26,20 +26,26 @@ def main():
     from rtamd import Renderer, scenes
     torch.cuda.set_device(0)
     cfg = scenes.CONFIGS[a.config]
-    r = Renderer(scenes.config_scene(cfg)).build_acceleration_structure(0).configure_camera(cfg.width, cfg.height)
     fb = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda")
     variants = []
     for v in a.variants:
         name, _, kv = v.partition(":")
         opts = dict(x.split("=") for x in kv.split(",") if x)
-        variants.append((name, {k: int(x) for k, x in opts.items()}))
+        variants.append((name, {k: (x if k == "build" else int(x)) for k, x in opts.items()}))
+    renderers = {}
+    for _, opts in variants:
+        b = opts.get("build", "compat")
+        if b not in renderers:
+            renderers[b] = Renderer(scenes.config_scene(cfg)).build_acceleration_structure(0, mode=b).configure_camera(
+                cfg.width, cfg.height)
     res = {n: [] for n, _ in variants}
     rays = {}
     for rnd in range(a.rounds + 1):
         for name, opts in variants:
             exact = bool(opts.get("exact", 0))
+            r = renderers[opts.get("build", "compat")]
             for k, x in opts.items():
-                if k != "exact":
+                if k not in ("exact", "build"):
                     r.set_option(k, x)
             for f in range(a.frames):
                 _, _, st = r.render(f, exact=exact, want_rgba=False, rgba8_device=fb.data_ptr())
