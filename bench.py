@@ -40,6 +40,10 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="C2")
     p.add_argument("--exact", action="store_true", help="time the EXACT (parity) kernel instead of FAST")
+    p.add_argument("--build", default="sah", choices=("sah", "compat"),
+                   help="BVH builder: SAH (default) or the reference's random-axis median split")
+    p.add_argument("--kernel", type=int, default=1, help="1 = persistent megakernel, 0 = grid kernel")
+    p.add_argument("--threshold", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
@@ -75,13 +79,15 @@ def cpu_baseline(scene, cfg, budget_s):
             "ms_per_frame": round(dt * 1e3 / frames, 2)}
 
 
-def load_traffic(kernel_prefix):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this bench command."""
+def load_traffic(kname):
+    """HBM bytes per launch of this kernel from the committed rocprofv3 PMC summary of the default
+    bench command (profiles/pmc_latest.json, written by scripts/pmc_passes.sh); None if absent."""
     path = os.path.join(REPO, "profiles", "pmc_latest.json")
+    want = ("dev_exact::" if "<exact>" in kname else "dev_fast::") + kname.split("<")[0] + "<"
     try:
         with open(path) as f:
             d = json.load(f)
-        if d.get("kernel", "").startswith(kernel_prefix):
+        if want in d.get("kernel", ""):
             return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
@@ -108,7 +114,9 @@ def main():
 
     cfg = scenes.CONFIGS[args.config]
     scene = scenes.config_scene(cfg)
-    r = Renderer(scene, device=local_rank).build_acceleration_structure(0).configure_camera(cfg.width, cfg.height)
+    r = Renderer(scene, device=local_rank).build_acceleration_structure(0, mode=args.build).configure_camera(
+        cfg.width, cfg.height)
+    r.set_option("kernel", args.kernel).set_option("threshold", args.threshold)
     info = r.info()
     stream = torch.cuda.current_stream().cuda_stream
 
@@ -123,17 +131,17 @@ def main():
     else:
         frame_buf = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda")
 
-    def step(frame):
+    def step(frame, sync=True, keep=False):
+        """One frame; sync=False pipelines it (host TLAS build of the next frame overlaps the GPU)."""
         if n == 1:
-            _, _, st = r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=frame_buf.data_ptr(),
-                                stream=stream)
-            return st
-        _, _, st = r.render(frame, exact=args.exact, want_rgba=False, tiles=tiles, rgba8_device=slab.data_ptr(),
-                            stream=stream)
+            r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=frame_buf.data_ptr(), stream=stream,
+                     sync=sync, keep_counters=keep)
+            return
+        r.render(frame, exact=args.exact, want_rgba=False, tiles=tiles, rgba8_device=slab.data_ptr(), stream=stream,
+                 sync=sync, keep_counters=keep)
         dist.gather(slab, list(gathered.chunk(n)) if rank == 0 else None, dst=0)
         if rank == 0:
             r.assemble_tiles(gathered.data_ptr(), slab_tiles, TILE, TILE, n, frame_buf.data_ptr(), stream)
-        return st
 
     for f in range(args.warmup):
         step(f)
@@ -142,18 +150,18 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
 
-    rays = 0
-    kernel_ms = []
+    r.collect()                                            # drop warm-up timings
     t0 = time.perf_counter()
     for k in range(args.steps):
-        st = step(args.warmup + k)
-        rays += int(st["rays"])
-        kernel_ms.append(st["kernel_ms"])
+        step(args.warmup + k, sync=False, keep=k > 0)
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    acc, kernel_ms = r.collect()                           # device counters + HIP-event kernel times
+    rays = int(acc["rays"])
+    assert len(kernel_ms) == args.steps, (len(kernel_ms), args.steps)
 
     # max over ranks of the elapsed time; total rays over ranks
     if n > 1:
@@ -173,8 +181,8 @@ def main():
         avg_kernel_ms = float(np.mean(kernel_ms))
         bytes_launch = algorithmic_bytes(cst)
         achieved = bytes_launch / (avg_kernel_ms * 1e-3) / 1e9
-        kname = "render_kernel" + ("_exact" if args.exact else "")
-        traffic = load_traffic("rtamd::dev_exact::render_kernel" if args.exact else "rtamd::dev_fast::render_kernel")
+        kname = ("render_persistent_kernel" if args.kernel else "render_kernel") + ("<exact>" if args.exact else "<fast>")
+        traffic = load_traffic(kname)
         value = rays / elapsed / 1e6
         out = {
             "metric": METRIC,
@@ -195,7 +203,9 @@ def main():
                 "triangles": scene.triangle_count, "instances": len(scene.instances),
                 "blas_node_pairs": info["blas_node_pairs"],
                 "parallelism": f"screen-tiles{n} ({TILE}x{TILE} interleaved, RCCL gather)" if n > 1 else "single-gpu",
-                "kernel": "EXACT" if args.exact else "FAST",
+                "kernel": ("EXACT" if args.exact else "FAST") + (" persistent" if args.kernel else " grid"),
+                "bvh": args.build,
+                "frames": "animated (Main.cu updateInstance), per-frame TLAS rebuild + upload, pipelined",
             },
             "rays_per_frame": round(rays / args.steps, 1),
             "kernel_ms": round(avg_kernel_ms, 4),

@@ -161,7 +161,8 @@ typedef enum rt_render_flags {
     RT_RENDER_EXACT = 1u << 0,        /* bit-faithful arithmetic (IEEE division, no FMA) */
     RT_RENDER_COUNT_WORK = 1u << 1,   /* fill rt_stats work counters (slower)              */
     RT_RENDER_NO_SYNC = 1u << 2,      /* return after enqueue (device outputs only)        */
-    RT_RENDER_SKIP_UPDATE = 1u << 3   /* do not run the instance update / TLAS rebuild     */
+    RT_RENDER_SKIP_UPDATE = 1u << 3,  /* do not run the instance update / TLAS rebuild     */
+    RT_RENDER_KEEP_COUNTERS = 1u << 4 /* accumulate device counters (see rt_scene_collect) */
 } rt_render_flags;
 
 /* Per-call options for rt_render.  Zero-initialise, then set what you need. */
@@ -264,6 +265,13 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "variant"   : persistent kernel register budget: 0 = compiler's choice, 4 / 5 = at least
  *                 4 / 5 waves per SIMD                                                          */
 rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
+
+/* Pipelined frames (RT_RENDER_NO_SYNC): wait for the last enqueued frame, return the device
+ * counters accumulated since the last frame rendered without RT_RENDER_KEEP_COUNTERS (rays, pixels
+ * and, with RT_RENDER_COUNT_WORK, the work counters) and the kernel duration of every frame
+ * rendered since the previous collect (HIP events on the kernel's stream; up to 256 kept). */
+rt_status rt_scene_collect(rt_scene *scene, rt_stats *accumulated, float *kernel_ms, uint32_t capacity,
+                           uint32_t *count);
 
 /* Blocks until all work the scene enqueued has finished. */
 rt_status rt_synchronize(rt_scene *scene);

@@ -130,6 +130,11 @@ struct rt_scene {
 
     hipStream_t stream = nullptr;
     hipEvent_t k_start = nullptr, k_stop = nullptr;
+    // per-frame kernel timing ring for pipelined frames (rt_scene_collect)
+    static constexpr uint32_t RING = 256;
+    hipEvent_t ring_start[RING] = {}, ring_stop[RING] = {};
+    uint32_t ring_head = 0, ring_pending = 0;
+    hipStream_t last_stream = nullptr;
     // persistent megakernel: work-queue head, grid size (#CUs x resident blocks), refill threshold
     uint32_t *queue = nullptr;
     uint32_t cus = 0;
@@ -162,6 +167,10 @@ struct rt_scene {
         if (counters) (void)hipFree(counters);
         if (queue) (void)hipFree(queue);
         if (counters_host) (void)hipHostFree(counters_host);
+        for (uint32_t i = 0; i < RING; i++) {
+            if (ring_start[i]) (void)hipEventDestroy(ring_start[i]);
+            if (ring_stop[i]) (void)hipEventDestroy(ring_stop[i]);
+        }
         if (k_start) (void)hipEventDestroy(k_start);
         if (k_stop) (void)hipEventDestroy(k_stop);
         if (stream) (void)hipStreamDestroy(stream);
@@ -284,6 +293,8 @@ uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t tw, uint32_t th, uint32
 }
 
 }  // namespace
+
+static void fill_stats(rt_stats *st, const unsigned long long *c);
 
 extern "C" {
 
@@ -470,6 +481,10 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     }
     if (!s->k_start) HIP_TRY(hipEventCreate(&s->k_start));
     if (!s->k_stop) HIP_TRY(hipEventCreate(&s->k_stop));
+    for (uint32_t i = 0; i < rt_scene::RING; i++) {
+        if (!s->ring_start[i]) HIP_TRY(hipEventCreate(&s->ring_start[i]));
+        if (!s->ring_stop[i]) HIP_TRY(hipEventCreate(&s->ring_stop[i]));
+    }
     if (!s->counters) HIP_TRY(hipMalloc(&s->counters, CNT_NUM * sizeof(unsigned long long)));
     if (!s->queue) HIP_TRY(hipMalloc(&s->queue, 16));
     {
@@ -601,7 +616,13 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     const bool count = (o.flags & RT_RENDER_COUNT_WORK) != 0;
 
     HIP_TRY(hipStreamWaitEvent(stream, s->ev_copied[s->active], 0));
-    HIP_TRY(hipMemsetAsync(s->counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
+    if (!(o.flags & RT_RENDER_KEEP_COUNTERS))
+        HIP_TRY(hipMemsetAsync(s->counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
+    const uint32_t slot = s->ring_head;
+    s->ring_head = (s->ring_head + 1) % rt_scene::RING;
+    if (s->ring_pending < rt_scene::RING) s->ring_pending++;
+    s->last_stream = stream;
+    HIP_TRY(hipEventRecord(s->ring_start[slot], stream));
     HIP_TRY(hipEventRecord(s->k_start, stream));
     if (s->use_persistent)
         HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, s->counters, s->queue,
@@ -614,6 +635,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, s->counters, stream)
                       : launch_render_fast(g, cam, out, count, s->counters, stream));
     HIP_TRY(hipEventRecord(s->k_stop, stream));
+    HIP_TRY(hipEventRecord(s->ring_stop[slot], stream));
     HIP_TRY(hipEventRecord(s->ev_used[s->active], stream));
     if (o.flags & RT_RENDER_NO_SYNC) {
         if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; }
@@ -621,20 +643,13 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     }
     HIP_TRY(hipMemcpyAsync(s->counters_host, s->counters, CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
+    s->ring_pending = 0;
     if (rgba_host) HIP_TRY(hipMemcpy(rgba_host, out.rgba, npix * 4, hipMemcpyDeviceToHost));
     if (rgb_host) HIP_TRY(hipMemcpy(rgb_host, out.rgb, npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
     if (stats) {
         float kms = 0.0f;
         HIP_TRY(hipEventElapsedTime(&kms, s->k_start, s->k_stop));
-        const unsigned long long *c = s->counters_host;
-        stats->rays = c[CNT_RAYS];
-        stats->pixels = c[CNT_PIXELS];
-        stats->aabb_tests = 2ull * c[CNT_PAIRS];
-        stats->triangle_tests = c[CNT_TRI];
-        stats->sphere_quad_tests = c[CNT_SPHQUAD];
-        stats->quad_tests = c[CNT_QUAD];
-        stats->instance_visits = c[CNT_INST];
-        stats->hits = c[CNT_HITS];
+        fill_stats(stats, s->counters_host);
         stats->kernel_ms = kms;
         stats->update_ms = update_ms;
         stats->frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
@@ -696,6 +711,40 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else {
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown option " + k);
     }
+    return RT_OK;
+}
+
+static void fill_stats(rt_stats *st, const unsigned long long *c) {
+    std::memset(st, 0, sizeof *st);
+    st->rays = c[CNT_RAYS];
+    st->pixels = c[CNT_PIXELS];
+    st->aabb_tests = 2ull * c[CNT_PAIRS];
+    st->triangle_tests = c[CNT_TRI];
+    st->sphere_quad_tests = c[CNT_SPHQUAD];
+    st->quad_tests = c[CNT_QUAD];
+    st->instance_visits = c[CNT_INST];
+    st->hits = c[CNT_HITS];
+}
+
+rt_status rt_scene_collect(rt_scene *s, rt_stats *acc, float *kernel_ms, uint32_t capacity, uint32_t *count) {
+    if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
+    if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
+    HIP_TRY(hipSetDevice(s->device));
+    if (s->last_stream) HIP_TRY(hipStreamSynchronize(s->last_stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    HIP_TRY(hipMemcpy(s->counters_host, s->counters, CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    if (acc) fill_stats(acc, s->counters_host);
+    const uint32_t n = s->ring_pending;
+    uint32_t written = 0;
+    for (uint32_t k = 0; k < n; k++) {
+        const uint32_t slot = (s->ring_head + rt_scene::RING - n + k) % rt_scene::RING;
+        float ms = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&ms, s->ring_start[slot], s->ring_stop[slot]));
+        if (kernel_ms && written < capacity) kernel_ms[written] = ms;
+        written++;
+    }
+    if (count) *count = written < capacity ? written : capacity;
+    s->ring_pending = 0;
     return RT_OK;
 }
 

@@ -27,6 +27,7 @@ RT_RENDER_EXACT = 1 << 0
 RT_RENDER_COUNT_WORK = 1 << 1
 RT_RENDER_NO_SYNC = 1 << 2
 RT_RENDER_SKIP_UPDATE = 1 << 3
+RT_RENDER_KEEP_COUNTERS = 1 << 4
 
 MISS = 0xFFFFFFFF
 
@@ -130,6 +131,7 @@ EXPORTED_SYMBOLS = (
     "rt_camera_set", "rt_scene_update", "rt_render", "rt_assemble_tiles", "rt_tiles_for_rank",
     "rt_trace_rays", "rt_synchronize", "rt_scene_destroy", "rt_scene_get_info",
     "rt_scene_export_blas", "rt_scene_export_tlas", "rt_demo_update", "rt_scene_set_option",
+    "rt_scene_collect",
 )
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -167,6 +169,8 @@ def _declare(lib):
                  "rt_assemble_tiles", "rt_trace_rays", "rt_synchronize", "rt_scene_get_info",
                  "rt_scene_export_blas", "rt_scene_export_tlas"):
         getattr(lib, name).restype = C.c_int
+    lib.rt_scene_collect.argtypes = [C.c_void_p, P(Stats), P(C.c_float), C.c_uint32, P(C.c_uint32)]
+    lib.rt_scene_collect.restype = C.c_int
     lib.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
     lib.rt_scene_set_option.restype = C.c_int
     lib.rt_demo_update.argtypes = [C.c_void_p, P(Xform), C.c_size_t, C.c_uint64]

@@ -62,13 +62,15 @@ class Renderer:
 
     def render(self, frame: int = 0, frame_seed: int = 0x5EED, exact: bool = False, count_work: bool = False,
                want_rgb: bool = False, want_rgba: bool = True, skip_update: bool = False,
-               tiles=None, rgba8_device=None, rgb32_device=None, stream=None, sync: bool = True):
+               tiles=None, rgba8_device=None, rgb32_device=None, stream=None, sync: bool = True,
+               keep_counters: bool = False):
         """One frame.  Returns (rgba[H,W,4] uint8 | None, rgb[H,W,3] float32 | None, stats dict).
         tiles = (tile_w, tile_h, rank, count) renders a tile shard into tile-compact outputs."""
         o = abi.RenderOpts()
         o.frame_seed = frame_seed
         o.flags = (abi.RT_RENDER_EXACT if exact else 0) | (abi.RT_RENDER_COUNT_WORK if count_work else 0) | \
-                  (abi.RT_RENDER_SKIP_UPDATE if skip_update else 0) | (0 if sync else abi.RT_RENDER_NO_SYNC)
+                  (abi.RT_RENDER_SKIP_UPDATE if skip_update else 0) | (0 if sync else abi.RT_RENDER_NO_SYNC) | \
+                  (abi.RT_RENDER_KEEP_COUNTERS if keep_counters else 0)
         if tiles is not None:
             o.tile_w, o.tile_h, o.tile_rank, o.tile_count = tiles
             npix = self.tiles_for_rank(*tiles) * tiles[0] * tiles[1]
@@ -86,6 +88,14 @@ class Renderer:
                                                rgb.ctypes.data if rgb is not None else None, C.byref(st)))
         stats = {k: getattr(st, k) for k, _ in abi.Stats._fields_}
         return rgba, rgb, stats
+
+    def collect(self, capacity: int = 256):
+        """After pipelined renders: (accumulated stats dict, list of per-frame kernel ms)."""
+        st = abi.Stats()
+        ms = (C.c_float * capacity)()
+        n = C.c_uint32()
+        abi.check(self.lib, self.lib.rt_scene_collect(self.h, C.byref(st), ms, capacity, C.byref(n)))
+        return {k: getattr(st, k) for k, _ in abi.Stats._fields_}, [ms[i] for i in range(n.value)]
 
     def tiles_for_rank(self, tile_w, tile_h, rank, count):
         return int(self.lib.rt_tiles_for_rank(self.h, tile_w, tile_h, rank, count))

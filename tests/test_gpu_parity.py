@@ -248,3 +248,16 @@ def test_sah_trees_within_tolerance(gpu_lib, depth, need):
         f, mx = frac_within(rgba, orgba)
         assert f >= need, (exact, f, mx)
         assert abs(st["rays"] - ocnt["rays"]) <= 0.001 * ocnt["rays"]
+
+
+def test_pipelined_frames_collect(gpu_lib):
+    """NO_SYNC frames with accumulated counters == the sum of synchronous frames; one kernel time
+    per frame is collected from the event ring."""
+    s = scenes.demo_with_particles(8)
+    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(256, 144, ray_trace_depth=2)
+    rays = [r.render(f)[2]["rays"] for f in range(5)]
+    r.collect()
+    for f in range(5):
+        r.render(f, sync=False, keep_counters=f > 0, want_rgba=False)
+    acc, kms = r.collect()
+    assert acc["rays"] == sum(rays) and len(kms) == 5 and all(k > 0 for k in kms)
