@@ -37,10 +37,12 @@ def prim_kats(seed=1234, n=4096):
     prims["tri"] = t
     fns = {"sphere": lib().oracle_hit_sphere, "quad": lib().oracle_hit_parallelogram, "tri": lib().oracle_hit_triangle}
     out = {}
+    aim = {"sphere": ((0.3, -0.2, 0.1), 1.6), "quad": ((0.1, 0.5, 0.4), 1.4), "tri": ((0.1, -0.2, 0.1), 1.1)}
     for k, p in prims.items():
         o = g.uniform(-3, 3, (n, 3))
         o[:, 2] = g.uniform(2.5, 5, n)
-        tgt = g.uniform(-1.6, 1.6, (n, 3))
+        c, ext = aim[k]
+        tgt = np.asarray(c) + g.uniform(-ext, ext, (n, 3))     # aimed near the primitive: ~half hit
         d = tgt - o
         d *= g.uniform(0.5, 2.0, (n, 1)) / np.linalg.norm(d, axis=1, keepdims=True)   # unnormalised too
         rays = np.concatenate([o, d], 1).astype(np.float32)
