@@ -59,7 +59,8 @@ def prim_kats(seed=1234, n=4096):
     b6 = np.stack([boxes[:, 0], boxes[:, 0] + ext[:, 0], boxes[:, 1], boxes[:, 1] + ext[:, 1],
                    boxes[:, 2], boxes[:, 2] + ext[:, 2]], 1).astype(np.float32)
     o = g.uniform(-4, 4, (n, 3))
-    d = g.normal(size=(n, 3))
+    centre = boxes + ext / 2
+    d = (centre - o) + g.normal(size=(n, 3)) * 0.8      # aimed at the box: roughly half hit
     d[g.random(n) < 0.1, 0] = 0.0                      # parallel-axis branch
     rays = np.concatenate([o, d], 1).astype(np.float32)
     res = np.zeros((n, 2), np.float32)
