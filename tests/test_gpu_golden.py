@@ -55,3 +55,58 @@ def test_image_crops(gpu_lib, vec, name):
     fast, _, _ = r.render(frame)
     d = np.abs(fast[y0:y0 + h, x0:x0 + w].astype(int) - vec[f"img_{name}_rgba"].astype(int)).max(axis=2)
     assert (d <= 1).mean() >= 0.995
+
+
+def _single_prim_scene(kind, prim):
+    from rtamd import abi
+    s = scenes.demo_scene()
+    s.animated = False
+    if kind == "sphere":
+        s.spheres = [(abi.ROUGH, 0, prim.center.tuple(), prim.radius)]
+        s.instances = [dict(type=abi.SPHERE, index=0)]
+    elif kind == "quad":
+        s.parallelograms = [(abi.ROUGH, 0, prim.q.tuple(), prim.u.tuple(), prim.v.tuple())]
+        s.instances = [dict(type=abi.PARALLELOGRAM, index=0)]
+    else:
+        t = np.zeros(1, dtype=scenes.TRIANGLE_DTYPE)
+        t["vertex"][0] = [prim.vertex[i].tuple() for i in range(3)]
+        t["normal"][0] = [prim.normal[i].tuple() for i in range(3)]
+        t["has_normals"] = prim.has_normals
+        s.triangles = t
+        s.instances = [dict(type=abi.TRIANGLE, index=0)]
+    return s
+
+
+@pytest.mark.parametrize("kind", ["sphere", "tri", "quad"])
+def test_prim_kats_through_trace(gpu_lib, kind):
+    """The KAT rays traced through a one-primitive scene (identity instance): t bit-identical to the
+    oracle's single-primitive hit function; the parallelogram's hits are additionally clipped by its
+    q-centred box (Parallelogram.cu:48-50), so there the GPU hits must be a subset."""
+    from rtamd import abi
+    g = np.load(os.path.join(GOLDEN, "prim_kats.npz"))
+    rays, out = g[f"{kind}_rays"], g[f"{kind}_out"]
+    prims = {
+        "sphere": abi.Sphere(abi.Vec3(0.3, -0.2, 0.1), 1.3, 0, 0),
+        "quad": abi.Parallelogram(abi.Vec3(-1, -0.5, 0.2), abi.Vec3(2, 0.3, 0), abi.Vec3(0.2, 1.7, 0.4), 0, 0),
+    }
+    if kind == "tri":
+        t = abi.Triangle()
+        for i, v in enumerate(((-1, -1, 0.1), (1.2, -0.8, -0.2), (0.1, 1.1, 0.3))):
+            t.vertex[i] = abi.Vec3(*v)
+        for i, v in enumerate(((0, 0, 1), (0.3, 0, 0.95), (0, 0.3, 0.95))):
+            t.normal[i] = abi.Vec3(*v)
+        t.has_normals = 1
+        prims["tri"] = t
+    r = Renderer(_single_prim_scene(kind, prims[kind]), update=False).build_acceleration_structure(0)
+    h = r.trace_rays(rays, exact=True)
+    gpu_hit = h["instance"] != 0xFFFFFFFF
+    kat_hit = out[:, 0] > 0
+    if kind == "quad":
+        assert not (gpu_hit & ~kat_hit).any()
+        assert gpu_hit.sum() >= 0.5 * kat_hit.sum()
+    else:
+        assert np.array_equal(gpu_hit, kat_hit)
+    m = gpu_hit
+    assert np.array_equal(h["t"][m], out[m, 1])
+    assert np.array_equal(h["point"][m], out[m, 2:5])
+    assert np.abs(h["normal"][m] - out[m, 5:8]).max() <= 2e-7
