@@ -141,6 +141,13 @@ struct rt_scene {
     uint32_t threshold = 16;
     uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4, 5)
     bool use_persistent = true;
+    uint32_t queue_parts = 4;       // measured: 4 bands beat 1 (global queue) and 8 on C2
+    bool timeline_on = false;
+    bool costmap_on = false;
+    DevBuf<uint32_t> costmap;
+    size_t costmap_pixels = 0;
+    DevBuf<unsigned long long> timeline;
+    uint32_t timeline_waves = 0;    // waves of the last launch that recorded a timeline
     unsigned long long *counters = nullptr;       // HBM CNT_NUM
     unsigned long long *counters_host = nullptr;  // pinned
 
@@ -158,6 +165,7 @@ struct rt_scene {
         if (stream) (void)hipStreamSynchronize(stream);
         blas_pairs.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
         quad_hot.release(); quad_cold.release(); materials.release(); out_rgba.release(); out_rgb.release();
+        timeline.release(); costmap.release();
         for (int b = 0; b < 2; b++) {
             if (staging[b]) (void)hipHostFree(staging[b]);
             if (frame_dev[b]) (void)hipFree(frame_dev[b]);
@@ -486,7 +494,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         if (!s->ring_stop[i]) HIP_TRY(hipEventCreate(&s->ring_stop[i]));
     }
     if (!s->counters) HIP_TRY(hipMalloc(&s->counters, CNT_NUM * sizeof(unsigned long long)));
-    if (!s->queue) HIP_TRY(hipMalloc(&s->queue, 16));
+    if (!s->queue) HIP_TRY(hipMalloc(&s->queue, QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t)));
     {
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, s->device));
@@ -615,6 +623,32 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     const bool exact = (o.flags & RT_RENDER_EXACT) != 0;
     const bool count = (o.flags & RT_RENDER_COUNT_WORK) != 0;
 
+    if (s->use_persistent) {
+        out.queue_parts = s->queue_parts;
+        if (s->timeline_on) {
+            const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant)
+                                                    : persistent_blocks_per_cu_fast(s->variant));
+            const size_t words = (size_t)blocks * 4 * TIMELINE_WORDS;
+            if (s->timeline.n < words) {
+                s->timeline.release();
+                HIP_TRY(hipMalloc(&s->timeline.p, words * sizeof(unsigned long long)));
+                s->timeline.n = words;
+            }
+            HIP_TRY(hipMemsetAsync(s->timeline.p, 0, words * sizeof(unsigned long long), stream));
+            out.timeline = s->timeline.p;
+            s->timeline_waves = blocks * 4;
+        }
+        if (s->costmap_on && count) {
+            if (s->costmap.n < npix) {
+                s->costmap.release();
+                HIP_TRY(hipMalloc(&s->costmap.p, npix * sizeof(uint32_t)));
+                s->costmap.n = npix;
+            }
+            HIP_TRY(hipMemsetAsync(s->costmap.p, 0, npix * sizeof(uint32_t), stream));
+            out.costmap = s->costmap.p;
+            s->costmap_pixels = npix;
+        }
+    }
     HIP_TRY(hipStreamWaitEvent(stream, s->ev_copied[s->active], 0));
     if (!(o.flags & RT_RENDER_KEEP_COUNTERS))
         HIP_TRY(hipMemsetAsync(s->counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
@@ -708,9 +742,42 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "variant") {
         if (value != 0 && value != 4 && value != 5) return fail(RT_ERR_INVALID_ARGUMENT, "variant must be 0, 4 or 5");
         s->variant = (uint32_t)value;
+    } else if (k == "queue_parts") {
+        if (value < 1 || value > (int64_t)QUEUE_MAX_PARTS) return fail(RT_ERR_INVALID_ARGUMENT, "queue_parts must be in 1..8");
+        s->queue_parts = (uint32_t)value;
+    } else if (k == "timeline") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "timeline must be 0 or 1");
+        s->timeline_on = value == 1;
+    } else if (k == "costmap") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
+        s->costmap_on = value == 1;
     } else {
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown option " + k);
     }
+    return RT_OK;
+}
+
+rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t capacity, size_t *bytes) {
+    if (!s || !name || !bytes || (!dst && capacity)) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
+    *bytes = 0;
+    const std::string k(name);
+    const void *src = nullptr;
+    size_t size = 0;
+    if (k == "timeline") {
+        src = s->timeline.p;
+        size = (size_t)s->timeline_waves * TIMELINE_WORDS * sizeof(uint64_t);
+    } else if (k == "costmap") {
+        src = s->costmap.p;
+        size = s->costmap_pixels * sizeof(uint32_t);
+    } else {
+        return fail(RT_ERR_INVALID_ARGUMENT, "unknown debug buffer " + k);
+    }
+    if (!src || size == 0) return fail(RT_ERR_STATE, "debug buffer " + k + " not recorded (set the option first)");
+    HIP_TRY(hipSetDevice(s->device));
+    if (s->last_stream) HIP_TRY(hipStreamSynchronize(s->last_stream));
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    if (capacity) HIP_TRY(hipMemcpy(dst, src, capacity < size ? capacity : size, hipMemcpyDeviceToHost));
+    *bytes = size;
     return RT_OK;
 }
 

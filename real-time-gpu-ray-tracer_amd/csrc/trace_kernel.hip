@@ -546,16 +546,39 @@ __device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEn
     if (T.cur == REF_NONE) T.tracing = false;
 }
 
+#ifndef RT_DIAG
+#define RT_DIAG 0
+#endif
+// Diagnostic builds (make diag -> librtamd_diag.so): wave-uniform cycle stamps per phase.
+struct PhaseCycles { unsigned long long refill, interior, leaf, shade; };
+__device__ __forceinline__ unsigned long long stamp() {
+    unsigned long long t;
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    return t;
+}
+#if RT_DIAG
+#define DIAG_T(var) const unsigned long long var = stamp()
+#define DIAG_ADD(acc, t0) (acc) += stamp() - (t0)
+#else
+#define DIAG_T(var) (void)0
+#define DIAG_ADD(acc, t0) (void)0
+#endif
+
 // One round: interior loop until every traversing lane holds a leaf, then the leaf phase.
 template <bool COUNT>
-__device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
+__device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt,
+                                           PhaseCycles &pc) {
+    DIAG_T(t0);
     for (;;) {
         if (T.tracing && T.pleaf == REF_NONE && T.cur == REF_NONE) T.tracing = false;   // done, no leaf left
         if (!__any(T.tracing && T.pleaf == REF_NONE)) break;
         const bool active = T.tracing && T.cur != REF_NONE && (!(T.cur & REF_LEAF) || T.pleaf == REF_NONE);
         if (active) spec_interior_step<COUNT>(T, sc, spill, cnt);
     }
+    DIAG_ADD(pc.interior, t0);
+    DIAG_T(t1);
     if (T.tracing) spec_leaf_phase<COUNT>(T, sc, spill, cnt);
+    DIAG_ADD(pc.leaf, t1);
 }
 
 template <bool COUNT>
@@ -735,6 +758,18 @@ __global__ __launch_bounds__(BLOCK) void render_kernel(SceneGPU sc, CameraGPU ca
 // work queue).  Lanes are refilled from a per-wave pool of 64 consecutive work items claimed with
 // one atomic per pool (ballot-compacted lane refill).  Each pixel's RNG stream
 // is consumed in exactly the reference order, so the image equals the grid kernel's bit for bit.
+// XCD (XCC) of the executing wave, 0..7, and the raw HW_ID register (CU / SE / SIMD of the wave).
+__device__ __forceinline__ uint32_t xcc_id() {
+    uint32_t v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(v));
+    return v;
+}
+__device__ __forceinline__ uint32_t hw_id() {
+    uint32_t v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
+    return v;
+}
+
 __device__ __forceinline__ bool map_item(const OutputGPU &out, const CameraGPU &cam, uint32_t item,
                                          uint32_t &px, uint32_t &py, uint32_t &oi) {
     const uint32_t wunit = item >> 6, l = item & 63u;
@@ -790,7 +825,6 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     __shared__ unsigned long long lds_stack[LDS_DEPTH][BLOCK];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const uint32_t total = out.units * 64u;
 
     Trav T;
     T.stk.lds = (LdsU2 *)&lds_stack[0][tid];
@@ -801,6 +835,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     uint32_t rays = 0, pixels = 0;
 
     bool has = false;                  // lane owns a pixel
+    uint32_t px_rounds = 0;            // COUNT: traversal rounds spent on the lane's pixel
     uint32_t item = 0, sample = 0, depth = 0;
     Rng rng;
     rng.s = 0;
@@ -808,19 +843,40 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     uint32_t pool_next = 0, pool_end = 0;     // wave-uniform
     bool exhausted = false;                   // wave-uniform
     const uint32_t S2 = cam.sqrt_s * cam.sqrt_s;
+    // Work queue: the frame's units are split into `parts` bands; a wave drains the band of its own
+    // XCD first (primary rays of one band share geometry in that XCD's L2), then steals from the others.
+    const uint32_t parts = out.queue_parts;
+    const uint32_t xcc = xcc_id();
+    uint32_t part = xcc % parts, tried = 0;
+    unsigned long long t_start = 0, t_exhaust = 0;
+    uint32_t n_rounds = 0, n_shades = 0, n_grabs = 0;      // wave-uniform (timeline)
+    PhaseCycles pc = {0, 0, 0, 0};
+    if (out.timeline) t_start = __builtin_amdgcn_s_memrealtime();
 
     for (;;) {
         // ---- refill idle lanes from the wave's pool / the global queue
+        DIAG_T(t_refill);
         uint64_t need = __ballot(!has);
         while (need && !exhausted) {
             const uint32_t n_need = __popcll(need);
             if (pool_next >= pool_end) {
+                const uint32_t p_begin = (uint32_t)(((uint64_t)out.units * part) / parts) * 64u;
+                const uint32_t p_end = (uint32_t)(((uint64_t)out.units * (part + 1)) / parts) * 64u;
                 uint32_t b = 0;
-                if (lane == 0) b = atomicAdd(queue, 64u);
-                b = __shfl(b, 0, 64);
-                if (b >= total) { exhausted = true; break; }
+                if (lane == 0) b = atomicAdd(queue + part * QUEUE_STRIDE, 64u);
+                b = p_begin + __shfl(b, 0, 64);
+                n_grabs++;
+                if (b >= p_end) {
+                    if (++tried >= parts) {
+                        exhausted = true;
+                        if (out.timeline) t_exhaust = __builtin_amdgcn_s_memrealtime();
+                        break;
+                    }
+                    part = part + 1 == parts ? 0 : part + 1;
+                    continue;
+                }
                 pool_next = b;
-                pool_end = min(b + 64u, total);
+                pool_end = min(b + 64u, p_end);
             }
             const uint32_t take = min(n_need, pool_end - pool_next);
             const uint32_t rank = __popcll(need & ((1ull << lane) - 1ull));
@@ -834,6 +890,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     acc = mk(0.0f, 0.0f, 0.0f);
                     thr = mk(1.0f, 1.0f, 1.0f);
                     sample = 0; depth = 0;
+                    px_rounds = 0;
                     f3 o, d;
                     camera_ray(cam, px, py, 0, rng, o, d);
                     trav_init(T, sc, o, d);
@@ -843,6 +900,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             pool_next += take;
             need = __ballot(!has);          // lanes handed an out-of-frame item (edge units) retry
         }
+        DIAG_ADD(pc.refill, t_refill);
         if (!__any(has)) {
             if (exhausted) break;
             continue;
@@ -853,9 +911,13 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             if (tr == 0) break;
             const uint64_t want = __ballot(!T.tracing && (has || !exhausted));
             if ((uint32_t)__popcll(want) >= threshold) break;
-            spec_round<COUNT>(T, sc, spill, cnt);
+            spec_round<COUNT>(T, sc, spill, cnt, pc);
+            n_rounds++;
+            if (COUNT) px_rounds += T.tracing ? 1u : 0u;
         }
         // ---- shade lanes whose segment finished (rayColor body, Kernel.cu:64-100)
+        n_shades++;
+        DIAG_T(t_shade);
         if (has && !T.tracing) {
             rays++;
             bool path_done;
@@ -896,11 +958,13 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     camera_ray(cam, px, py, sample, rng, no, nd);
                 } else {
                     write_pixel(out, oi, scl(acc, cam.recip_sqrt * cam.recip_sqrt));   // Kernel.cu:143-146
+                    if (COUNT && out.costmap) out.costmap[oi] = px_rounds;
                     has = false;
                 }
             }
             if (has) trav_init(T, sc, no, nd);
         }
+        DIAG_ADD(pc.shade, t_shade);
     }
 
     const uint32_t wr = wave_sum(rays);
@@ -921,6 +985,21 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     if (lane == 0) {
         atomicAdd(&counters[CNT_RAYS], (unsigned long long)wr);
         atomicAdd(&counters[CNT_PIXELS], (unsigned long long)wp);
+        if (out.timeline) {
+            unsigned long long *w = out.timeline + (unsigned long long)TIMELINE_WORDS * (blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6));
+            w[0] = t_start;
+            w[1] = __builtin_amdgcn_s_memrealtime();
+            w[2] = ((unsigned long long)hw_id() << 32) | xcc;
+            w[3] = wp;
+            w[4] = t_exhaust;
+            w[5] = n_rounds;
+            w[6] = n_shades;
+            w[7] = n_grabs;
+            w[8] = pc.refill;
+            w[9] = pc.interior;
+            w[10] = pc.leaf;
+            w[11] = pc.shade;
+        }
     }
 }
 
@@ -1001,7 +1080,7 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
                                                unsigned long long *counters, uint32_t *queue, uint32_t blocks,
                                                uint32_t threshold, uint32_t variant, hipStream_t stream) {
     if (out.units == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(queue, 0, sizeof(uint32_t), stream);
+    hipError_t e = hipMemsetAsync(queue, 0, QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
     if (variant == 4) return launch_persistent_wpe<4>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     if (variant == 5) return launch_persistent_wpe<5>(sc, cam, out, count, counters, queue, blocks, threshold, stream);

@@ -131,7 +131,7 @@ EXPORTED_SYMBOLS = (
     "rt_camera_set", "rt_scene_update", "rt_render", "rt_assemble_tiles", "rt_tiles_for_rank",
     "rt_trace_rays", "rt_synchronize", "rt_scene_destroy", "rt_scene_get_info",
     "rt_scene_export_blas", "rt_scene_export_tlas", "rt_demo_update", "rt_scene_set_option",
-    "rt_scene_collect",
+    "rt_scene_collect", "rt_scene_debug_read",
 )
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -173,6 +173,8 @@ def _declare(lib):
     lib.rt_scene_collect.restype = C.c_int
     lib.rt_scene_set_option.argtypes = [C.c_void_p, C.c_char_p, C.c_int64]
     lib.rt_scene_set_option.restype = C.c_int
+    lib.rt_scene_debug_read.argtypes = [C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t, P(C.c_size_t)]
+    lib.rt_scene_debug_read.restype = C.c_int
     lib.rt_demo_update.argtypes = [C.c_void_p, P(Xform), C.c_size_t, C.c_uint64]
     lib.rt_demo_update.restype = None
     return lib
@@ -186,7 +188,7 @@ def load_library(path: str | None = None):
     global _LIB
     if _LIB is not None and path is None:
         return _LIB
-    p = path or LIB_PATH
+    p = path or os.environ.get("RTAMD_LIB") or LIB_PATH   # RTAMD_LIB: diagnostic builds (make DIAG=1)
     if not os.path.exists(p):
         raise RtError(f"librtamd.so not built ({p}); run __graft_entry__.build()")
     lib = _declare(C.CDLL(p, mode=C.RTLD_GLOBAL))

@@ -97,6 +97,33 @@ class Renderer:
         abi.check(self.lib, self.lib.rt_scene_collect(self.h, C.byref(st), ms, capacity, C.byref(n)))
         return {k: getattr(st, k) for k, _ in abi.Stats._fields_}, [ms[i] for i in range(n.value)]
 
+    def debug_read(self, name: str) -> np.ndarray:
+        """Debug buffer of the last launch that recorded it ("timeline", "costmap"), as raw bytes."""
+        n = C.c_size_t()
+        abi.check(self.lib, self.lib.rt_scene_debug_read(self.h, name.encode(), None, 0, C.byref(n)))
+        buf = np.zeros(n.value, np.uint8)
+        abi.check(self.lib, self.lib.rt_scene_debug_read(self.h, name.encode(), buf.ctypes.data, n.value, C.byref(n)))
+        return buf
+
+    def timeline(self):
+        """Per-wave timeline of the last persistent launch (set_option("timeline", 1) first).
+        Structured array: start/end in s_memrealtime ticks (100 MHz), xcc, hw_id, pixels."""
+        w = self.debug_read("timeline").view(np.uint64).reshape(-1, 12)
+        out = np.zeros(len(w), dtype=[("start", np.uint64), ("end", np.uint64), ("xcc", np.uint32),
+                                      ("hw_id", np.uint32), ("pixels", np.uint32), ("exhaust", np.uint64),
+                                      ("rounds", np.uint32), ("shades", np.uint32), ("grabs", np.uint32),
+                                      ("cyc_refill", np.uint64), ("cyc_interior", np.uint64), ("cyc_leaf", np.uint64),
+                                      ("cyc_shade", np.uint64)])
+        out["start"], out["end"], out["exhaust"] = w[:, 0], w[:, 1], w[:, 4]
+        out["xcc"], out["hw_id"], out["pixels"] = w[:, 2] & 0xFFFFFFFF, w[:, 2] >> 32, w[:, 3]
+        out["rounds"], out["shades"], out["grabs"] = w[:, 5], w[:, 6], w[:, 7]
+        out["cyc_refill"], out["cyc_interior"], out["cyc_leaf"], out["cyc_shade"] = w[:, 8], w[:, 9], w[:, 10], w[:, 11]
+        return out
+
+    def costmap(self):
+        """Traversal rounds per output pixel of the last COUNT_WORK render with option "costmap"."""
+        return self.debug_read("costmap").view(np.uint32)
+
     def tiles_for_rank(self, tile_w, tile_h, rank, count):
         return int(self.lib.rt_tiles_for_rank(self.h, tile_w, tile_h, rank, count))
 

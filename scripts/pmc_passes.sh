@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 PMC passes (one counter group per run; --pmc is never combined with tracing domains).
 # usage: pmc_passes.sh OUTDIR KERNEL_SUBSTRING -- command...
+# (TA_* counters are left out: a pass collecting them hung the box once in round 1.)
 OUT=$1; KSUB=$2; shift 3
 export TMPDIR=/tmp
 mkdir -p "$OUT"
@@ -9,7 +10,6 @@ PASSES=(
   "WRITE_SIZE"
   "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
   "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM"
-  "TA_BUSY_avr TA_TOTAL_WAVEFRONTS_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TA_DATA_STALLED_BY_TC_CYCLES_sum"
   "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum"
   "TCC_HIT_sum TCC_MISS_sum SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
 )
