@@ -265,15 +265,17 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "variant"   : persistent kernel register budget: 0 = compiler's choice, 4 / 5 = at least
  *                 4 / 5 waves per SIMD
  *   "queue_parts": persistent kernel work-queue bands (1..8, default 4; a wave starts on band XCC_ID % parts)
+ *   "interleave": 1 = each 64-pixel chunk of the queue samples its whole band (load balance)
  *   "timeline"  : 1 = record a per-wave timeline of each persistent launch (debug)
  *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal rounds (debug)       */
 rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
 
 /* Debug buffers of the last launch that recorded them (synchronises the scene's stream):
- *   "timeline": 12 u64 per wave of the persistent kernel: start and end s_memrealtime (100 MHz),
+ *   "timeline": 16 u64 per wave of the persistent kernel: start and end s_memrealtime (100 MHz),
  *               (HW_ID << 32) | XCC_ID, pixels finished by the wave, time the queue ran dry,
  *               traversal rounds, shade phases, queue grabs, and (diagnostic builds only) shader
- *               cycles spent refilling, descending, testing leaves and shading;
+ *               cycles spent refilling, descending, testing leaves and shading, descent-loop
+ *               iterations, refill-loop iterations, 2 reserved;
  *   "costmap" : 1 u32 per output pixel: traversal rounds the pixel's lane spent on it.
  * Copies min(capacity, size) bytes to dst and stores the buffer's full size in *bytes. */
 rt_status rt_scene_debug_read(rt_scene *scene, const char *name, void *dst, size_t capacity, size_t *bytes);

@@ -222,6 +222,7 @@ struct FlatTree {
     uint32_t root_ref = 0;
     float root_box[6] = {0, 0, 0, 0, 0, 0};
     uint32_t leaves = 0;
+    uint32_t height = 0;           // interior nodes on the longest root-to-leaf path
 };
 
 // pair_base: index of this tree's first pair in the global pair array; slot_base: index of the
@@ -254,6 +255,15 @@ inline FlatTree flatten_tree(const Tree &t, uint32_t pair_base, uint32_t slot_ba
     if (n) {
         f.root_ref = ref_of(0);
         t.nodes[0].box.store(f.root_box);
+        std::vector<std::pair<uint32_t, uint32_t>> todo{{0u, 0u}};   // (node, interior nodes above it)
+        while (!todo.empty()) {
+            const auto [j, d] = todo.back();
+            todo.pop_back();
+            const TreeNode &nd = t.nodes[j];
+            if (nd.count > 0) { f.height = std::max(f.height, d); continue; }
+            todo.push_back({nd.index, d + 1});
+            todo.push_back({nd.index + 1, d + 1});
+        }
     }
     return f;
 }

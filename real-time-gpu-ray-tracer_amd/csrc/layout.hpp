@@ -131,12 +131,13 @@ struct OutputGPU {
     // persistent kernel: work queue split into `queue_parts` bands of units (one per XCD), each with
     // its own head counter QUEUE_STRIDE words apart; optional per-wave timeline (debug)
     uint32_t queue_parts;
+    uint32_t interleave;            // 1: a 64-pixel chunk samples its whole band (load balance)
     unsigned long long *timeline;   // TIMELINE_WORDS per wave (rt.h, rt_scene_debug_read)
     uint32_t *costmap;              // COUNT launches: traversal rounds per output pixel (debug)
 };
 constexpr uint32_t QUEUE_STRIDE = 32;         // u32 words between partition heads (128 B lines)
 constexpr uint32_t QUEUE_MAX_PARTS = 8;
-constexpr uint32_t TIMELINE_WORDS = 12;
+constexpr uint32_t TIMELINE_WORDS = 16;
 
 // Counter slots (device uint64 array)
 enum CounterSlot : uint32_t {

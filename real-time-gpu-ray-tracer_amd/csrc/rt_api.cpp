@@ -142,6 +142,7 @@ struct rt_scene {
     uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4, 5)
     bool use_persistent = true;
     uint32_t queue_parts = 4;       // measured: 4 bands beat 1 (global queue) and 8 on C2
+    uint32_t interleave = 0;
     bool timeline_on = false;
     bool costmap_on = false;
     DevBuf<uint32_t> costmap;
@@ -625,6 +626,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
 
     if (s->use_persistent) {
         out.queue_parts = s->queue_parts;
+        out.interleave = s->interleave;
         if (s->timeline_on) {
             const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant)
                                                     : persistent_blocks_per_cu_fast(s->variant));
@@ -745,6 +747,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "queue_parts") {
         if (value < 1 || value > (int64_t)QUEUE_MAX_PARTS) return fail(RT_ERR_INVALID_ARGUMENT, "queue_parts must be in 1..8");
         s->queue_parts = (uint32_t)value;
+    } else if (k == "interleave") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "interleave must be 0 or 1");
+        s->interleave = (uint32_t)value;
     } else if (k == "timeline") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "timeline must be 0 or 1");
         s->timeline_on = value == 1;

@@ -550,7 +550,7 @@ __device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEn
 #define RT_DIAG 0
 #endif
 // Diagnostic builds (make diag -> librtamd_diag.so): wave-uniform cycle stamps per phase.
-struct PhaseCycles { unsigned long long refill, interior, leaf, shade; };
+struct PhaseCycles { unsigned long long refill, interior, leaf, shade, iters, refill_iters; };
 __device__ __forceinline__ unsigned long long stamp() {
     unsigned long long t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -574,6 +574,7 @@ __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *sp
         if (!__any(T.tracing && T.pleaf == REF_NONE)) break;
         const bool active = T.tracing && T.cur != REF_NONE && (!(T.cur & REF_LEAF) || T.pleaf == REF_NONE);
         if (active) spec_interior_step<COUNT>(T, sc, spill, cnt);
+        if (RT_DIAG) pc.iters++;
     }
     DIAG_ADD(pc.interior, t0);
     DIAG_T(t1);
@@ -848,9 +849,10 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     const uint32_t parts = out.queue_parts;
     const uint32_t xcc = xcc_id();
     uint32_t part = xcc % parts, tried = 0;
+    uint32_t band_u0 = 0, band_n = 1, band_k = 1;   // units of the band the pool came from
     unsigned long long t_start = 0, t_exhaust = 0;
     uint32_t n_rounds = 0, n_shades = 0, n_grabs = 0;      // wave-uniform (timeline)
-    PhaseCycles pc = {0, 0, 0, 0};
+    PhaseCycles pc = {0, 0, 0, 0, 0, 0};
     if (out.timeline) t_start = __builtin_amdgcn_s_memrealtime();
 
     for (;;) {
@@ -858,6 +860,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
         DIAG_T(t_refill);
         uint64_t need = __ballot(!has);
         while (need && !exhausted) {
+            if (RT_DIAG) pc.refill_iters++;
             const uint32_t n_need = __popcll(need);
             if (pool_next >= pool_end) {
                 const uint32_t p_begin = (uint32_t)(((uint64_t)out.units * part) / parts) * 64u;
@@ -877,12 +880,24 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                 }
                 pool_next = b;
                 pool_end = min(b + 64u, p_end);
+                band_u0 = p_begin >> 6;
+                band_n = (p_end - p_begin) >> 6;
+                band_k = band_n > 64u ? band_n / 64u : 1u;
             }
             const uint32_t take = min(n_need, pool_end - pool_next);
             const uint32_t rank = __popcll(need & ((1ull << lane) - 1ull));
             if (!has && rank < take) {
                 uint32_t px, py, oi;
                 item = pool_next + rank;
+                if (out.interleave) {
+                    // lane l of band chunk c renders pixel l of unit (c + l*K) mod N: every chunk samples
+                    // the whole band, so no wave inherits a run of expensive units (a bijection on the band)
+                    const uint32_t c = (item >> 6) - band_u0, l = item & 63u;
+                    uint32_t u = c + l * band_k;
+                    if (u >= band_n) u -= band_n;
+                    if (u >= band_n) u %= band_n;
+                    item = ((band_u0 + u) << 6) | l;
+                }
                 if (map_item(out, cam, item, px, py, oi)) {
                     has = true;
                     const uint32_t pixel = cam.pitch * py + px;                    // Kernel.cu:109
@@ -999,6 +1014,8 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             w[9] = pc.interior;
             w[10] = pc.leaf;
             w[11] = pc.shade;
+            w[12] = pc.iters;
+            w[13] = pc.refill_iters;
         }
     }
 }

@@ -39,6 +39,12 @@ def summarize(tl, tag):
                                                         for k in ("cyc_refill", "cyc_interior", "cyc_leaf", "cyc_shade")],
             "stamped_cycles_over_life": round(float((tl["cyc_refill"] + tl["cyc_interior"] + tl["cyc_leaf"] + tl["cyc_shade"]).sum()
                                                     / max(1.0, ((tl["end"] - tl["start"]).astype(np.float64) * 0.01 * 1e-6).sum())) / 1e9, 3),
+            "cycles_per_interior_iter": round(float(tl["cyc_interior"].sum() / max(1, tl["iters"].sum())), 1),
+            "interior_iters_per_round": round(float(tl["iters"].sum() / max(1, tl["rounds"].sum())), 2),
+            "cycles_per_leaf_phase": round(float(tl["cyc_leaf"].sum() / max(1, tl["rounds"].sum())), 1),
+            "cycles_per_shade": round(float(tl["cyc_shade"].sum() / max(1, tl["shades"].sum())), 1),
+            "cycles_per_refill_iter": round(float(tl["cyc_refill"].sum() / max(1, tl["refill_iters"].sum())), 1),
+            "refill_iters_per_shade": round(float(tl["refill_iters"].sum() / max(1, tl["shades"].sum())), 2),
             "us_per_round_plus_shade_p50": round(float(np.median(life / (tl["rounds"] + tl["shades"]))), 3),
             "mean_life_frac": round(float(life.mean() / span), 3),
             "start_us_p50_p99_max": [round(float(np.percentile(st, q)), 1) for q in (50, 99, 100)],
