@@ -265,6 +265,9 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "variant"   : persistent kernel register budget: 0 = compiler's choice, 4 / 5 = at least
  *                 4 / 5 waves per SIMD
  *   "queue_parts": persistent kernel work-queue bands (1..8, default 4; a wave starts on band XCC_ID % parts)
+ *   "lean"      : 1 = FAST persistent kernel uses the LDS-only-stack traversal (default 0) when the
+ *                 TLAS height + deepest BLAS height + 2 <= 24
+ *   "nt_store"  : 1 = non-temporal RGBA8 stores
  *   "interleave": 1 = each 64-pixel chunk of the queue samples its whole band (load balance)
  *   "timeline"  : 1 = record a per-wave timeline of each persistent launch (debug)
  *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal rounds (debug)       */
@@ -304,6 +307,8 @@ typedef struct rt_scene_info {
     uint32_t width, height;
     uint32_t sqrt_sample_count;
     uint32_t ray_trace_depth;
+    uint32_t tlas_height;          /* interior levels on the longest TLAS root-to-leaf path */
+    uint32_t blas_height_max;      /* the same, deepest BLAS */
 } rt_scene_info;
 
 rt_status rt_scene_get_info(const rt_scene *scene, rt_scene_info *info);

@@ -132,12 +132,14 @@ struct OutputGPU {
     // its own head counter QUEUE_STRIDE words apart; optional per-wave timeline (debug)
     uint32_t queue_parts;
     uint32_t interleave;            // 1: a 64-pixel chunk samples its whole band (load balance)
+    uint32_t nt_store;              // 1: RGBA8 stores are non-temporal (keep the scene in L2)
     unsigned long long *timeline;   // TIMELINE_WORDS per wave (rt.h, rt_scene_debug_read)
     uint32_t *costmap;              // COUNT launches: traversal rounds per output pixel (debug)
 };
 constexpr uint32_t QUEUE_STRIDE = 32;         // u32 words between partition heads (128 B lines)
 constexpr uint32_t QUEUE_MAX_PARTS = 8;
 constexpr uint32_t TIMELINE_WORDS = 16;
+constexpr uint32_t LEAN_STACK = 24;       // LDS stack entries of the lean traversal
 
 // Counter slots (device uint64 array)
 enum CounterSlot : uint32_t {

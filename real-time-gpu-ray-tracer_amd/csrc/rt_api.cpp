@@ -28,11 +28,11 @@ hipError_t launch_trace_rays_exact(const SceneGPU &, const float *, uint32_t, rt
 hipError_t launch_trace_rays_fast(const SceneGPU &, const float *, uint32_t, rt_hit *, hipStream_t);
 hipError_t launch_assemble(const void *, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, void *, hipStream_t);
 hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
-                                          uint32_t *, uint32_t, uint32_t, uint32_t, hipStream_t);
+                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
-                                         uint32_t *, uint32_t, uint32_t, uint32_t, hipStream_t);
-uint32_t persistent_blocks_per_cu_exact(uint32_t variant);
-uint32_t persistent_blocks_per_cu_fast(uint32_t variant);
+                                         uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
+uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean);
+uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -143,6 +143,9 @@ struct rt_scene {
     bool use_persistent = true;
     uint32_t queue_parts = 4;       // measured: 4 bands beat 1 (global queue) and 8 on C2
     uint32_t interleave = 0;
+    uint32_t nt_store = 0;
+    bool lean = false;              // FAST persistent kernel: LDS-only-stack traversal when the trees fit (measured slower on C2)
+    uint32_t max_blas_height = 0;
     bool timeline_on = false;
     bool costmap_on = false;
     DevBuf<uint32_t> costmap;
@@ -358,6 +361,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     s->build_mode = mode;
     s->inst.clear();
     s->blas.clear();
+    s->max_blas_height = 0;
 
     // buildBLASPinMem (RenderPin.cu:99-201): complete instances, one BLAS per unique (type, index).
     // The reference's map stores the instance index instead of the BLAS index (RenderPin.cu:151);
@@ -407,6 +411,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             if ((uint64_t)slot_base[in.ptype] + in.pcount >= MAX_LEAF_SLOTS)
                 return fail(RT_ERR_UNSUPPORTED, "too many primitives of one type (2^26 leaf slots)");
             bh.flat = flatten_tree(bh.tree, pair_base, bh.slot_base, in.ptype, true);
+            s->max_blas_height = std::max(s->max_blas_height, bh.flat.height);
             pair_base += (uint32_t)bh.flat.pairs.size();
             slot_base[in.ptype] += in.pcount;
             s->blas.push_back(std::move(bh));
@@ -582,6 +587,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     hipStream_t stream = o.stream ? static_cast<hipStream_t>(o.stream) : s->stream;
 
     OutputGPU out{};
+    out.nt_store = s->nt_store;
     const uint32_t W = s->width, H = s->height;
     size_t npix;
     if (o.tile_count == 0) {
@@ -624,12 +630,14 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     const bool exact = (o.flags & RT_RENDER_EXACT) != 0;
     const bool count = (o.flags & RT_RENDER_COUNT_WORK) != 0;
 
+    // lean traversal: FAST kernel, LDS-only stack deep enough for TLAS + deepest BLAS (+ 2 resume entries)
+    const bool lean = !exact && s->lean && s->tlas_flat.height + s->max_blas_height + 2 <= LEAN_STACK;
     if (s->use_persistent) {
         out.queue_parts = s->queue_parts;
         out.interleave = s->interleave;
         if (s->timeline_on) {
-            const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant)
-                                                    : persistent_blocks_per_cu_fast(s->variant));
+            const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false)
+                                                    : persistent_blocks_per_cu_fast(s->variant, lean));
             const size_t words = (size_t)blocks * 4 * TIMELINE_WORDS;
             if (s->timeline.n < words) {
                 s->timeline.release();
@@ -662,11 +670,11 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     HIP_TRY(hipEventRecord(s->k_start, stream));
     if (s->use_persistent)
         HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, s->counters, s->queue,
-                                                       s->cus * persistent_blocks_per_cu_exact(s->variant), s->threshold,
-                                                       s->variant, stream)
+                                                       s->cus * persistent_blocks_per_cu_exact(s->variant, false), s->threshold,
+                                                       s->variant, false, stream)
                       : launch_render_persistent_fast(g, cam, out, count, s->counters, s->queue,
-                                                      s->cus * persistent_blocks_per_cu_fast(s->variant), s->threshold,
-                                                      s->variant, stream));
+                                                      s->cus * persistent_blocks_per_cu_fast(s->variant, lean), s->threshold,
+                                                      s->variant, lean, stream));
     else
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, s->counters, stream)
                       : launch_render_fast(g, cam, out, count, s->counters, stream));
@@ -747,6 +755,12 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "queue_parts") {
         if (value < 1 || value > (int64_t)QUEUE_MAX_PARTS) return fail(RT_ERR_INVALID_ARGUMENT, "queue_parts must be in 1..8");
         s->queue_parts = (uint32_t)value;
+    } else if (k == "lean") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "lean must be 0 or 1");
+        s->lean = value == 1;
+    } else if (k == "nt_store") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "nt_store must be 0 or 1");
+        s->nt_store = (uint32_t)value;
     } else if (k == "interleave") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "interleave must be 0 or 1");
         s->interleave = (uint32_t)value;
@@ -843,6 +857,8 @@ rt_status rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
     info->width = s->width; info->height = s->height;
     info->sqrt_sample_count = s->cam.sqrt_s;
     info->ray_trace_depth = s->cam.depth;
+    info->tlas_height = s->tlas_flat.height;
+    info->blas_height_max = s->max_blas_height;
     return RT_OK;
 }
 

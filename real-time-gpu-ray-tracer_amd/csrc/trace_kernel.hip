@@ -139,7 +139,10 @@ struct RayP {
 __device__ __forceinline__ void prep(RayP &r) {
 #if !RT_EXACT
     r.tiny = fabsf(r.d.x) < FZERO || fabsf(r.d.y) < FZERO || fabsf(r.d.z) < FZERO;
-    r.inv = mk(rcp(r.d.x), rcp(r.d.y), rcp(r.d.z));
+    // |d| < 1e-20 -> +-1e-20: finite reciprocals, so the branch-free slab of the lean traversal
+    // never forms 0 * inf
+    const auto nz = [](float x) { return fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x; };
+    r.inv = mk(rcp(nz(r.d.x)), rcp(nz(r.d.y)), rcp(nz(r.d.z)));
     r.oinv = mk(r.o.x * r.inv.x, r.o.y * r.inv.y, r.o.z * r.inv.z);
 #else
     (void)r;
@@ -351,6 +354,7 @@ struct Trav {
     Hit hit;
     bool found;
     bool tracing;
+    bool in_blas;          // lean traversal: lr holds the instance ray (else lr == wr)
     Stack stk;
 };
 
@@ -363,6 +367,7 @@ __device__ __forceinline__ void trav_init(Trav &T, const SceneGPU &sc, const f3 
     T.stk.spilled = 0;
     T.cur = sc.tlas_root_ref;
     T.cur_inst = 0;
+    T.in_blas = false;
     T.pleaf = REF_NONE;
     float te = 0.0f;
     T.tracing = slab(sc.tlas_root_box, T.wr, TMIN, T.tmax, te);          // root pop test (TLAS.cu:150)
@@ -581,6 +586,155 @@ __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *sp
     if (T.tracing) spec_leaf_phase<COUNT>(T, sc, spill, cnt);
     DIAG_ADD(pc.leaf, t1);
 }
+
+constexpr int LEAN_DEPTH = (int)LEAN_STACK;   // lean traversal: LDS-only stack entries
+#if !RT_EXACT
+// ---- lean traversal (FAST kernel on shallow trees) ----------------------------------------
+// Same speculative while-while order as spec_*, written for a short, mostly straight-line loop body
+// (divergent branches cost exec-mask bookkeeping on every step):
+//   * the stack lives in LDS only (LEAN_DEPTH entries; the host picks this path only when the TLAS
+//     height + the deepest BLAS height + 2 fits), so push/pop carry no paging code;
+//   * a step pops at most one entry: a lane that needs a node marks cur = REF_POP and pops at the
+//     start of its next step; a popped entry that fails its re-test (entry t >= tmax) is marked
+//     REF_POP again, so the reference's pop loop becomes one pop per step;
+//   * push is unconditional (the slot above the top is scratch space; sp only advances on a push);
+//   * one active ray: lr is the world ray in the TLAS and the instance ray inside a BLAS; a lane
+//     holding a postponed BLAS leaf does not cross back into the TLAS until the leaf is tested;
+//   * branch-free slabs on clamped reciprocals (prep), no parallel-axis path.
+constexpr uint32_t REF_POP = 0xFFFFFFFEu;    // marker: pop the next entry (leaf bit + type 3)
+__device__ __forceinline__ bool ref_is_marker(uint32_t r) { return (r & 0xF0000000u) == 0xF0000000u; }
+
+__device__ __forceinline__ bool slab_lean(float x0, float x1, float y0, float y1, float z0, float z1, const RayP &r,
+                                          float tmax, float &te) {
+    const float tx1 = fmaf(x0, r.inv.x, -r.oinv.x), tx2 = fmaf(x1, r.inv.x, -r.oinv.x);
+    const float ty1 = fmaf(y0, r.inv.y, -r.oinv.y), ty2 = fmaf(y1, r.inv.y, -r.oinv.y);
+    const float tz1 = fmaf(z0, r.inv.z, -r.oinv.z), tz2 = fmaf(z1, r.inv.z, -r.oinv.z);
+    const float lo = fmaxf(fmaxf(TMIN, fminf(tx1, tx2)), fmaxf(fminf(ty1, ty2), fminf(tz1, tz2)));
+    const float hi = fminf(fminf(tmax, fmaxf(tx1, tx2)), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
+    te = lo;
+    return lo < hi;
+}
+__device__ __forceinline__ void lean_push(Trav &T, uint32_t ref, float tn, bool do_push, LaneCount &c) {
+    SEnt e;
+    e.ref = ref;
+    e.tn = __float_as_uint(tn);
+    const int slot = T.stk.sp < LEAN_DEPTH ? T.stk.sp : LEAN_DEPTH - 1;
+    if (do_push) {
+        if (T.stk.sp >= LEAN_DEPTH) c.overflow++;
+        T.stk.lds[slot * BLOCK] = pack(e);
+        T.stk.sp = min(T.stk.sp + 1, LEAN_DEPTH);
+    }
+}
+
+// One step of a lane that may step: pop / re-test, postpone a leaf, or test a node pair.
+template <bool COUNT>
+__device__ __forceinline__ void lean_step(Trav &T, const SceneGPU &sc, LaneCount &cnt) {
+    uint32_t cur = T.cur;
+    float curT = T.curT;
+    if (cur == REF_POP) {                                   // pop one entry, re-test it (BLAS.cu:145)
+        const int top = T.stk.sp > 0 ? T.stk.sp - 1 : 0;
+        const SEnt e = unpack(T.stk.lds[top * BLOCK]);
+        if (T.stk.sp > 0) {
+            T.stk.sp = top;
+            cur = __uint_as_float(e.tn) < T.tmax ? e.ref : REF_POP;
+            curT = __uint_as_float(e.tn);
+        } else {
+            cur = REF_NONE;
+        }
+    }
+    const bool blocked = T.pleaf != REF_NONE && T.in_blas && !ref_is_marker(cur) && !(cur & REF_BLAS);
+    if (!ref_is_marker(cur) && !blocked) {
+        if (T.in_blas && !(cur & REF_BLAS)) { T.lr = T.wr; T.in_blas = false; }   // back in the TLAS
+        if (cur & REF_LEAF) {
+            if (T.pleaf == REF_NONE) { T.pleaf = cur; cur = REF_POP; }            // postpone, keep walking
+        } else {
+            const NodePair *P = ((cur & REF_BLAS) ? sc.blas_pairs : sc.tlas_pairs) + (cur & REF_INDEX_MASK);
+            const float4 *P4 = reinterpret_cast<const float4 *>(P);
+            const float4 A = P4[0], B = P4[1], C = P4[2];
+            const uint4 D = reinterpret_cast<const uint4 *>(P)[3];
+            if (COUNT) cnt.pairs++;
+            float e0, e1;
+            const bool h0 = slab_lean(A.x, A.y, A.z, A.w, B.x, B.y, T.lr, T.tmax, e0);
+            const bool h1 = slab_lean(B.z, B.w, C.x, C.y, C.z, C.w, T.lr, T.tmax, e1);
+            const bool right_near = h0 && h1 && e0 > e1;          // TLAS.cu:185-192 ordering
+            lean_push(T, right_near ? D.x : D.y, right_near ? e0 : e1, h0 && h1, cnt);
+            const bool go0 = h0 && !right_near;
+            cur = go0 ? D.x : (h1 ? D.y : REF_POP);
+            curT = go0 ? e0 : e1;
+        }
+    }
+    T.cur = cur;
+    T.curT = curT;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void lean_leaf_phase(Trav &T, const SceneGPU &sc, LaneCount &cnt) {
+    const uint32_t leaf = T.pleaf;
+    T.pleaf = REF_NONE;
+    if (!(leaf & REF_BLAS)) {
+        // TLAS leaf (lane is in the TLAS: lr == wr): successor and remaining instances wait on the stack
+        const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf);
+        lean_push(T, T.cur, T.curT, !ref_is_marker(T.cur), cnt);
+        lean_push(T, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), count > 1, cnt);
+        T.cur_inst = sc.tlas_slots[start];
+        const InstHot &I = sc.inst_hot[T.cur_inst];
+        if (COUNT) cnt.inst++;
+        T.lr.o = xf_point(I.inv, T.wr.o);                      // Instance.cu:26-27
+        T.lr.d = xf_vector(I.inv, T.wr.d);
+        prep(T.lr);
+        T.in_blas = true;
+        float te;
+        const bool h = slab_lean(I.root_box[0], I.root_box[1], I.root_box[2], I.root_box[3], I.root_box[4],
+                                 I.root_box[5], T.lr, T.tmax, te);
+        T.cur = h ? I.root_ref : REF_POP;
+        T.curT = te;
+    } else {
+        const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf), type = ref_leaf_type(leaf);
+        for (uint32_t k = 0; k < count; k++) {
+            const uint32_t slot = start + k;
+            float t = 0.0f, u = 0.0f, v = 0.0f;
+            bool h;
+            if (type == RT_PRIM_TRIANGLE) {
+                if (COUNT) cnt.tri++;
+                h = tri_test(sc.tri_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
+            } else if (type == RT_PRIM_SPHERE) {
+                if (COUNT) cnt.sq++;
+                h = sphere_test(sc.sph_hot[slot], T.lr, TMIN, T.tmax, t);
+            } else {
+                if (COUNT) { cnt.sq++; cnt.quad++; }
+                h = quad_test(sc.quad_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
+            }
+            if (h) {
+                T.found = true; T.tmax = t;
+                T.hit.t = t; T.hit.inst = T.cur_inst; T.hit.ptype = type; T.hit.slot = slot; T.hit.u = u; T.hit.v = v;
+            }
+        }
+        if (!ref_is_marker(T.cur) && !(T.curT < T.tmax)) T.cur = REF_POP;   // re-test the successor
+    }
+    if (T.cur == REF_POP && T.stk.sp == 0) T.cur = REF_NONE;
+    if (T.cur == REF_NONE) T.tracing = false;
+}
+
+// lane takes a step this iteration: tracing, not finished, and not waiting at a second leaf
+__device__ __forceinline__ bool lean_active(const Trav &T) {
+    return T.tracing && T.cur != REF_NONE && !(T.pleaf != REF_NONE && (T.cur & REF_LEAF) && !ref_is_marker(T.cur));
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void lean_round(Trav &T, const SceneGPU &sc, LaneCount &cnt, PhaseCycles &pc) {
+    DIAG_T(t0);
+    for (;;) {
+        if (T.tracing && T.pleaf == REF_NONE && T.cur == REF_NONE) T.tracing = false;   // done, no leaf left
+        if (!__any(T.tracing && T.pleaf == REF_NONE)) break;
+        if (lean_active(T)) lean_step<COUNT>(T, sc, cnt);
+        if (RT_DIAG) pc.iters++;
+    }
+    DIAG_ADD(pc.interior, t0);
+    DIAG_T(t1);
+    if (T.tracing) lean_leaf_phase<COUNT>(T, sc, cnt);
+    DIAG_ADD(pc.leaf, t1);
+}
+#endif
 
 template <bool COUNT>
 __device__ __forceinline__ bool trace(const SceneGPU &sc, const f3 &o, const f3 &d, Hit &hit, Trav &T, SEnt *spill,
@@ -816,14 +970,15 @@ __device__ __forceinline__ void write_pixel(const OutputGPU &out, uint32_t oi, f
     const float cb = fminf(fmaxf(sqrtf(result.z), 0.0f), 0.999f);
     const uint32_t packed = (uint32_t)(uint8_t)(256.0f * cr) | ((uint32_t)(uint8_t)(256.0f * cg) << 8) |
                             ((uint32_t)(uint8_t)(256.0f * cb) << 16) | (255u << 24);
-    reinterpret_cast<uint32_t *>(out.rgba)[oi] = packed;
+    if (out.nt_store) __builtin_nontemporal_store(packed, reinterpret_cast<uint32_t *>(out.rgba) + oi);
+    else reinterpret_cast<uint32_t *>(out.rgba)[oi] = packed;
 }
 
-template <bool COUNT>
+template <bool COUNT, bool LEAN>
 __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out,
                                                        uint32_t *queue, uint32_t threshold,
                                                        unsigned long long *counters) {
-    __shared__ unsigned long long lds_stack[LDS_DEPTH][BLOCK];
+    __shared__ unsigned long long lds_stack[LEAN ? LEAN_DEPTH : LDS_DEPTH][BLOCK];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
 
@@ -926,7 +1081,11 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             if (tr == 0) break;
             const uint64_t want = __ballot(!T.tracing && (has || !exhausted));
             if ((uint32_t)__popcll(want) >= threshold) break;
-            spec_round<COUNT>(T, sc, spill, cnt, pc);
+#if !RT_EXACT
+            if constexpr (LEAN) lean_round<COUNT>(T, sc, cnt, pc);
+            else
+#endif
+                spec_round<COUNT>(T, sc, spill, cnt, pc);
             n_rounds++;
             if (COUNT) px_rounds += T.tracing ? 1u : 0u;
         }
@@ -1021,11 +1180,11 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
 }
 
 // Register budget variants: WPE = minimum waves per SIMD the compiler must allow (0 = its choice).
-template <bool COUNT, int WPE>
+template <bool COUNT, int WPE, bool LEAN>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
 void render_persistent_kernel(SceneGPU sc, CameraGPU cam, OutputGPU out, uint32_t *queue, uint32_t threshold,
                               unsigned long long *counters) {
-    render_persistent_body<COUNT>(sc, cam, out, queue, threshold, counters);
+    render_persistent_body<COUNT, LEAN>(sc, cam, out, queue, threshold, counters);
 }
 
 __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const float *rays, uint32_t n, rt_hit *hits) {
@@ -1070,7 +1229,7 @@ hipError_t RT_SUFFIX(launch_render)(const SceneGPU &sc, const CameraGPU &cam, co
 }
 
 namespace {
-template <int WPE>
+template <int WPE, bool LEAN>
 hipError_t launch_persistent_wpe(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
                                  unsigned long long *counters, uint32_t *queue, uint32_t blocks_per_cu_cus,
                                  uint32_t threshold, hipStream_t stream) {
@@ -1078,36 +1237,52 @@ hipError_t launch_persistent_wpe(const SceneGPU &sc, const CameraGPU &cam, const
     const uint32_t need = (out.units + (BLOCK / 64) - 1) / (BLOCK / 64);
     const dim3 grid(blocks_per_cu_cus < need ? blocks_per_cu_cus : need);
     if (count)
-        hipLaunchKernelGGL((render_persistent_kernel<true, WPE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
+        hipLaunchKernelGGL((render_persistent_kernel<true, WPE, LEAN>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
     else
-        hipLaunchKernelGGL((render_persistent_kernel<false, WPE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
+        hipLaunchKernelGGL((render_persistent_kernel<false, WPE, LEAN>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
     return hipGetLastError();
 }
-template <int WPE>
+template <int WPE, bool LEAN>
 uint32_t blocks_per_cu_wpe() {
     using namespace RT_SUFFIX(dev);
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false, WPE>, BLOCK, 0) != hipSuccess) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false, WPE, LEAN>, BLOCK, 0) != hipSuccess) return 1;
     return n > 0 ? (uint32_t)n : 1u;
 }
+#if RT_EXACT
+constexpr bool HAS_LEAN = false;
+#else
+constexpr bool HAS_LEAN = true;
+#endif
 }  // namespace
 
-// variant: 0 = compiler's register budget, 4 / 5 = at least 4 / 5 waves per SIMD
+// variant: 0 = compiler's register budget, 4 / 5 = at least 4 / 5 waves per SIMD.
+// lean: LDS-only-stack traversal (FAST kernel; the caller checks the tree heights).
 hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
                                                unsigned long long *counters, uint32_t *queue, uint32_t blocks,
-                                               uint32_t threshold, uint32_t variant, hipStream_t stream) {
+                                               uint32_t threshold, uint32_t variant, bool lean, hipStream_t stream) {
     if (out.units == 0) return hipSuccess;
     hipError_t e = hipMemsetAsync(queue, 0, QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t), stream);
     if (e != hipSuccess) return e;
-    if (variant == 4) return launch_persistent_wpe<4>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-    if (variant == 5) return launch_persistent_wpe<5>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-    return launch_persistent_wpe<0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+    if (lean && HAS_LEAN) {
+        if (variant == 4) return launch_persistent_wpe<4, HAS_LEAN>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+        if (variant == 5) return launch_persistent_wpe<5, HAS_LEAN>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+        return launch_persistent_wpe<3, HAS_LEAN>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+    }
+    if (variant == 4) return launch_persistent_wpe<4, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+    if (variant == 5) return launch_persistent_wpe<5, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+    return launch_persistent_wpe<0, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
 }
 
-uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant) {
-    if (variant == 4) return blocks_per_cu_wpe<4>();
-    if (variant == 5) return blocks_per_cu_wpe<5>();
-    return blocks_per_cu_wpe<0>();
+uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, bool lean) {
+    if (lean && HAS_LEAN) {
+        if (variant == 4) return blocks_per_cu_wpe<4, HAS_LEAN>();
+        if (variant == 5) return blocks_per_cu_wpe<5, HAS_LEAN>();
+        return blocks_per_cu_wpe<3, HAS_LEAN>();
+    }
+    if (variant == 4) return blocks_per_cu_wpe<4, false>();
+    if (variant == 5) return blocks_per_cu_wpe<5, false>();
+    return blocks_per_cu_wpe<0, false>();
 }
 
 hipError_t RT_SUFFIX(launch_trace_rays)(const SceneGPU &sc, const float *rays, uint32_t n, rt_hit *hits,

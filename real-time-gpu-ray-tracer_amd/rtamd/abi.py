@@ -122,7 +122,8 @@ class SceneInfo(C.Structure):
     _fields_ = [("blas_count", C.c_uint64), ("blas_node_pairs", C.c_uint64),
                 ("blas_leaves", C.c_uint64), ("tlas_node_pairs", C.c_uint64),
                 ("device_bytes", C.c_uint64), ("width", C.c_uint32), ("height", C.c_uint32),
-                ("sqrt_sample_count", C.c_uint32), ("ray_trace_depth", C.c_uint32)]
+                ("sqrt_sample_count", C.c_uint32), ("ray_trace_depth", C.c_uint32),
+                ("tlas_height", C.c_uint32), ("blas_height_max", C.c_uint32)]
 
 
 # Every symbol include/rt.h declares; tests check the library exports all of them.

@@ -61,6 +61,12 @@ def main():
         res["derived_l2_hit_rate"] = a["TCC_HIT_sum"] / max(1.0, a["TCC_HIT_sum"] + a["TCC_MISS_sum"])
     if {"TCP_TCC_READ_REQ_LATENCY_sum", "TCP_TCC_READ_REQ_sum"} <= a.keys():
         res["derived_l1_to_l2_read_latency_cycles"] = a["TCP_TCC_READ_REQ_LATENCY_sum"] / max(1.0, a["TCP_TCC_READ_REQ_sum"])
+    for lvl, cnt in (("SQ_INST_LEVEL_VMEM", "SQ_INSTS_VMEM"), ("SQ_INST_LEVEL_LDS", "SQ_INSTS_LDS"),
+                     ("SQ_INST_LEVEL_SMEM", "SQ_INSTS_SMEM")):
+        if {lvl, cnt} <= a.keys():   # level accumulates in-flight instructions per cycle -> mean latency
+            res[f"derived_mean_latency_cycles_{cnt[9:].lower()}"] = a[lvl] / max(1.0, a[cnt])
+    if {"SQC_ICACHE_MISSES", "SQC_ICACHE_HITS"} <= a.keys():
+        res["derived_icache_miss_rate"] = a["SQC_ICACHE_MISSES"] / max(1.0, a["SQC_ICACHE_MISSES"] + a["SQC_ICACHE_HITS"])
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))

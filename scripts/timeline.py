@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--parts", type=int, nargs="+", default=[1, 8])
     ap.add_argument("--threshold", type=int, default=8)
     ap.add_argument("--out", default="gpurun_out/timeline.npz")
+    ap.add_argument("--opt", action="append", default=[], help="extra scene option key=value")
     a = ap.parse_args()
     import torch
     from rtamd import Renderer, scenes
@@ -68,6 +69,9 @@ def main():
     r = Renderer(scenes.config_scene(cfg)).build_acceleration_structure(0, mode=a.build).configure_camera(
         cfg.width, cfg.height)
     r.set_option("threshold", a.threshold)
+    for kv in a.opt:
+        k, v = kv.split("=")
+        r.set_option(k, int(v))
     saved = {}
     for parts in a.parts:
         r.set_option("queue_parts", parts)
