@@ -268,7 +268,8 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "lean"      : 1 = FAST persistent kernel uses the LDS-only-stack traversal (default 0) when the
  *                 TLAS height + deepest BLAS height + 2 <= 24
  *   "nt_store"  : 1 = non-temporal RGBA8 stores
- *   "interleave": 1 = each 64-pixel chunk of the queue samples its whole band (load balance)
+ *   "grab"      : pixels claimed per work-queue atomic (multiple of 8, default 64)
+ *   "supertile" : walk each band in supertile x supertile units of 8x8 pixels (default 16; 0 = rows)
  *   "timeline"  : 1 = record a per-wave timeline of each persistent launch (debug)
  *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal rounds (debug)       */
 rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);

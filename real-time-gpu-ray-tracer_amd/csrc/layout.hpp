@@ -131,8 +131,9 @@ struct OutputGPU {
     // persistent kernel: work queue split into `queue_parts` bands of units (one per XCD), each with
     // its own head counter QUEUE_STRIDE words apart; optional per-wave timeline (debug)
     uint32_t queue_parts;
-    uint32_t interleave;            // 1: a 64-pixel chunk samples its whole band (load balance)
     uint32_t nt_store;              // 1: RGBA8 stores are non-temporal (keep the scene in L2)
+    uint32_t grab;                  // pixels claimed per queue atomic
+    uint32_t supertile;             // frame mode, grab 64: walk bands in supertile x supertile units (0 = rows)
     unsigned long long *timeline;   // TIMELINE_WORDS per wave (rt.h, rt_scene_debug_read)
     uint32_t *costmap;              // COUNT launches: traversal rounds per output pixel (debug)
 };

@@ -142,8 +142,9 @@ struct rt_scene {
     uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4, 5)
     bool use_persistent = true;
     uint32_t queue_parts = 4;       // measured: 4 bands beat 1 (global queue) and 8 on C2
-    uint32_t interleave = 0;
     uint32_t nt_store = 0;
+    uint32_t grab = 64;             // pixels per queue claim
+    uint32_t supertile = 16;        // band walk order: st x st-unit supertiles (measured: 16 beats rows, 8 and 32)
     bool lean = false;              // FAST persistent kernel: LDS-only-stack traversal when the trees fit (measured slower on C2)
     uint32_t max_blas_height = 0;
     bool timeline_on = false;
@@ -634,7 +635,8 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     const bool lean = !exact && s->lean && s->tlas_flat.height + s->max_blas_height + 2 <= LEAN_STACK;
     if (s->use_persistent) {
         out.queue_parts = s->queue_parts;
-        out.interleave = s->interleave;
+        out.grab = s->grab;
+        out.supertile = s->supertile;
         if (s->timeline_on) {
             const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false)
                                                     : persistent_blocks_per_cu_fast(s->variant, lean));
@@ -761,9 +763,12 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "nt_store") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "nt_store must be 0 or 1");
         s->nt_store = (uint32_t)value;
-    } else if (k == "interleave") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "interleave must be 0 or 1");
-        s->interleave = (uint32_t)value;
+    } else if (k == "grab") {
+        if (value < 8 || value > 4096 || (value % 8)) return fail(RT_ERR_INVALID_ARGUMENT, "grab must be a multiple of 8 in 8..4096");
+        s->grab = (uint32_t)value;
+    } else if (k == "supertile") {
+        if (value < 0 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "supertile must be in 0..64");
+        s->supertile = (uint32_t)value;
     } else if (k == "timeline") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "timeline must be 0 or 1");
         s->timeline_on = value == 1;

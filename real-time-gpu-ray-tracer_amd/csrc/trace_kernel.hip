@@ -1004,7 +1004,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     const uint32_t parts = out.queue_parts;
     const uint32_t xcc = xcc_id();
     uint32_t part = xcc % parts, tried = 0;
-    uint32_t band_u0 = 0, band_n = 1, band_k = 1;   // units of the band the pool came from
+    const uint32_t grab = out.grab;                 // claim size (pixels)
     unsigned long long t_start = 0, t_exhaust = 0;
     uint32_t n_rounds = 0, n_shades = 0, n_grabs = 0;      // wave-uniform (timeline)
     PhaseCycles pc = {0, 0, 0, 0, 0, 0};
@@ -1018,10 +1018,13 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             if (RT_DIAG) pc.refill_iters++;
             const uint32_t n_need = __popcll(need);
             if (pool_next >= pool_end) {
-                const uint32_t p_begin = (uint32_t)(((uint64_t)out.units * part) / parts) * 64u;
-                const uint32_t p_end = (uint32_t)(((uint64_t)out.units * (part + 1)) / parts) * 64u;
+                // bands: whole unit rows in frame mode (so a band can be walked in supertiles)
+                const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
+                const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
+                const uint32_t p_begin = (rows * part / parts) * upr * 64u;
+                const uint32_t p_end = (rows * (part + 1) / parts) * upr * 64u;
                 uint32_t b = 0;
-                if (lane == 0) b = atomicAdd(queue + part * QUEUE_STRIDE, 64u);
+                if (lane == 0) b = atomicAdd(queue + part * QUEUE_STRIDE, grab);
                 b = p_begin + __shfl(b, 0, 64);
                 n_grabs++;
                 if (b >= p_end) {
@@ -1034,25 +1037,29 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     continue;
                 }
                 pool_next = b;
-                pool_end = min(b + 64u, p_end);
-                band_u0 = p_begin >> 6;
-                band_n = (p_end - p_begin) >> 6;
-                band_k = band_n > 64u ? band_n / 64u : 1u;
+                pool_end = min(b + grab, p_end);
+                if (out.supertile && out.tile_count == 0 && grab == 64u) {
+                    // walk the band in st x st-unit supertiles (row-major supertiles, row-major units
+                    // inside): the units in flight form a compact screen region, not a full-width strip
+                    const uint32_t W = out.units_x, st = out.supertile;
+                    const uint32_t r0 = p_begin / (64u * W), Hb = (p_end - p_begin) / (64u * W);
+                    const uint32_t j = (b - p_begin) >> 6;
+                    const uint32_t sr = j / (W * st);
+                    const uint32_t h = min(st, Hb - sr * st);
+                    const uint32_t k = j - sr * W * st;
+                    const uint32_t sc = k / (st * h);
+                    const uint32_t w = min(st, W - sc * st);
+                    const uint32_t m = k - sc * st * h;
+                    const uint32_t u = (r0 + sr * st + m / w) * W + sc * st + m % w;
+                    pool_next = u * 64u;
+                    pool_end = pool_next + 64u;
+                }
             }
             const uint32_t take = min(n_need, pool_end - pool_next);
             const uint32_t rank = __popcll(need & ((1ull << lane) - 1ull));
             if (!has && rank < take) {
                 uint32_t px, py, oi;
                 item = pool_next + rank;
-                if (out.interleave) {
-                    // lane l of band chunk c renders pixel l of unit (c + l*K) mod N: every chunk samples
-                    // the whole band, so no wave inherits a run of expensive units (a bijection on the band)
-                    const uint32_t c = (item >> 6) - band_u0, l = item & 63u;
-                    uint32_t u = c + l * band_k;
-                    if (u >= band_n) u -= band_n;
-                    if (u >= band_n) u %= band_n;
-                    item = ((band_u0 + u) << 6) | l;
-                }
                 if (map_item(out, cam, item, px, py, oi)) {
                     has = true;
                     const uint32_t pixel = cam.pitch * py + px;                    // Kernel.cu:109
