@@ -154,7 +154,14 @@ typedef enum rt_build_mode {
     RT_BUILD_COMPAT_MEDIAN = 0,
     /* Surface-area-heuristic BLAS and per-frame TLAS (leaf <= 4 items).  Different trees than the
      * reference: hits agree except where two surfaces tie within the 1e-6 window. */
-    RT_BUILD_SAH = 1
+    RT_BUILD_SAH = 1,
+    /* GPU builder: every BLAS and the per-frame TLAS are linear BVHs
+     * (30-bit Morton order per tree, Karras radix-tree hierarchy, subtrees of <= 4 primitives /
+     * <= 2 instances collapsed into leaves) built by HIP kernels on the scene's stream.  The host
+     * still runs the update callback and the instance matrices (Instance.cu:4-17); the TLAS build
+     * never blocks the host.  With rt_scene_set_option("rebuild", 1) every BLAS is rebuilt on the
+     * GPU each frame (config C5's per-frame rebuild); rt_scene_update_triangles marks them stale. */
+    RT_BUILD_LBVH = 2
 } rt_build_mode;
 
 typedef enum rt_render_flags {
@@ -270,6 +277,7 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "nt_store"  : 1 = non-temporal RGBA8 stores
  *   "grab"      : pixels claimed per work-queue atomic (multiple of 8, default 64)
  *   "supertile" : walk each band in supertile x supertile units of 8x8 pixels (default 16; 0 = rows)
+ *   "rebuild"   : RT_BUILD_LBVH only: 1 = rebuild every BLAS on the GPU every frame (default 0)
  *   "timeline"  : 1 = record a per-wave timeline of each persistent launch (debug)
  *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal rounds (debug)       */
 rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
@@ -290,6 +298,12 @@ rt_status rt_scene_debug_read(rt_scene *scene, const char *name, void *dst, size
  * rendered since the previous collect (HIP events on the kernel's stream; up to 256 kept). */
 rt_status rt_scene_collect(rt_scene *scene, rt_stats *accumulated, float *kernel_ms, uint32_t capacity,
                            uint32_t *count);
+
+/* Replace triangles [first, first + count) of the scene's triangle array (deforming geometry,
+ * e.g. the next frame of a VTK series, Renderer.cu:394-443).  RT_BUILD_LBVH scenes only: the
+ * BLASes are rebuilt on the GPU before the next frame traces.  Instances keep the local bounds
+ * their description supplied (has_local_bounds), as the reference keeps the VTK reader's. */
+rt_status rt_scene_update_triangles(rt_scene *scene, size_t first, size_t count, const rt_triangle *triangles);
 
 /* Blocks until all work the scene enqueued has finished. */
 rt_status rt_synchronize(rt_scene *scene);

@@ -86,6 +86,13 @@ struct alignas(16) InstCold {       // 96 B: hit finalisation (Instance.cu:41-45
 
 constexpr uint32_t MAT_METAL_BIT = 1u << 31;
 
+struct alignas(16) TreeRoot {       // 32 B: root of one tree (GPU-built trees keep it in HBM)
+    float box[6];
+    uint32_t ref;
+    uint32_t height;                // interior levels on the longest root-to-leaf path
+};
+static_assert(sizeof(TreeRoot) == 32, "TreeRoot must be 32 B");
+
 // ---- kernel arguments ----------------------------------------------------------------
 struct SceneGPU {
     const NodePair *blas_pairs;
@@ -100,8 +107,7 @@ struct SceneGPU {
     const QuadHot *quad_hot;
     const PrimCold *quad_cold;
     const float *materials;         // 4 floats per slot: albedo.xyz, fuzz (roughs then metals)
-    float tlas_root_box[6];
-    uint32_t tlas_root_ref;
+    const TreeRoot *tlas_root;      // this frame's TLAS root, in the per-frame block (host- or GPU-built)
     uint32_t instance_count;
     uint32_t rough_count;           // material slot of metal m = rough_count + m
 };

@@ -1,0 +1,589 @@
+// lbvh.hip — GPU BVH builder (RT_BUILD_LBVH): BLAS forests over primitives and the per-frame TLAS
+// over instances, built on the device (interface and pipeline in lbvh.hpp).
+//
+// Karras, "Maximizing Parallelism in the Construction of BVHs, Octrees, and k-d Trees" (HPG 2012):
+// with items sorted by Morton code, interior node i of an n-leaf radix tree covers a key range with
+// one end at i; its direction, far end and split follow from the longest-common-prefix function
+// δ(i, j) alone, so every interior node is built by one thread with no dependencies.  Here δ is
+// evaluated per segment (indices outside the segment give -1), so one launch builds a whole forest
+// (9,766 particle BLASes of config C5, or one TLAS).  Equal Morton codes are ordered by sorted
+// position (the sort is stable, so by item index), making builds deterministic.
+//
+// Compiled with -ffp-contract=off: primitive boxes, centroids and the leaf-ordered hot / cold
+// records are computed with the reference's float evaluation order (host_math.hpp restates the
+// same functions on the host), so a GPU-built leaf holds the same bytes a host build would.
+#include <hip/hip_runtime.h>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "lbvh.hpp"
+
+namespace rtamd {
+namespace lbvh {
+
+constexpr int BLOCK = 256;
+constexpr uint32_t LEAF_BIT = 1u << 31;
+constexpr uint32_t NONE = 0xFFFFFFFFu;
+constexpr float FZERO = 1e-6f;                      // Global.cuh:147
+
+inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + BLOCK - 1) / BLOCK); }
+
+// ---- reference box / primitive arithmetic (host_math.hpp, device side) --------------------
+struct V3 { float x, y, z; };
+__device__ __forceinline__ V3 v3(float x, float y, float z) { V3 r; r.x = x; r.y = y; r.z = z; return r; }
+__device__ __forceinline__ V3 of(const rt_vec3 &a) { return v3(a.x, a.y, a.z); }
+__device__ __forceinline__ V3 operator+(V3 a, V3 b) { return v3(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ V3 operator-(V3 a, V3 b) { return v3(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ V3 operator*(V3 a, float s) { return v3(a.x * s, a.y * s, a.z * s); }
+__device__ __forceinline__ float comp(const V3 &a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+__device__ __forceinline__ float dot(V3 a, V3 b) {        // Vec3.cuh:113-119
+    float s = 0.0f; s += a.x * b.x; s += a.y * b.y; s += a.z * b.z; return s;
+}
+__device__ __forceinline__ V3 cross(V3 a, V3 b) {         // Vec3.cuh:120-126
+    return v3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+}
+__device__ __forceinline__ V3 unit(V3 a) {                // Vec3.cuh:129-137
+    const float f = 1.0f / sqrtf(dot(a, a));
+    return v3(a.x * f, a.y * f, a.z * f);
+}
+
+struct Box { float b[6]; };                                // {xmin,xmax,ymin,ymax,zmin,zmax}
+__device__ __forceinline__ float rlength(float mn, float mx) {   // Range.cuh: length()
+    return (mn >= mx || fabsf(mn - mx) < FZERO) ? 0.0f : mx - mn;
+}
+__device__ __forceinline__ Box from_points(V3 p1, V3 p2) {     // BoundingBox.cuh:24-28, 41-47
+    Box r;
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const float a = comp(p1, i), c = comp(p2, i);
+        float mn = a < c ? a : c, mx = a < c ? c : a;
+        if (rlength(mn, mx) < FZERO) { mn -= FZERO; mx += FZERO; }
+        r.b[2 * i] = mn; r.b[2 * i + 1] = mx;
+    }
+    return r;
+}
+__device__ __forceinline__ void merge_into(float *m, const float *a) {   // BoundingBox.cuh:50-55
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        m[2 * i] = a[2 * i] < m[2 * i] ? a[2 * i] : m[2 * i];
+        m[2 * i + 1] = a[2 * i + 1] > m[2 * i + 1] ? a[2 * i + 1] : m[2 * i + 1];
+    }
+}
+
+__device__ __forceinline__ void tri_box_centroid(const rt_triangle &t, Box &bx, V3 &c) {   // Triangle.cu:46-62, .cuh:53-61
+    V3 mn, mx;
+    float lo[3], hi[3], cc[3];
+#pragma unroll
+    for (int i = 0; i < 3; i++) {
+        const float a = comp(of(t.vertex[0]), i), b = comp(of(t.vertex[1]), i), d = comp(of(t.vertex[2]), i);
+        float l = a, h = a;
+        if (b < l) l = b;
+        if (d < l) l = d;
+        if (h < b) h = b;
+        if (h < d) h = d;
+        lo[i] = l; hi[i] = h;
+        float s = a + b + d;
+        s /= 3.0f;
+        cc[i] = s;
+    }
+    mn = v3(lo[0], lo[1], lo[2]); mx = v3(hi[0], hi[1], hi[2]);
+    bx = from_points(mn, mx);
+    c = v3(cc[0], cc[1], cc[2]);
+}
+__device__ __forceinline__ void sphere_box_centroid(const rt_sphere &s, Box &bx, V3 &c) {   // Sphere.cu:51-55
+    const V3 ce = of(s.center), e = v3(s.radius, s.radius, s.radius);
+    bx = from_points(ce - e, ce + e);
+    c = ce;
+}
+__device__ __forceinline__ void quad_box_centroid(const rt_parallelogram &p, Box &bx, V3 &c) {   // Parallelogram.cu:48-50 (q-centred), .cuh:45-47
+    const V3 h = (of(p.u) + of(p.v)) * 0.5f;
+    bx = from_points(of(p.q) + h, of(p.q) - h);
+    c = of(p.q) + of(p.u) * 0.5f + of(p.v) * 0.5f;
+}
+
+// ---- Morton / ordered-float helpers --------------------------------------------------------
+__device__ __forceinline__ uint32_t f2o(float f) {          // order-preserving float -> uint
+    const uint32_t u = __float_as_uint(f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float o2f(uint32_t u) {
+    return __uint_as_float((u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u);
+}
+__device__ __forceinline__ uint32_t expand10(uint32_t v) {  // 10 bits -> every third bit of 30
+    v = (v * 0x00010001u) & 0xFF0000FFu;
+    v = (v * 0x00000101u) & 0x0F00F00Fu;
+    v = (v * 0x00000011u) & 0xC30C30C3u;
+    v = (v * 0x00000005u) & 0x49249249u;
+    return v;
+}
+__device__ __forceinline__ uint32_t quant10(float c, float lo, float hi) {
+    const float ext = hi - lo;
+    if (!(ext > 0.0f)) return 0u;
+    const float q = (c - lo) / ext * 1024.0f;
+    if (!(q > 0.0f)) return 0u;
+    return q >= 1023.0f ? 1023u : (uint32_t)q;
+}
+
+__device__ __forceinline__ uint32_t seg_of_sorted(const unsigned long long *keys, uint32_t p) {
+    return (uint32_t)(keys[p] >> 32);
+}
+
+// ---- kernels -------------------------------------------------------------------------------
+__global__ void init_bounds_kernel(uint32_t *bounds, uint32_t n_segs) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n_segs * 6) return;
+    bounds[i] = (i & 1) ? 0u : 0xFFFFFFFFu;               // even: min slots, odd: max slots
+}
+
+__global__ void prep_blas_kernel(const LbvhSeg *segs, const uint32_t *seg_of, uint32_t n, RawPrimsGPU raw,
+                                 float *box, float4 *cent) {
+    const uint32_t it = blockIdx.x * BLOCK + threadIdx.x;
+    if (it >= n) return;
+    const LbvhSeg S = segs[seg_of[it]];
+    const uint32_t prim = S.prim_base + (it - S.item_base);
+    Box bx;
+    V3 c;
+    if (S.ptype == RT_PRIM_TRIANGLE) tri_box_centroid(raw.tris[prim], bx, c);
+    else if (S.ptype == RT_PRIM_SPHERE) sphere_box_centroid(raw.spheres[prim], bx, c);
+    else quad_box_centroid(raw.quads[prim], bx, c);
+#pragma unroll
+    for (int k = 0; k < 6; k++) box[6 * (size_t)it + k] = bx.b[k];
+    cent[it] = make_float4(c.x, c.y, c.z, 0.0f);
+}
+
+// Centroid bounds per segment: a wave whose 64 items share one segment reduces in registers and
+// issues 6 atomics; mixed waves (segment boundaries) fall back to per-lane atomics.
+__global__ void bounds_kernel(const uint32_t *seg_of, const float4 *cent, uint32_t n, uint32_t *bounds) {
+    const uint32_t it = blockIdx.x * BLOCK + threadIdx.x;
+    const bool valid = it < n;
+    const uint32_t seg = valid ? seg_of[it] : NONE;
+    float4 c = valid ? cent[it] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const uint32_t seg0 = __builtin_amdgcn_readfirstlane(seg);
+    const bool uniform = __all(seg == seg0);
+    if (uniform) {
+        if (seg0 == NONE) return;
+        float lo[3] = {c.x, c.y, c.z}, hi[3] = {c.x, c.y, c.z};
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                lo[a] = fminf(lo[a], __shfl_xor(lo[a], off));
+                hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off));
+            }
+        }
+        if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                atomicMin(&bounds[6 * seg0 + 2 * a], f2o(lo[a]));
+                atomicMax(&bounds[6 * seg0 + 2 * a + 1], f2o(hi[a]));
+            }
+        }
+        return;
+    }
+    if (!valid) return;
+    const float v[3] = {c.x, c.y, c.z};
+#pragma unroll
+    for (int a = 0; a < 3; a++) {
+        atomicMin(&bounds[6 * seg + 2 * a], f2o(v[a]));
+        atomicMax(&bounds[6 * seg + 2 * a + 1], f2o(v[a]));
+    }
+}
+
+__global__ void morton_kernel(const uint32_t *seg_of, const float4 *cent, uint32_t n, const uint32_t *bounds,
+                              unsigned long long *keys, uint32_t *vals) {
+    const uint32_t it = blockIdx.x * BLOCK + threadIdx.x;
+    if (it >= n) return;
+    const uint32_t seg = seg_of[it];
+    const float4 c = cent[it];
+    const uint32_t *B = bounds + 6 * seg;
+    const uint32_t x = quant10(c.x, o2f(B[0]), o2f(B[1]));
+    const uint32_t y = quant10(c.y, o2f(B[2]), o2f(B[3]));
+    const uint32_t z = quant10(c.z, o2f(B[4]), o2f(B[5]));
+    const uint32_t m = (expand10(x) << 2) | (expand10(y) << 1) | expand10(z);
+    keys[it] = ((unsigned long long)seg << 32) | m;
+    vals[it] = it;
+}
+
+// Karras 2012, one thread per interior node.  Local indices are positions inside the segment.
+__global__ void karras_kernel(const LbvhSeg *segs, const unsigned long long *keys, uint32_t n, uint32_t *child,
+                              uint32_t *parent, uint32_t *parent_leaf, uint32_t *range, uint32_t *flag) {
+    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= n) return;
+    const LbvhSeg S = segs[seg_of_sorted(keys, p)];
+    const int m = (int)S.count;
+    const int i = (int)(p - S.item_base);
+    const unsigned long long *K = keys + S.item_base;
+    if (m == 1) { parent_leaf[p] = NONE; return; }
+    if (i >= m - 1) return;
+    auto delta = [&](int a, int b) -> int {
+        if (b < 0 || b >= m) return -1;
+        const uint32_t ka = (uint32_t)K[a], kb = (uint32_t)K[b];
+        if (ka != kb) return __clz(ka ^ kb);
+        return 32 + __clz((uint32_t)a ^ (uint32_t)b);
+    };
+    const int d = (delta(i, i + 1) - delta(i, i - 1)) >= 0 ? 1 : -1;
+    const int dmin = delta(i, i - d);
+    int lmax = 2;
+    while (delta(i, i + lmax * d) > dmin) lmax <<= 1;
+    int l = 0;
+    for (int t = lmax >> 1; t >= 1; t >>= 1)
+        if (delta(i, i + (l + t) * d) > dmin) l += t;
+    const int j = i + l * d;
+    const int dnode = delta(i, j);
+    int s = 0, t = l;
+    do {
+        t = (t + 1) >> 1;
+        if (delta(i, i + (s + t) * d) > dnode) s += t;
+    } while (t > 1);
+    const int gamma = i + s * d + (d < 0 ? -1 : 0);
+    const int lo = i < j ? i : j, hi = i < j ? j : i;
+    const uint32_t g = S.node_base + (uint32_t)i;
+    uint32_t c0, c1;
+    if (lo == gamma) { c0 = LEAF_BIT | (S.item_base + (uint32_t)gamma); parent_leaf[S.item_base + gamma] = g; }
+    else { c0 = S.node_base + (uint32_t)gamma; parent[c0] = g; }
+    if (hi == gamma + 1) { c1 = LEAF_BIT | (S.item_base + (uint32_t)gamma + 1); parent_leaf[S.item_base + gamma + 1] = g; }
+    else { c1 = S.node_base + (uint32_t)gamma + 1; parent[c1] = g; }
+    child[2 * g] = c0;
+    child[2 * g + 1] = c1;
+    range[2 * g] = S.item_base + (uint32_t)lo;
+    range[2 * g + 1] = S.item_base + (uint32_t)hi;
+    flag[g] = 0;
+    if (i == 0) parent[g] = NONE;
+}
+
+__device__ __forceinline__ float ld_coherent(const float *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_coherent(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// Bottom-up box union: each leaf climbs; the second thread to reach a node finishes it.
+__global__ void bottom_up_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals,
+                                 const float *item_box, uint32_t n, const uint32_t *child, const uint32_t *parent,
+                                 const uint32_t *parent_leaf, const uint32_t *range, uint32_t *flag, float *nbox,
+                                 uint32_t *height, uint32_t *kept) {
+    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= n) return;
+    uint32_t g = parent_leaf[p];
+    if (g == NONE) return;
+    const uint32_t cap = segs[seg_of_sorted(keys, p)].leaf_cap;
+    while (g != NONE) {
+        __threadfence();
+        if (atomicAdd(&flag[g], 1u) == 0u) return;
+        __threadfence();
+        float b[6];
+        uint32_t h = 0;
+#pragma unroll
+        for (int c = 0; c < 2; c++) {
+            const uint32_t ch = child[2 * g + c];
+            float cb[6];
+            uint32_t chh = 0;
+            if (ch & LEAF_BIT) {
+                const float *src = item_box + 6 * (size_t)vals[ch & ~LEAF_BIT];
+#pragma unroll
+                for (int k = 0; k < 6; k++) cb[k] = src[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 6; k++) cb[k] = ld_coherent(nbox + 6 * (size_t)ch + k);
+                chh = ld_coherent(height + ch);
+            }
+            if (c == 0) {
+#pragma unroll
+                for (int k = 0; k < 6; k++) b[k] = cb[k];
+            } else {
+                merge_into(b, cb);
+            }
+            h = chh > h ? chh : h;
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) nbox[6 * (size_t)g + k] = b[k];
+        const uint32_t size = range[2 * g + 1] - range[2 * g] + 1u;
+        const bool keep = size > cap;
+        height[g] = keep ? h + 1u : 0u;
+        kept[g] = keep ? 1u : 0u;
+        g = parent[g];
+    }
+}
+
+struct ChildInfo { uint32_t ref; const float *box; };
+
+__device__ __forceinline__ uint32_t child_ref(const LbvhSeg &S, uint32_t ch, const uint32_t *range, const uint32_t *pidx) {
+    if (ch & LEAF_BIT)
+        return make_leaf_ref(S.slot_base + ((ch & ~LEAF_BIT) - S.item_base), 1u, S.ptype, S.blas != 0);
+    const uint32_t first = range[2 * ch], size = range[2 * ch + 1] - first + 1u;
+    if (size <= S.leaf_cap) return make_leaf_ref(S.slot_base + (first - S.item_base), size, S.ptype, S.blas != 0);
+    return make_interior_ref(pidx[ch], S.blas != 0);
+}
+__device__ __forceinline__ const float *child_box(uint32_t ch, const uint32_t *vals, const float *item_box, const float *nbox) {
+    return (ch & LEAF_BIT) ? item_box + 6 * (size_t)vals[ch & ~LEAF_BIT] : nbox + 6 * (size_t)ch;
+}
+
+__global__ void emit_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals, const float *item_box,
+                            uint32_t n_int, const uint32_t *child, const uint32_t *range, const float *nbox,
+                            const uint32_t *kept, const uint32_t *pidx, NodePair *pairs, uint32_t *pair_count) {
+    const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
+    if (g >= n_int) return;
+    if (g == n_int - 1 && pair_count) *pair_count = pidx[g] + kept[g];
+    if (!kept[g]) return;
+    const LbvhSeg S = segs[seg_of_sorted(keys, range[2 * g])];
+    const uint32_t c0 = child[2 * g], c1 = child[2 * g + 1];
+    const float *b0 = child_box(c0, vals, item_box, nbox), *b1 = child_box(c1, vals, item_box, nbox);
+    NodePair P;
+#pragma unroll
+    for (int k = 0; k < 6; k++) { P.c0[k] = b0[k]; P.c1[k] = b1[k]; }
+    P.ref0 = child_ref(S, c0, range, pidx);
+    P.ref1 = child_ref(S, c1, range, pidx);
+    P.pad0 = 0; P.pad1 = 0;
+    float4 *dst = reinterpret_cast<float4 *>(pairs + pidx[g]);
+    const float4 *src = reinterpret_cast<const float4 *>(&P);
+#pragma unroll
+    for (int k = 0; k < 4; k++) dst[k] = src[k];
+}
+
+__global__ void roots_kernel(const LbvhSeg *segs, uint32_t n_segs, const uint32_t *vals, const float *item_box,
+                             const float *nbox, const uint32_t *height, const uint32_t *pidx, TreeRoot *roots) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s >= n_segs) return;
+    const LbvhSeg S = segs[s];
+    TreeRoot R;
+    const float *b;
+    if (S.count == 0) {
+        for (int k = 0; k < 6; k++) R.box[k] = 0.0f;
+        R.ref = NONE; R.height = 0;
+        roots[s] = R;
+        return;
+    }
+    if (S.count == 1) {
+        b = item_box + 6 * (size_t)vals[S.item_base];
+        R.ref = make_leaf_ref(S.slot_base, 1u, S.ptype, S.blas != 0);
+        R.height = 0;
+    } else {
+        b = nbox + 6 * (size_t)S.node_base;
+        R.ref = S.count <= S.leaf_cap ? make_leaf_ref(S.slot_base, S.count, S.ptype, S.blas != 0)
+                                      : make_interior_ref(pidx[S.node_base], S.blas != 0);
+        R.height = height[S.node_base];
+    }
+    for (int k = 0; k < 6; k++) R.box[k] = b[k];
+    roots[s] = R;
+}
+
+// Leaf-ordered BLAS records (rt_api.cpp builds the same records on the host: Triangle.cuh:26-46,
+// Parallelogram.cuh:26-39).
+__device__ __forceinline__ uint32_t material_slot(uint32_t type, uint32_t index, uint32_t rough_count) {
+    return type == RT_MAT_ROUGH ? index : ((rough_count + index) | MAT_METAL_BIT);
+}
+
+__global__ void gather_blas_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals, uint32_t n,
+                                   RawPrimsGPU raw, PrimOutGPU out) {
+    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= n) return;
+    const LbvhSeg S = segs[seg_of_sorted(keys, p)];
+    const uint32_t slot = S.slot_base + (p - S.item_base);
+    const uint32_t prim = S.prim_base + (vals[p] - S.item_base);
+    if (S.ptype == RT_PRIM_TRIANGLE) {
+        const rt_triangle t = raw.tris[prim];
+        const V3 v0 = of(t.vertex[0]);
+        const V3 e1 = of(t.vertex[1]) - v0, e2 = of(t.vertex[2]) - v0;
+        V3 nn[3];
+        if (t.has_normals) { nn[0] = of(t.normal[0]); nn[1] = of(t.normal[1]); nn[2] = of(t.normal[2]); }
+        else { const V3 u = unit(cross(e1, e2)); nn[0] = u; nn[1] = u; nn[2] = u; }
+        TriHot H;
+        H.v0[0] = v0.x; H.v0[1] = v0.y; H.v0[2] = v0.z; H.pad0 = 0.0f;
+        H.e1[0] = e1.x; H.e1[1] = e1.y; H.e1[2] = e1.z; H.pad1 = 0.0f;
+        H.e2[0] = e2.x; H.e2[1] = e2.y; H.e2[2] = e2.z; H.pad2 = 0.0f;
+        TriCold C;
+        C.n0[0] = nn[0].x; C.n0[1] = nn[0].y; C.n0[2] = nn[0].z;
+        C.n1[0] = nn[1].x; C.n1[1] = nn[1].y; C.n1[2] = nn[1].z;
+        C.n2[0] = nn[2].x; C.n2[1] = nn[2].y; C.n2[2] = nn[2].z;
+        C.material = material_slot(t.material_type, t.material_index, raw.rough_count);
+        C.orig_index = prim;
+        C.pad = 0;
+        out.tri_hot[slot] = H;
+        out.tri_cold[slot] = C;
+    } else if (S.ptype == RT_PRIM_SPHERE) {
+        const rt_sphere sp = raw.spheres[prim];
+        SphereHot H;
+        H.center[0] = sp.center.x; H.center[1] = sp.center.y; H.center[2] = sp.center.z; H.radius = sp.radius;
+        PrimCold C;
+        C.material = material_slot(sp.material_type, sp.material_index, raw.rough_count);
+        C.orig_index = prim; C.pad0 = 0; C.pad1 = 0;
+        out.sph_hot[slot] = H;
+        out.sph_cold[slot] = C;
+    } else {
+        const rt_parallelogram q = raw.quads[prim];
+        const V3 nx = cross(of(q.u), of(q.v));
+        const V3 nn = unit(nx);
+        float d = 0.0f;
+        d += nn.x * q.q.x; d += nn.y * q.q.y; d += nn.z * q.q.z;
+        QuadHot H;
+        H.n[0] = nn.x; H.n[1] = nn.y; H.n[2] = nn.z; H.d = d;
+        H.q[0] = q.q.x; H.q[1] = q.q.y; H.q[2] = q.q.z; H.den = dot(nx, nx);
+        H.u[0] = q.u.x; H.u[1] = q.u.y; H.u[2] = q.u.z; H.pad0 = 0.0f;
+        H.v[0] = q.v.x; H.v[1] = q.v.y; H.v[2] = q.v.z; H.pad1 = 0.0f;
+        H.nx[0] = nx.x; H.nx[1] = nx.y; H.nx[2] = nx.z; H.pad2 = 0.0f;
+        PrimCold C;
+        C.material = material_slot(q.material_type, q.material_index, raw.rough_count);
+        C.orig_index = prim; C.pad0 = 0; C.pad1 = 0;
+        out.quad_hot[slot] = H;
+        out.quad_cold[slot] = C;
+    }
+}
+
+__global__ void gather_items_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals, uint32_t n,
+                                    uint32_t *slots) {
+    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
+    if (p >= n) return;
+    const LbvhSeg S = segs[seg_of_sorted(keys, p)];
+    slots[S.slot_base + (p - S.item_base)] = vals[p];
+}
+
+}  // namespace lbvh
+
+// ---- host --------------------------------------------------------------------------------------
+using namespace lbvh;
+
+#define LB_TRY(x)                               \
+    do {                                        \
+        hipError_t e_ = (x);                    \
+        if (e_ != hipSuccess) return e_;        \
+    } while (0)
+
+template <typename T>
+static hipError_t dalloc(T *&p, size_t n) {
+    return hipMalloc(reinterpret_cast<void **>(&p), (n ? n : 1) * sizeof(T));
+}
+template <typename T>
+static void dfree(T *&p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+void LbvhBuilder::release() {
+    dfree(segs_); dfree(seg_of_); dfree(own_box_); dfree(own_cent_); dfree(bounds_);
+    dfree(k0_); dfree(k1_); dfree(v0_); dfree(v1_); dfree(child_); dfree(parent_); dfree(parent_leaf_);
+    dfree(range_); dfree(flag_); dfree(height_); dfree(nbox_); dfree(kept_); dfree(pidx_);
+    if (tmp_) (void)hipFree(tmp_);
+    tmp_ = nullptr; tmp_bytes_ = 0;
+    box_ = nullptr; cent_ = nullptr;
+    n_items_ = n_segs_ = seg_bits_ = 0;
+}
+
+hipError_t LbvhBuilder::init(const std::vector<LbvhSeg> &segs, hipStream_t stream) {
+    release();
+    uint64_t n = 0;
+    for (const LbvhSeg &s : segs) {
+        if (s.item_base != n || s.leaf_cap < 1 || s.leaf_cap > 4) return hipErrorInvalidValue;
+        n += s.count;
+    }
+    if (n >= (1ull << 31) || segs.empty()) return hipErrorInvalidValue;
+    n_items_ = (uint32_t)n;
+    n_segs_ = (uint32_t)segs.size();
+    seg_bits_ = 0;
+    while ((1ull << seg_bits_) < n_segs_) seg_bits_++;
+    const size_t N = n_items_, NI = max_pairs();
+    LB_TRY(dalloc(segs_, n_segs_));
+    LB_TRY(hipMemcpyAsync(segs_, segs.data(), n_segs_ * sizeof(LbvhSeg), hipMemcpyHostToDevice, stream));
+    std::vector<uint32_t> seg_of(N);
+    for (uint32_t s = 0; s < n_segs_; s++)
+        for (uint32_t k = 0; k < segs[s].count; k++) seg_of[segs[s].item_base + k] = s;
+    LB_TRY(dalloc(seg_of_, N));
+    LB_TRY(hipMemcpyAsync(seg_of_, seg_of.data(), N * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+    LB_TRY(dalloc(bounds_, 6 * (size_t)n_segs_));
+    LB_TRY(dalloc(k0_, N)); LB_TRY(dalloc(k1_, N)); LB_TRY(dalloc(v0_, N)); LB_TRY(dalloc(v1_, N));
+    LB_TRY(dalloc(child_, 2 * NI)); LB_TRY(dalloc(parent_, NI)); LB_TRY(dalloc(parent_leaf_, N));
+    LB_TRY(dalloc(range_, 2 * NI)); LB_TRY(dalloc(flag_, NI)); LB_TRY(dalloc(height_, NI));
+    LB_TRY(dalloc(nbox_, 6 * NI)); LB_TRY(dalloc(kept_, NI)); LB_TRY(dalloc(pidx_, NI));
+    size_t sort_bytes = 0, scan_bytes = 0;
+    LB_TRY(rocprim::radix_sort_pairs(nullptr, sort_bytes, k0_, k1_, v0_, v1_, N, 0, 32 + seg_bits_, stream));
+    LB_TRY(rocprim::exclusive_scan(nullptr, scan_bytes, kept_, pidx_, 0u, NI, rocprim::plus<uint32_t>(), stream));
+    tmp_bytes_ = sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
+    LB_TRY(hipMalloc(&tmp_, tmp_bytes_ ? tmp_bytes_ : 1));
+    // kept/pidx of nodes that no thread visits (none in a valid forest) start defined
+    LB_TRY(hipMemsetAsync(kept_, 0, NI * sizeof(uint32_t), stream));
+    // synchronous: seg_of (host vector) must outlive the copy
+    return hipStreamSynchronize(stream);
+}
+
+hipError_t LbvhBuilder::prep_blas_items(const RawPrimsGPU &raw, hipStream_t stream) {
+    if (!own_box_) {
+        LB_TRY(dalloc(own_box_, 6 * (size_t)n_items_));
+        LB_TRY(dalloc(own_cent_, n_items_));
+    }
+    box_ = own_box_;
+    cent_ = own_cent_;
+    hipLaunchKernelGGL(prep_blas_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, seg_of_, n_items_, raw,
+                       box_, cent_);
+    return hipGetLastError();
+}
+
+hipError_t LbvhBuilder::set_items(const float *boxes, const float4 *centroids) {
+    box_ = const_cast<float *>(boxes);
+    cent_ = const_cast<float4 *>(centroids);
+    return hipSuccess;
+}
+
+hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_count, hipStream_t stream) {
+    if (!box_ || !cent_ || n_items_ == 0) return hipErrorInvalidValue;
+    const uint32_t N = n_items_, NI = n_items_ - n_segs_;
+    hipLaunchKernelGGL(init_bounds_kernel, dim3(blocks_for(6ull * n_segs_)), dim3(BLOCK), 0, stream, bounds_, n_segs_);
+    hipLaunchKernelGGL(bounds_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, seg_of_, cent_, N, bounds_);
+    hipLaunchKernelGGL(morton_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, seg_of_, cent_, N, bounds_, k0_, v0_);
+    LB_TRY(hipGetLastError());
+    size_t bytes = tmp_bytes_;
+    LB_TRY(rocprim::radix_sort_pairs(tmp_, bytes, k0_, k1_, v0_, v1_, N, 0, 32 + seg_bits_, stream));
+    hipLaunchKernelGGL(karras_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, k1_, N, child_, parent_,
+                       parent_leaf_, range_, flag_);
+    hipLaunchKernelGGL(bottom_up_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, box_, N, child_,
+                       parent_, parent_leaf_, range_, flag_, nbox_, height_, kept_);
+    LB_TRY(hipGetLastError());
+    if (NI > 0) {
+        bytes = tmp_bytes_;
+        LB_TRY(rocprim::exclusive_scan(tmp_, bytes, kept_, pidx_, 0u, NI, rocprim::plus<uint32_t>(), stream));
+        hipLaunchKernelGGL(emit_kernel, dim3(blocks_for(NI)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, box_, NI, child_,
+                           range_, nbox_, kept_, pidx_, pairs, pair_count);
+    } else if (pair_count) {
+        LB_TRY(hipMemsetAsync(pair_count, 0, sizeof(uint32_t), stream));
+    }
+    hipLaunchKernelGGL(roots_kernel, dim3(blocks_for(n_segs_)), dim3(BLOCK), 0, stream, segs_, n_segs_, v1_, box_, nbox_,
+                       height_, pidx_, roots);
+    return hipGetLastError();
+}
+
+hipError_t LbvhBuilder::gather_blas(const RawPrimsGPU &raw, const PrimOutGPU &out, hipStream_t stream) {
+    hipLaunchKernelGGL(gather_blas_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, n_items_,
+                       raw, out);
+    return hipGetLastError();
+}
+
+hipError_t LbvhBuilder::gather_items(uint32_t *slots, hipStream_t stream) {
+    hipLaunchKernelGGL(gather_items_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, n_items_,
+                       slots);
+    return hipGetLastError();
+}
+
+}  // namespace rtamd
+
+namespace rtamd {
+namespace lbvh {
+// Per-frame: copy each instance's BLAS root {box, ref} into its hot record (the host staging block
+// carries the matrices; the roots of GPU-built BLASes live only in HBM).
+__global__ void patch_roots_kernel(InstHot *hot, const uint32_t *inst_blas, const TreeRoot *roots, uint32_t n) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    const TreeRoot R = roots[inst_blas[i]];
+#pragma unroll
+    for (int k = 0; k < 6; k++) hot[i].root_box[k] = R.box[k];
+    hot[i].root_ref = R.ref;
+    hot[i].pad = 0;
+}
+}  // namespace lbvh
+
+hipError_t launch_patch_inst_roots(InstHot *hot, const uint32_t *inst_blas, const TreeRoot *roots, uint32_t n,
+                                   hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(lbvh::patch_roots_kernel, dim3(lbvh::blocks_for(n)), dim3(lbvh::BLOCK), 0, stream, hot, inst_blas,
+                       roots, n);
+    return hipGetLastError();
+}
+}  // namespace rtamd

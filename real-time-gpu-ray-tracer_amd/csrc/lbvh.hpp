@@ -1,0 +1,108 @@
+// lbvh.hpp — host interface of the GPU BVH builder (RT_BUILD_LBVH, lbvh.hip).
+//
+// The reference builds every BLAS once and the TLAS every frame on the host with a random-axis
+// median split (src/AS/BLAS.cu:4-117, src/AS/TLAS.cu:4-129, driven from Renderer.cu:123-155 and
+// :269-293).  SURVEY §8f rows 1-2 move both builds onto the GPU so that a frame never waits on a
+// host build, and so that a 10 M-triangle scene (config C5) can rebuild its BLASes every frame.
+//
+// One builder instance owns the device workspace of one forest: a set of independent trees
+// ("segments") over disjoint, contiguous item ranges.  A build is a fixed sequence of kernels on
+// one stream, no host synchronisation:
+//   centroid bounds per segment -> 30-bit Morton key per item, segment id in the high word ->
+//   radix sort (rocPRIM) -> Karras radix-tree hierarchy per segment -> bottom-up box union
+//   (atomic arrival counters) -> subtrees of <= leaf_cap items collapse into leaves, the surviving
+//   interior nodes are compacted (exclusive scan) into the node-pair layout of layout.hpp ->
+//   per-segment root {box, ref}.
+// Item boxes are exact unions (min/max) of the ε-expanded primitive boxes the reference builds
+// (BoundingBox.cuh:24-55), so every node box equals the one a host build over the same leaf sets
+// would produce, bit for bit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "layout.hpp"
+#include "../../include/rt.h"
+
+namespace rtamd {
+
+struct LbvhSeg {            // one tree of the forest
+    uint32_t item_base;     // first item (= first sorted position) of the segment
+    uint32_t count;         // items
+    uint32_t slot_base;     // first leaf slot of the tree in its (leaf-ordered) output array
+    uint32_t prim_base;     // BLAS: caller primitive index of item item_base
+    uint32_t ptype;         // BLAS: rt_primitive_type
+    uint32_t node_base;     // first Karras interior node = item_base - segment index
+    uint32_t leaf_cap;      // subtrees of <= leaf_cap items become one leaf (<= 4)
+    uint32_t blas;          // 1: BLAS-level refs
+};
+
+// Raw caller primitives in HBM (the builder recomputes boxes, centroids and the leaf-ordered hot /
+// cold records from them on every BLAS build).
+struct RawPrimsGPU {
+    const rt_triangle *tris;
+    const rt_sphere *spheres;
+    const rt_parallelogram *quads;
+    uint32_t rough_count;   // material slot of metal m = rough_count + m
+};
+
+struct PrimOutGPU {         // leaf-ordered arrays written by the BLAS gather
+    TriHot *tri_hot; TriCold *tri_cold;
+    SphereHot *sph_hot; PrimCold *sph_cold;
+    QuadHot *quad_hot; PrimCold *quad_cold;
+};
+
+class LbvhBuilder {
+public:
+    LbvhBuilder() = default;
+    LbvhBuilder(const LbvhBuilder &) = delete;
+    LbvhBuilder &operator=(const LbvhBuilder &) = delete;
+    ~LbvhBuilder() { release(); }
+
+    // Allocates the workspace for `segs` (item ranges must tile [0, n_items) in order).
+    hipError_t init(const std::vector<LbvhSeg> &segs, hipStream_t stream);
+    void release();
+
+    uint32_t items() const { return n_items_; }
+    uint32_t segments() const { return n_segs_; }
+    uint32_t max_pairs() const { return n_items_ > n_segs_ ? n_items_ - n_segs_ : 1u; }
+
+    // BLAS items: boxes / centroids of the segments' primitives (reference box semantics).
+    hipError_t prep_blas_items(const RawPrimsGPU &raw, hipStream_t stream);
+    // TLAS items: caller-provided boxes (6 floats per item) and centroids (4 floats per item).
+    hipError_t set_items(const float *boxes, const float4 *centroids);
+
+    // Builds every segment: pairs written from index 0 of `pairs` (capacity max_pairs()),
+    // roots[s] receives segment s's root; `pair_count` (device, may be null) the pairs written.
+    hipError_t build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_count, hipStream_t stream);
+
+    // After build(): leaf-ordered BLAS primitive records.
+    hipError_t gather_blas(const RawPrimsGPU &raw, const PrimOutGPU &out, hipStream_t stream);
+    // After build(): item index per leaf slot (TLAS: instance index per slot).
+    hipError_t gather_items(uint32_t *slots, hipStream_t stream);
+
+private:
+    uint32_t n_items_ = 0, n_segs_ = 0, seg_bits_ = 0;
+    LbvhSeg *segs_ = nullptr;
+    uint32_t *seg_of_ = nullptr;          // item -> segment
+    float *box_ = nullptr;                // 6 floats per item (owned or caller's)
+    float4 *cent_ = nullptr;
+    float *own_box_ = nullptr;
+    float4 *own_cent_ = nullptr;
+    uint32_t *bounds_ = nullptr;          // 6 ordered-uint per segment (centroid bounds)
+    unsigned long long *k0_ = nullptr, *k1_ = nullptr;
+    uint32_t *v0_ = nullptr, *v1_ = nullptr;
+    uint32_t *child_ = nullptr;           // 2 per interior node: LEAF_BIT | sorted position, or node
+    uint32_t *parent_ = nullptr;          // per interior node
+    uint32_t *parent_leaf_ = nullptr;     // per sorted position
+    uint32_t *range_ = nullptr;           // 2 per interior node: first, last sorted position
+    uint32_t *flag_ = nullptr;            // arrival counters
+    uint32_t *height_ = nullptr;          // per interior node
+    float *nbox_ = nullptr;               // 6 per interior node
+    uint32_t *kept_ = nullptr, *pidx_ = nullptr;
+    void *tmp_ = nullptr;
+    size_t tmp_bytes_ = 0;
+};
+
+}  // namespace rtamd

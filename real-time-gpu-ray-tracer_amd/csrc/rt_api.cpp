@@ -20,6 +20,7 @@
 #include "bvh_build.hpp"
 #include "host_math.hpp"
 #include "layout.hpp"
+#include "lbvh.hpp"
 
 namespace rtamd {
 hipError_t launch_render_exact(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *, hipStream_t);
@@ -32,6 +33,7 @@ hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, c
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean);
+hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, uint32_t, hipStream_t);
 uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean);
 }  // namespace rtamd
 
@@ -57,6 +59,8 @@ rt_status fail(rt_status s, const std::string &msg) {
 constexpr uint32_t BLAS_LEAF_CAP = 4;   // BLAS.cuh:17
 constexpr uint32_t TLAS_LEAF_CAP = 2;   // TLAS.cuh:22
 constexpr uint32_t SAH_LEAF_CAP = 4;    // RT_BUILD_SAH: <= 4 items per leaf (2-bit count in a leaf ref)
+constexpr uint32_t LBVH_BLAS_LEAF_CAP = 4;
+constexpr uint32_t LBVH_TLAS_LEAF_CAP = 2;   // the reference's TLAS leaf size (TLAS.cuh:22)
 
 struct InstState {
     uint32_t ptype, pindex, pcount, blas;
@@ -118,15 +122,16 @@ struct rt_scene {
     DevBuf<float> materials;
     uint64_t blas_pair_count = 0, blas_leaf_count = 0;
 
-    // per-frame data, double-buffered: [tlas pairs | tlas slots | inst hot | inst cold]
-    size_t frame_block = 0, off_slots = 0, off_hot = 0, off_cold = 0;
+    // per-frame data, double-buffered:
+    //   [tlas root | tlas pairs | tlas slots | inst hot | inst cold | tlas item boxes | tlas item centroids]
+    // (the root and the item arrays are used by GPU-built TLASes only)
+    size_t frame_block = 0, off_root = 0, off_pairs = 0, off_slots = 0, off_hot = 0, off_cold = 0, off_tbox = 0,
+           off_tcent = 0;
     uint8_t *staging[2] = {nullptr, nullptr};     // pinned host
     uint8_t *frame_dev[2] = {nullptr, nullptr};   // HBM
     hipEvent_t ev_copied[2] = {nullptr, nullptr}; // upload from staging[b] finished
     hipEvent_t ev_used[2] = {nullptr, nullptr};   // last kernel reading frame_dev[b] finished
     int active = -1;
-    uint32_t tlas_root_ref = 0;
-    float tlas_root_box[6] = {0, 0, 0, 0, 0, 0};
 
     hipStream_t stream = nullptr;
     hipEvent_t k_start = nullptr, k_stop = nullptr;
@@ -165,12 +170,30 @@ struct rt_scene {
     DevBuf<uint8_t> out_rgba;
     DevBuf<float> out_rgb;
 
+    // RT_BUILD_LBVH: GPU builders and the raw caller primitives they read
+    LbvhBuilder *blas_builder = nullptr, *tlas_builder = nullptr;
+    DevBuf<rt_triangle> raw_tris;
+    DevBuf<rt_sphere> raw_sph;
+    DevBuf<rt_parallelogram> raw_quad;
+    DevBuf<TreeRoot> blas_roots;        // per unique BLAS
+    DevBuf<uint32_t> inst_blas;         // instance -> BLAS
+    DevBuf<uint32_t> gpu_counts;        // [0] BLAS pairs written, [1] TLAS pairs written (last frame)
+    bool rebuild_blas = false;          // option "rebuild": rebuild every BLAS each frame
+    bool blas_dirty = false;            // rt_scene_update_triangles since the last BLAS build
+    uint64_t blas_builds = 0;
+    hipEvent_t ev_render_done = nullptr;   // last trace launch finished (BLAS rebuilds wait on it)
+    bool gpu_tlas() const { return build_mode == RT_BUILD_LBVH; }
+
     ~rt_scene() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         blas_pairs.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
         quad_hot.release(); quad_cold.release(); materials.release(); out_rgba.release(); out_rgb.release();
         timeline.release(); costmap.release();
+        delete blas_builder; delete tlas_builder;
+        raw_tris.release(); raw_sph.release(); raw_quad.release(); blas_roots.release(); inst_blas.release();
+        gpu_counts.release();
+        if (ev_render_done) (void)hipEventDestroy(ev_render_done);
         for (int b = 0; b < 2; b++) {
             if (staging[b]) (void)hipHostFree(staging[b]);
             if (frame_dev[b]) (void)hipFree(frame_dev[b]);
@@ -228,7 +251,11 @@ void store_rows(float *dst, const hm::Mat &m) {   // rows 1..3, cols 1..4
         for (int j = 0; j < 4; j++) dst[4 * i + j] = m.d[i + 1][j + 1];
 }
 
+rt_status gpu_build_blas(rt_scene *s);
+
 // Host half of one frame: update callback, instance matrices, TLAS rebuild, staging, upload.
+// RT_BUILD_LBVH: the host stages matrices and transformed instance boxes only; the BLAS roots are
+// patched into the instance records and the TLAS is built by kernels on the scene's stream.
 rt_status frame_update(rt_scene *s, uint64_t frame) {
     const int b = s->active < 0 ? 0 : 1 - s->active;
     HIP_TRY(hipEventSynchronize(s->ev_copied[b]));     // staging[b] no longer read by a pending copy
@@ -238,20 +265,55 @@ rt_status frame_update(rt_scene *s, uint64_t frame) {
         s->update(s->update_user, xs.data(), xs.size(), frame);
         for (size_t i = 0; i < xs.size(); i++) instance_update(s->inst[i], xs[i]);
     }
+    uint8_t *st = s->staging[b];
+    InstHot *hot = reinterpret_cast<InstHot *>(st + s->off_hot);
+    InstCold *cold = reinterpret_cast<InstCold *>(st + s->off_cold);
+    if (s->gpu_tlas()) {
+        float *tbox = reinterpret_cast<float *>(st + s->off_tbox);
+        float *tcent = reinterpret_cast<float *>(st + s->off_tcent);
+        for (size_t i = 0; i < s->inst.size(); i++) {
+            const InstState &in = s->inst[i];
+            store_rows(hot[i].inv, in.inv);
+            store_rows(cold[i].fwd, in.fwd);
+            store_rows(cold[i].nrm, in.nrm);
+            in.tbox.store(tbox + 6 * i);
+            tcent[4 * i] = in.tcentroid.x; tcent[4 * i + 1] = in.tcentroid.y; tcent[4 * i + 2] = in.tcentroid.z;
+            tcent[4 * i + 3] = 0.0f;
+        }
+        uint8_t *fd = s->frame_dev[b];
+        HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_used[b], 0));
+        HIP_TRY(hipMemcpyAsync(fd, st, s->frame_block, hipMemcpyHostToDevice, s->stream));
+        if (s->rebuild_blas || s->blas_dirty) {
+            const rt_status bs = gpu_build_blas(s);
+            if (bs != RT_OK) return bs;
+        }
+        const uint32_t n = (uint32_t)s->inst.size();
+        HIP_TRY(launch_patch_inst_roots(reinterpret_cast<InstHot *>(fd + s->off_hot), s->inst_blas.p, s->blas_roots.p, n,
+                                        s->stream));
+        HIP_TRY(s->tlas_builder->set_items(reinterpret_cast<const float *>(fd + s->off_tbox),
+                                           reinterpret_cast<const float4 *>(fd + s->off_tcent)));
+        HIP_TRY(s->tlas_builder->build(reinterpret_cast<NodePair *>(fd + s->off_pairs), reinterpret_cast<TreeRoot *>(fd + s->off_root),
+                                       s->gpu_counts.p + 1, s->stream));
+        HIP_TRY(s->tlas_builder->gather_items(reinterpret_cast<uint32_t *>(fd + s->off_slots), s->stream));
+        HIP_TRY(hipEventRecord(s->ev_copied[b], s->stream));
+        s->active = b;
+        s->frame = frame;
+        return RT_OK;
+    }
     // TLAS::constructTLAS over transformed instance boxes (Renderer.cu:275, TLAS.cu:4-129)
     std::vector<BuildItem> items(s->inst.size());
     for (size_t i = 0; i < items.size(); i++) items[i] = {s->inst[i].tbox, s->inst[i].tcentroid, (uint32_t)i};
     s->tlas = s->build_mode == RT_BUILD_SAH ? build_sah_tree(std::move(items), SAH_LEAF_CAP)
                                             : build_median_tree(std::move(items), TLAS_LEAF_CAP, hm::tlas_axis_state(s->build_seed, frame));
     s->tlas_flat = flatten_tree(s->tlas, 0, 0, 0, false);
-    s->tlas_root_ref = s->tlas_flat.root_ref;
-    std::memcpy(s->tlas_root_box, s->tlas_flat.root_box, sizeof s->tlas_root_box);
 
-    uint8_t *st = s->staging[b];
-    std::memcpy(st, s->tlas_flat.pairs.data(), s->tlas_flat.pairs.size() * sizeof(NodePair));
+    TreeRoot root{};
+    std::memcpy(root.box, s->tlas_flat.root_box, sizeof root.box);
+    root.ref = s->tlas_flat.root_ref;
+    root.height = s->tlas_flat.height;
+    std::memcpy(st + s->off_root, &root, sizeof root);
+    std::memcpy(st + s->off_pairs, s->tlas_flat.pairs.data(), s->tlas_flat.pairs.size() * sizeof(NodePair));
     std::memcpy(st + s->off_slots, s->tlas.refs.data(), s->tlas.refs.size() * sizeof(uint32_t));
-    InstHot *hot = reinterpret_cast<InstHot *>(st + s->off_hot);
-    InstCold *cold = reinterpret_cast<InstCold *>(st + s->off_cold);
     for (size_t i = 0; i < s->inst.size(); i++) {
         const InstState &in = s->inst[i];
         const BlasHost &bl = s->blas[in.blas];
@@ -274,7 +336,8 @@ SceneGPU scene_gpu(const rt_scene *s) {
     SceneGPU g{};
     const int b = s->active;
     g.blas_pairs = s->blas_pairs.p;
-    g.tlas_pairs = reinterpret_cast<const NodePair *>(s->frame_dev[b]);
+    g.tlas_pairs = reinterpret_cast<const NodePair *>(s->frame_dev[b] + s->off_pairs);
+    g.tlas_root = reinterpret_cast<const TreeRoot *>(s->frame_dev[b] + s->off_root);
     g.tlas_slots = reinterpret_cast<const uint32_t *>(s->frame_dev[b] + s->off_slots);
     g.inst_hot = reinterpret_cast<const InstHot *>(s->frame_dev[b] + s->off_hot);
     g.inst_cold = reinterpret_cast<const InstCold *>(s->frame_dev[b] + s->off_cold);
@@ -282,8 +345,6 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.sph_hot = s->sph_hot.p; g.sph_cold = s->sph_cold.p;
     g.quad_hot = s->quad_hot.p; g.quad_cold = s->quad_cold.p;
     g.materials = s->materials.p;
-    std::memcpy(g.tlas_root_box, s->tlas_root_box, sizeof g.tlas_root_box);
-    g.tlas_root_ref = s->tlas_root_ref;
     g.instance_count = (uint32_t)s->inst.size();
     g.rough_count = (uint32_t)s->roughs.size();
     return g;
@@ -296,6 +357,73 @@ rt_status upload(DevBuf<T> &buf, const std::vector<T> &v) {
     HIP_TRY(hipMalloc(&buf.p, n * sizeof(T)));
     buf.n = v.size();
     if (!v.empty()) HIP_TRY(hipMemcpy(buf.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return RT_OK;
+}
+
+template <typename T>
+rt_status alloc_buf(DevBuf<T> &buf, size_t n) {
+    buf.release();
+    HIP_TRY(hipMalloc(&buf.p, (n ? n : 1) * sizeof(T)));
+    buf.n = n;
+    return RT_OK;
+}
+
+// RT_BUILD_LBVH: rebuild every BLAS on the GPU (prep -> Morton -> sort -> Karras -> boxes -> pairs ->
+// leaf-ordered primitive records), on the scene stream, after the last trace that read them.
+rt_status gpu_build_blas(rt_scene *s) {
+    if (s->blas_builds && s->ev_render_done) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_render_done, 0));
+    const RawPrimsGPU raw{s->raw_tris.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
+    const PrimOutGPU out{s->tri_hot.p, s->tri_cold.p, s->sph_hot.p, s->sph_cold.p, s->quad_hot.p, s->quad_cold.p};
+    HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
+    HIP_TRY(s->blas_builder->build(s->blas_pairs.p, s->blas_roots.p, s->gpu_counts.p, s->stream));
+    HIP_TRY(s->blas_builder->gather_blas(raw, out, s->stream));
+    s->blas_dirty = false;
+    s->blas_builds++;
+    return RT_OK;
+}
+
+// RT_BUILD_LBVH: upload the raw primitives, allocate the leaf-ordered arrays, build every BLAS once.
+rt_status gpu_setup_blas(rt_scene *s, const std::vector<LbvhSeg> &segs, const uint32_t *slot_count) {
+    bool ok = true;                                  // the host builds check the same materials
+    for (const LbvhSeg &g : segs)
+        for (uint32_t k = 0; k < g.count; k++) {
+            const uint32_t pi = g.prim_base + k;
+            if (g.ptype == RT_PRIM_TRIANGLE) material_slot(s, s->tris[pi].material_type, s->tris[pi].material_index, ok);
+            else if (g.ptype == RT_PRIM_SPHERE) material_slot(s, s->spheres[pi].material_type, s->spheres[pi].material_index, ok);
+            else material_slot(s, s->quads[pi].material_type, s->quads[pi].material_index, ok);
+        }
+    if (!ok) return fail(RT_ERR_INVALID_ARGUMENT, "primitive references a material out of range");
+    rt_status st;
+    if ((st = upload(s->raw_tris, s->tris)) != RT_OK) return st;
+    if ((st = upload(s->raw_sph, s->spheres)) != RT_OK) return st;
+    if ((st = upload(s->raw_quad, s->quads)) != RT_OK) return st;
+    if ((st = alloc_buf(s->tri_hot, slot_count[RT_PRIM_TRIANGLE])) != RT_OK) return st;
+    if ((st = alloc_buf(s->tri_cold, slot_count[RT_PRIM_TRIANGLE])) != RT_OK) return st;
+    if ((st = alloc_buf(s->sph_hot, slot_count[RT_PRIM_SPHERE])) != RT_OK) return st;
+    if ((st = alloc_buf(s->sph_cold, slot_count[RT_PRIM_SPHERE])) != RT_OK) return st;
+    if ((st = alloc_buf(s->quad_hot, slot_count[RT_PRIM_PARALLELOGRAM])) != RT_OK) return st;
+    if ((st = alloc_buf(s->quad_cold, slot_count[RT_PRIM_PARALLELOGRAM])) != RT_OK) return st;
+    delete s->blas_builder;
+    s->blas_builder = new LbvhBuilder();
+    HIP_TRY(s->blas_builder->init(segs, s->stream));
+    if ((st = alloc_buf(s->blas_pairs, s->blas_builder->max_pairs())) != RT_OK) return st;
+    if ((st = alloc_buf(s->blas_roots, segs.size())) != RT_OK) return st;
+    if ((st = alloc_buf(s->gpu_counts, 2)) != RT_OK) return st;
+    std::vector<uint32_t> ib(s->inst.size());
+    for (size_t i = 0; i < ib.size(); i++) ib[i] = s->inst[i].blas;
+    if ((st = upload(s->inst_blas, ib)) != RT_OK) return st;
+    if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
+    s->blas_builds = 0;
+    if ((st = gpu_build_blas(s)) != RT_OK) return st;
+    // one-time readback for introspection (rt_scene_get_info)
+    uint32_t pairs = 0;
+    std::vector<TreeRoot> roots(segs.size());
+    HIP_TRY(hipStreamSynchronize(s->stream));
+    HIP_TRY(hipMemcpy(&pairs, s->gpu_counts.p, sizeof pairs, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(roots.data(), s->blas_roots.p, roots.size() * sizeof(TreeRoot), hipMemcpyDeviceToHost));
+    s->blas_pair_count = pairs;
+    s->blas_leaf_count = pairs + segs.size();        // binary trees: leaves = interior nodes + 1
+    for (const TreeRoot &r : roots) s->max_blas_height = std::max(s->max_blas_height, r.height);
     return RT_OK;
 }
 
@@ -356,7 +484,8 @@ rt_status rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
 
 rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
-    if (mode != RT_BUILD_COMPAT_MEDIAN && mode != RT_BUILD_SAH) return fail(RT_ERR_UNSUPPORTED, "unsupported build mode");
+    if (mode != RT_BUILD_COMPAT_MEDIAN && mode != RT_BUILD_SAH && mode != RT_BUILD_LBVH)
+        return fail(RT_ERR_UNSUPPORTED, "unsupported build mode");
     HIP_TRY(hipSetDevice(s->device));
     s->build_seed = seed;
     s->build_mode = mode;
@@ -368,6 +497,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     // The reference's map stores the instance index instead of the BLAS index (RenderPin.cu:151);
     // the BLAS index is stored here (identical whenever the reference's demo order is used).
     std::vector<std::pair<uint64_t, uint32_t>> seen;
+    std::vector<LbvhSeg> segs;                  // RT_BUILD_LBVH: one tree per unique BLAS
+    uint64_t item_total = 0;
     uint32_t pair_base = 0;
     uint32_t slot_base[3] = {0, 0, 0};
     for (size_t i = 0; i < s->inst_desc.size(); i++) {
@@ -402,6 +533,19 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             seen.push_back({key, in.blas});
             BlasHost bh;
             bh.type = in.ptype;
+            if (mode == RT_BUILD_LBVH) {
+                if ((uint64_t)slot_base[in.ptype] + in.pcount >= MAX_LEAF_SLOTS || item_total + in.pcount >= (1ull << 31))
+                    return fail(RT_ERR_UNSUPPORTED, "too many primitives of one type (2^26 leaf slots)");
+                bh.pair_base = 0;
+                bh.slot_base = slot_base[in.ptype];
+                segs.push_back(LbvhSeg{(uint32_t)item_total, in.pcount, slot_base[in.ptype], in.pindex, in.ptype,
+                                       (uint32_t)(item_total - segs.size()), LBVH_BLAS_LEAF_CAP, 1u});
+                item_total += in.pcount;
+                slot_base[in.ptype] += in.pcount;
+                s->blas.push_back(std::move(bh));
+                s->inst.push_back(in);
+                continue;
+            }
             std::vector<BuildItem> items(in.pcount);
             for (uint32_t k = 0; k < in.pcount; k++)
                 items[k] = {prim_box(s, in.ptype, in.pindex + k), prim_centroid(s, in.ptype, in.pindex + k), in.pindex + k};
@@ -420,6 +564,14 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         s->inst.push_back(in);
     }
 
+    std::vector<float> mats;
+    for (const auto &r : s->roughs) { mats.push_back(r.albedo.x); mats.push_back(r.albedo.y); mats.push_back(r.albedo.z); mats.push_back(0.0f); }
+    for (const auto &m : s->metals) { mats.push_back(m.albedo.x); mats.push_back(m.albedo.y); mats.push_back(m.albedo.z); mats.push_back(m.fuzz); }
+    rt_status st;
+    if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    if (mode == RT_BUILD_LBVH) {
+        if ((st = gpu_setup_blas(s, segs, slot_base)) != RT_OK) return st;
+    } else {
     // leaf-ordered primitive arrays + node pairs
     std::vector<NodePair> pairs;
     pairs.reserve(pair_base);
@@ -464,12 +616,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         }
     }
     if (!mat_ok) return fail(RT_ERR_INVALID_ARGUMENT, "primitive references a material out of range");
-    std::vector<float> mats;
-    for (const auto &r : s->roughs) { mats.push_back(r.albedo.x); mats.push_back(r.albedo.y); mats.push_back(r.albedo.z); mats.push_back(0.0f); }
-    for (const auto &m : s->metals) { mats.push_back(m.albedo.x); mats.push_back(m.albedo.y); mats.push_back(m.albedo.z); mats.push_back(m.fuzz); }
     s->blas_pair_count = pairs.size();
 
-    rt_status st;
     if ((st = upload(s->blas_pairs, pairs)) != RT_OK) return st;
     if ((st = upload(s->tri_hot, th)) != RT_OK) return st;
     if ((st = upload(s->tri_cold, tc)) != RT_OK) return st;
@@ -477,15 +625,25 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     if ((st = upload(s->sph_cold, sc)) != RT_OK) return st;
     if ((st = upload(s->quad_hot, qh)) != RT_OK) return st;
     if ((st = upload(s->quad_cold, qc)) != RT_OK) return st;
+    }
     if ((st = upload(s->materials, mats)) != RT_OK) return st;
 
     // per-frame double buffers
     const size_t n = s->inst.size();
-    s->off_slots = align16(n * sizeof(NodePair));
+    s->off_root = 0;
+    s->off_pairs = 64;
+    s->off_slots = align16(s->off_pairs + n * sizeof(NodePair));
     s->off_hot = align16(s->off_slots + n * sizeof(uint32_t));
     s->off_cold = align16(s->off_hot + n * sizeof(InstHot));
-    s->frame_block = align16(s->off_cold + n * sizeof(InstCold));
-    if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    s->off_tbox = align16(s->off_cold + n * sizeof(InstCold));
+    s->off_tcent = align16(s->off_tbox + n * 6 * sizeof(float));
+    s->frame_block = align16(s->off_tcent + n * 4 * sizeof(float));
+    if (mode == RT_BUILD_LBVH) {
+        delete s->tlas_builder;
+        s->tlas_builder = new LbvhBuilder();
+        const std::vector<LbvhSeg> tseg{LbvhSeg{0u, (uint32_t)n, 0u, 0u, 0u, 0u, LBVH_TLAS_LEAF_CAP, 0u}};
+        HIP_TRY(s->tlas_builder->init(tseg, s->stream));
+    }
     for (int b = 0; b < 2; b++) {
         if (s->staging[b]) { (void)hipHostFree(s->staging[b]); s->staging[b] = nullptr; }
         if (s->frame_dev[b]) { (void)hipFree(s->frame_dev[b]); s->frame_dev[b] = nullptr; }
@@ -632,7 +790,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     const bool count = (o.flags & RT_RENDER_COUNT_WORK) != 0;
 
     // lean traversal: FAST kernel, LDS-only stack deep enough for TLAS + deepest BLAS (+ 2 resume entries)
-    const bool lean = !exact && s->lean && s->tlas_flat.height + s->max_blas_height + 2 <= LEAN_STACK;
+    const bool lean = !exact && s->lean && !s->gpu_tlas() && s->tlas_flat.height + s->max_blas_height + 2 <= LEAN_STACK;
     if (s->use_persistent) {
         out.queue_parts = s->queue_parts;
         out.grab = s->grab;
@@ -683,6 +841,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     HIP_TRY(hipEventRecord(s->k_stop, stream));
     HIP_TRY(hipEventRecord(s->ring_stop[slot], stream));
     HIP_TRY(hipEventRecord(s->ev_used[s->active], stream));
+    if (s->ev_render_done) HIP_TRY(hipEventRecord(s->ev_render_done, stream));
     if (o.flags & RT_RENDER_NO_SYNC) {
         if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; }
         return RT_OK;
@@ -734,6 +893,7 @@ rt_status rt_trace_rays(rt_scene *s, const float *rays, size_t n, uint32_t flags
         e = (flags & RT_RENDER_EXACT) ? launch_trace_rays_exact(g, d_rays, (uint32_t)n, d_hits, s->stream)
                                       : launch_trace_rays_fast(g, d_rays, (uint32_t)n, d_hits, s->stream);
     if (e == hipSuccess) e = hipEventRecord(s->ev_used[s->active], s->stream);
+    if (e == hipSuccess && s->ev_render_done) e = hipEventRecord(s->ev_render_done, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     if (e == hipSuccess) e = hipMemcpy(hits, d_hits, n * sizeof(rt_hit), hipMemcpyDeviceToHost);
     (void)hipFree(d_rays);
@@ -769,6 +929,11 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "supertile") {
         if (value < 0 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "supertile must be in 0..64");
         s->supertile = (uint32_t)value;
+    } else if (k == "rebuild") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "rebuild must be 0 or 1");
+        if (value == 1 && s->built && s->build_mode != RT_BUILD_LBVH)
+            return fail(RT_ERR_UNSUPPORTED, "per-frame BLAS rebuild needs RT_BUILD_LBVH");
+        s->rebuild_blas = value == 1;
     } else if (k == "timeline") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "timeline must be 0 or 1");
         s->timeline_on = value == 1;
@@ -839,6 +1004,41 @@ rt_status rt_scene_collect(rt_scene *s, rt_stats *acc, float *kernel_ms, uint32_
     return RT_OK;
 }
 
+rt_status rt_scene_update_triangles(rt_scene *s, size_t first, size_t count, const rt_triangle *tris) {
+    if (!s || (count && !tris)) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
+    if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
+    if (s->build_mode != RT_BUILD_LBVH) return fail(RT_ERR_UNSUPPORTED, "triangle updates need RT_BUILD_LBVH");
+    if (first > s->tris.size() || count > s->tris.size() - first) return fail(RT_ERR_INVALID_ARGUMENT, "triangle range out of bounds");
+    if (count == 0) return RT_OK;
+    bool ok = true;
+    for (size_t k = 0; k < count; k++) material_slot(s, tris[k].material_type, tris[k].material_index, ok);
+    if (!ok) return fail(RT_ERR_INVALID_ARGUMENT, "triangle references a material out of range");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipStreamSynchronize(s->stream));        // a pending BLAS build may still read the raw array
+    std::memcpy(s->tris.data() + first, tris, count * sizeof(rt_triangle));
+    HIP_TRY(hipMemcpy(s->raw_tris.p + first, tris, count * sizeof(rt_triangle), hipMemcpyHostToDevice));
+    // instance boxes derived from the triangles (RenderPin.cu:124-139); VTK-style bounds stay as given
+    for (size_t i = 0; i < s->inst.size(); i++) {
+        InstState &in = s->inst[i];
+        const rt_instance_desc &id = s->inst_desc[i];
+        if (in.ptype != RT_PRIM_TRIANGLE || id.has_local_bounds) continue;
+        if ((size_t)in.pindex + in.pcount <= first || in.pindex >= first + count) continue;
+        hm::Box bb = prim_box(s, in.ptype, in.pindex);
+        double c[3] = {0, 0, 0};
+        for (uint32_t k = 0; k < in.pcount; k++) {
+            if (k) bb = hm::Box::merge(bb, prim_box(s, in.ptype, in.pindex + k));
+            const hm::V3 pc = prim_centroid(s, in.ptype, in.pindex + k);
+            for (int a = 0; a < 3; a++) c[a] += pc[a];
+        }
+        in.box = bb;
+        in.centroid = in.pcount == 1 ? prim_centroid(s, in.ptype, in.pindex)
+                                     : hm::v3((float)(c[0] / in.pcount), (float)(c[1] / in.pcount), (float)(c[2] / in.pcount));
+        instance_update(in, in.x);
+    }
+    s->blas_dirty = true;
+    return RT_OK;
+}
+
 rt_status rt_synchronize(rt_scene *s) {
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
     HIP_TRY(hipSetDevice(s->device));
@@ -855,14 +1055,26 @@ rt_status rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
     info->blas_node_pairs = s->blas_pair_count;
     info->blas_leaves = s->blas_leaf_count;
     info->tlas_node_pairs = s->tlas_flat.pairs.size();
+    if (s->gpu_tlas() && s->built) {                 // GPU-built TLAS: read the last frame's count / root
+        HIP_TRY(hipSetDevice(s->device));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        uint32_t np = 0;
+        TreeRoot root{};
+        HIP_TRY(hipMemcpy(&np, s->gpu_counts.p + 1, sizeof np, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&root, s->frame_dev[s->active] + s->off_root, sizeof root, hipMemcpyDeviceToHost));
+        info->tlas_node_pairs = np;
+        info->tlas_height = root.height;
+    }
     info->device_bytes = s->blas_pairs.n * sizeof(NodePair) + s->tri_hot.n * sizeof(TriHot) + s->tri_cold.n * sizeof(TriCold) +
                          s->sph_hot.n * sizeof(SphereHot) + s->sph_cold.n * sizeof(PrimCold) +
                          s->quad_hot.n * sizeof(QuadHot) + s->quad_cold.n * sizeof(PrimCold) +
-                         s->materials.n * sizeof(float) + 2 * s->frame_block + s->out_rgba.n + s->out_rgb.n * sizeof(float);
+                         s->materials.n * sizeof(float) + 2 * s->frame_block + s->out_rgba.n + s->out_rgb.n * sizeof(float) +
+                         s->raw_tris.n * sizeof(rt_triangle) + s->raw_sph.n * sizeof(rt_sphere) +
+                         s->raw_quad.n * sizeof(rt_parallelogram);
     info->width = s->width; info->height = s->height;
     info->sqrt_sample_count = s->cam.sqrt_s;
     info->ray_trace_depth = s->cam.depth;
-    info->tlas_height = s->tlas_flat.height;
+    if (!s->gpu_tlas()) info->tlas_height = s->tlas_flat.height;
     info->blas_height_max = s->max_blas_height;
     return RT_OK;
 }
@@ -874,11 +1086,75 @@ static void export_tree(const Tree &t, float *boxes, uint32_t *ci) {
     }
 }
 
+}  // extern "C"
+
+// Reference node form (BLASNode/TLASNode arrays, children adjacent, DFS leaf order) of a tree held in
+// the node-pair layout: used to export GPU-built trees.
+static Tree tree_from_pairs(const TreeRoot &root, const std::vector<NodePair> &pairs, uint32_t slot_base,
+                            const std::vector<uint32_t> &item_of_slot) {
+    Tree t;
+    if (root.ref == 0xFFFFFFFFu) return t;
+    auto box_of = [](const float *b) { return hm::Box{{{b[0], b[1]}, {b[2], b[3]}, {b[4], b[5]}}}; };
+    struct Work { uint32_t ref; hm::Box box; uint32_t node; };
+    std::vector<Work> todo{{root.ref, box_of(root.box), 0u}};
+    t.nodes.push_back(TreeNode{});
+    while (!todo.empty()) {
+        const Work w = todo.back();
+        todo.pop_back();
+        t.nodes[w.node].box = w.box;
+        if (w.ref & REF_LEAF) {
+            const uint32_t start = ref_leaf_start(w.ref) - slot_base, cnt = ref_leaf_count(w.ref);
+            t.nodes[w.node].count = cnt;
+            t.nodes[w.node].index = (uint32_t)t.refs.size();
+            for (uint32_t k = 0; k < cnt; k++) t.refs.push_back(item_of_slot[start + k]);
+            continue;
+        }
+        const NodePair &P = pairs[w.ref & REF_INDEX_MASK];
+        const uint32_t left = (uint32_t)t.nodes.size();
+        t.nodes.resize(left + 2);
+        t.nodes[w.node].count = 0;
+        t.nodes[w.node].index = left;
+        todo.push_back({P.ref1, box_of(P.c1), left + 1});
+        todo.push_back({P.ref0, box_of(P.c0), left});
+    }
+    return t;
+}
+
+template <typename T>
+static hipError_t read_back(std::vector<T> &v, const T *src, size_t n) {
+    v.resize(n);
+    return n ? hipMemcpy(v.data(), src, n * sizeof(T), hipMemcpyDeviceToHost) : hipSuccess;
+}
+
+extern "C" {
+
 rt_status rt_scene_export_blas(const rt_scene *s, uint32_t b, float *boxes, uint32_t *ci, uint32_t *refs,
                                uint32_t *n_nodes, uint32_t *n_prims) {
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
     if (!s->built || b >= s->blas.size()) return fail(RT_ERR_INVALID_ARGUMENT, "no such BLAS");
-    const Tree &t = s->blas[b].tree;
+    Tree gpu_tree;
+    if (s->build_mode == RT_BUILD_LBVH) {
+        HIP_TRY(hipSetDevice(s->device));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        std::vector<NodePair> pairs;
+        std::vector<TreeRoot> roots;
+        HIP_TRY(read_back(pairs, s->blas_pairs.p, s->blas_pair_count));
+        HIP_TRY(read_back(roots, s->blas_roots.p, s->blas.size()));
+        const uint32_t type = s->blas[b].type;
+        std::vector<uint32_t> orig;
+        if (type == RT_PRIM_TRIANGLE) {
+            std::vector<TriCold> c;
+            HIP_TRY(read_back(c, s->tri_cold.p, s->tri_cold.n));
+            for (const TriCold &x : c) orig.push_back(x.orig_index);
+        } else {
+            std::vector<PrimCold> c;
+            HIP_TRY(read_back(c, type == RT_PRIM_SPHERE ? s->sph_cold.p : s->quad_cold.p,
+                              type == RT_PRIM_SPHERE ? s->sph_cold.n : s->quad_cold.n));
+            for (const PrimCold &x : c) orig.push_back(x.orig_index);
+        }
+        gpu_tree = tree_from_pairs(roots[b], pairs, 0, orig);
+    }
+    const Tree &t = s->build_mode == RT_BUILD_LBVH ? gpu_tree : s->blas[b].tree;
     if (n_nodes) *n_nodes = (uint32_t)t.nodes.size();
     if (n_prims) *n_prims = (uint32_t)t.refs.size();
     export_tree(t, boxes, ci);
@@ -890,10 +1166,24 @@ rt_status rt_scene_export_tlas(const rt_scene *s, float *boxes, uint32_t *ci, ui
                                uint32_t *n_refs) {
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
     if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
-    if (n_nodes) *n_nodes = (uint32_t)s->tlas.nodes.size();
-    if (n_refs) *n_refs = (uint32_t)s->tlas.refs.size();
-    export_tree(s->tlas, boxes, ci);
-    if (refs) std::memcpy(refs, s->tlas.refs.data(), s->tlas.refs.size() * sizeof(uint32_t));
+    Tree gpu_tree;
+    if (s->gpu_tlas()) {
+        HIP_TRY(hipSetDevice(s->device));
+        HIP_TRY(hipStreamSynchronize(s->stream));
+        const uint8_t *fd = s->frame_dev[s->active];
+        TreeRoot root{};
+        std::vector<NodePair> pairs;
+        std::vector<uint32_t> slots;
+        HIP_TRY(hipMemcpy(&root, fd + s->off_root, sizeof root, hipMemcpyDeviceToHost));
+        HIP_TRY(read_back(pairs, reinterpret_cast<const NodePair *>(fd + s->off_pairs), s->inst.size()));
+        HIP_TRY(read_back(slots, reinterpret_cast<const uint32_t *>(fd + s->off_slots), s->inst.size()));
+        gpu_tree = tree_from_pairs(root, pairs, 0, slots);
+    }
+    const Tree &t = s->gpu_tlas() ? gpu_tree : s->tlas;
+    if (n_nodes) *n_nodes = (uint32_t)t.nodes.size();
+    if (n_refs) *n_refs = (uint32_t)t.refs.size();
+    export_tree(t, boxes, ci);
+    if (refs) std::memcpy(refs, t.refs.data(), t.refs.size() * sizeof(uint32_t));
     return RT_OK;
 }
 

@@ -365,12 +365,13 @@ __device__ __forceinline__ void trav_init(Trav &T, const SceneGPU &sc, const f3 
     T.found = false;
     T.stk.sp = 0;
     T.stk.spilled = 0;
-    T.cur = sc.tlas_root_ref;
+    const TreeRoot &R = *sc.tlas_root;                                    // this frame's TLAS root (HBM)
+    T.cur = R.ref;
     T.cur_inst = 0;
     T.in_blas = false;
     T.pleaf = REF_NONE;
     float te = 0.0f;
-    T.tracing = slab(sc.tlas_root_box, T.wr, TMIN, T.tmax, te);          // root pop test (TLAS.cu:150)
+    T.tracing = slab(R.box, T.wr, TMIN, T.tmax, te);                     // root pop test (TLAS.cu:150)
     T.curT = te;
 }
 

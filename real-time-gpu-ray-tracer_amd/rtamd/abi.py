@@ -22,6 +22,7 @@ ROUGH, METAL = 0, 1
 
 RT_BUILD_COMPAT_MEDIAN = 0
 RT_BUILD_SAH = 1
+RT_BUILD_LBVH = 2
 
 RT_RENDER_EXACT = 1 << 0
 RT_RENDER_COUNT_WORK = 1 << 1
@@ -132,7 +133,7 @@ EXPORTED_SYMBOLS = (
     "rt_camera_set", "rt_scene_update", "rt_render", "rt_assemble_tiles", "rt_tiles_for_rank",
     "rt_trace_rays", "rt_synchronize", "rt_scene_destroy", "rt_scene_get_info",
     "rt_scene_export_blas", "rt_scene_export_tlas", "rt_demo_update", "rt_scene_set_option",
-    "rt_scene_collect", "rt_scene_debug_read",
+    "rt_scene_collect", "rt_scene_debug_read", "rt_scene_update_triangles",
 )
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -176,6 +177,8 @@ def _declare(lib):
     lib.rt_scene_set_option.restype = C.c_int
     lib.rt_scene_debug_read.argtypes = [C.c_void_p, C.c_char_p, C.c_void_p, C.c_size_t, P(C.c_size_t)]
     lib.rt_scene_debug_read.restype = C.c_int
+    lib.rt_scene_update_triangles.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p]
+    lib.rt_scene_update_triangles.restype = C.c_int
     lib.rt_demo_update.argtypes = [C.c_void_p, P(Xform), C.c_size_t, C.c_uint64]
     lib.rt_demo_update.restype = None
     return lib

@@ -42,8 +42,9 @@ class Renderer:
 
     # ---- lifecycle ---------------------------------------------------------------------
     def build_acceleration_structure(self, seed: int = 0, mode: str = "compat"):
-        """mode "compat": the reference's random-axis median split (pinned seed); "sah": SAH trees."""
-        m = {"compat": abi.RT_BUILD_COMPAT_MEDIAN, "sah": abi.RT_BUILD_SAH}[mode]
+        """mode "compat": the reference's random-axis median split (pinned seed); "sah": SAH trees;
+        "lbvh": BLASes and the per-frame TLAS built on the GPU (linear BVH)."""
+        m = {"compat": abi.RT_BUILD_COMPAT_MEDIAN, "sah": abi.RT_BUILD_SAH, "lbvh": abi.RT_BUILD_LBVH}[mode]
         abi.check(self.lib, self.lib.rt_scene_build(self.h, m, seed))
         return self
 
@@ -55,6 +56,12 @@ class Renderer:
 
     def set_option(self, key: str, value: int):
         abi.check(self.lib, self.lib.rt_scene_set_option(self.h, key.encode(), int(value)))
+        return self
+
+    def update_triangles(self, first: int, triangles):
+        """Replace triangles [first, first + len) (scenes.TRIANGLE_DTYPE array); "lbvh" scenes only."""
+        t = np.ascontiguousarray(triangles)
+        abi.check(self.lib, self.lib.rt_scene_update_triangles(self.h, first, t.shape[0], t.ctypes.data))
         return self
 
     def update(self, frame: int):

@@ -1,0 +1,202 @@
+"""RT_BUILD_LBVH: BLASes and the per-frame TLAS built on the GPU (lbvh.hip), through the C ABI.
+
+* every GPU-built BLAS equals the numpy restatement (tests/lbvh_ref.py) of the builder over the
+  oracle's primitive boxes, bit for bit (node boxes, topology, leaf order);
+* every GPU-built TLAS is a valid tree over all instances whose boxes are exact unions;
+* images traverse different trees than the reference's, so they are held to the FAST tolerance
+  against the oracle (compat trees), as RT_BUILD_SAH is;
+* rebuilding every frame is deterministic (same bytes), and rt_scene_update_triangles followed by
+  the GPU rebuild gives the same frame as a scene created with the moved triangles.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from lbvh_ref import check_tree, lbvh_tree
+from rtamd import Renderer, abi, scenes
+
+pytestmark = pytest.mark.gpu
+
+THREADS = 16
+
+
+def frac_within(a, b, lsb=1):
+    d = np.abs(a.astype(np.int32) - b.astype(np.int32)).max(axis=-1)
+    return float((d <= lsb).mean()), int(d.max())
+
+
+def prim_items(scene, ptype, first, count):
+    """Reference primitive boxes (oracle) and centroids of primitives [first, first + count)."""
+    from oracle.oracle import lib
+    boxes = np.zeros((count, 6), np.float32)
+    cents = np.zeros((count, 3), np.float32)
+    f = np.float32
+    for k in range(count):
+        i = first + k
+        if ptype == abi.TRIANGLE:
+            t = scene.triangles[i]
+            prim = abi.Triangle.from_buffer_copy(t.tobytes())
+            v = t["vertex"].astype(np.float32)
+            cents[k] = ((v[0] + v[1]) + v[2]) / f(3.0)
+        elif ptype == abi.SPHERE:
+            mt, mi, c, r = scene.spheres[i]
+            prim = abi.Sphere(abi.Vec3.of(c), float(r), mt, mi)
+            cents[k] = np.asarray(c, np.float32)
+        else:
+            mt, mi, q, u, v = scene.parallelograms[i]
+            prim = abi.Parallelogram(abi.Vec3.of(q), abi.Vec3.of(u), abi.Vec3.of(v), mt, mi)
+            q, u, v = (np.asarray(x, np.float32) for x in (q, u, v))
+            cents[k] = (q + u * f(0.5)) + v * f(0.5)
+        lib().oracle_prim_bounds(ptype, C.byref(prim), boxes[k].ctypes.data)
+    return boxes, cents
+
+
+def unique_blas(scene):
+    """(type, first, count) per unique BLAS in instance order (RenderPin.cu:99-201 dedup)."""
+    seen, out = set(), []
+    for d in scene.instances:
+        key = (d["type"], d["index"])
+        if key not in seen:
+            seen.add(key)
+            out.append((d["type"], d["index"], d.get("count", 0) or 1))
+    return out
+
+
+def test_blas_trees_equal_restatement(gpu_lib):
+    s = scenes.demo_with_particles(5)
+    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(64, 64)
+    blas = unique_blas(s)
+    assert r.info()["blas_count"] == len(blas)
+    for b, (ptype, first, count) in enumerate(blas):
+        boxes, cents = prim_items(s, ptype, first, count)
+        nb, ci, refs = r.export_blas(b)
+        wb, wci, wrefs = lbvh_tree(boxes, cents, 4)
+        assert np.array_equal(ci, wci), b
+        assert np.array_equal(refs, wrefs + first), b
+        assert np.array_equal(nb, wb), b
+        check_tree(nb, ci, refs - first, boxes, 4)
+
+
+def test_tlas_valid_every_frame(gpu_lib):
+    s = scenes.demo_with_particles(12)
+    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(64, 64)
+    n = len(s.instances)
+    for frame in (0, 5, 37):
+        r.update(frame)
+        nb, ci, refs = r.export_tlas()
+        assert sorted(refs.tolist()) == list(range(n))
+        # leaves <= 2 instances; interior boxes are exact unions of their children
+        todo = [0]
+        while todo:
+            j = todo.pop()
+            if ci[j, 0]:
+                assert ci[j, 0] <= 2
+                continue
+            k = int(ci[j, 1])
+            u = np.empty(6, np.float32)
+            u[0::2] = nb[k:k + 2, 0::2].min(axis=0)
+            u[1::2] = nb[k:k + 2, 1::2].max(axis=0)
+            assert np.array_equal(nb[j], u), (frame, j)
+            todo += [k, k + 1]
+        assert r.info()["tlas_node_pairs"] == int((ci[:, 0] == 0).sum())
+
+
+@pytest.mark.parametrize("depth,need", [(1, 0.999), (2, 0.999), (4, 0.995)])
+def test_lbvh_images_within_tolerance(gpu_lib, depth, need):
+    from oracle.oracle import OracleScene
+    s = scenes.demo_with_particles(16)
+    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(320, 180, ray_trace_depth=depth)
+    o = OracleScene(s, build_seed=0)
+    o.camera(320, 180, ray_trace_depth=depth)
+    for frame in (0, 37):
+        o.update(frame)
+        orgb, orgba, ocnt = o.render(threads=THREADS)
+        for exact in (True, False):
+            rgba, rgb, st = r.render(frame, exact=exact, want_rgb=True, count_work=True)
+            f, mx = frac_within(rgba, orgba)
+            assert f >= need, (frame, exact, f, mx)
+            assert abs(st["rays"] - ocnt["rays"]) <= 0.001 * ocnt["rays"]
+
+
+def test_trace_rays_hits_match_oracle(gpu_lib):
+    """Per-ray closest hits through GPU-built trees: same surface as the oracle's compat trees on
+    >= 99.9 % of rays (ties within 1e-6 may resolve to another primitive)."""
+    from oracle.oracle import OracleScene
+    s = scenes.demo_with_particles(20)
+    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(64, 64)
+    o = OracleScene(s, build_seed=0)
+    rng = np.random.default_rng(5)
+    n = 20000
+    org = np.stack([rng.uniform(-6, 6, n), rng.uniform(0.5, 8, n), rng.uniform(6, 12, n)], 1)
+    tgt = np.stack([rng.uniform(-2, 2, n), rng.uniform(3.5, 5.5, n), rng.uniform(-1, 1, n)], 1)
+    rays = np.concatenate([org, tgt - org], 1).astype(np.float32)
+    g = r.trace_rays(rays, exact=True)
+    h, _ = o.trace(rays)
+    same = (g["instance"] == h["instance"]) & (g["pindex"] == h["pindex"])
+    assert same.mean() >= 0.999, same.mean()
+    hit = same & (h["instance"] != 0xFFFFFFFF)
+    assert np.array_equal(g["t"][hit], h["t"][hit])
+
+
+def test_per_frame_rebuild_is_deterministic(gpu_lib):
+    s = scenes.demo_with_particles(10)
+    a = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(256, 144, ray_trace_depth=2)
+    b = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(256, 144, ray_trace_depth=2)
+    b.set_option("rebuild", 1)
+    for frame in range(4):
+        x = a.render(frame, want_rgb=True)
+        y = b.render(frame, want_rgb=True)
+        assert np.array_equal(x[1], y[1]) and x[2]["rays"] == y[2]["rays"], frame
+    # pipelined frames with a rebuild each frame
+    b.collect()
+    for frame in range(6):
+        b.render(frame, sync=False, want_rgba=False, keep_counters=frame > 0)
+    acc, kms = b.collect()
+    assert len(kms) == 6 and acc["rays"] > 0
+
+
+def test_update_triangles_rebuilds(gpu_lib):
+    s = scenes.demo_with_particles(8)
+    moved = s.triangles.copy()
+    n_p = 8 * 1024
+    moved["vertex"][:n_p] += np.asarray([0.05, 0.0, -0.03], np.float32)
+    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(256, 144, ray_trace_depth=2)
+    before = r.render(0, want_rgb=True)[1]
+    r.update_triangles(0, moved[:n_p])
+    after = r.render(0, want_rgb=True)[1]
+    assert not np.array_equal(before, after)
+    s2 = scenes.demo_with_particles(8)
+    s2.triangles = moved
+    fresh = Renderer(s2).build_acceleration_structure(0, mode="lbvh").configure_camera(256, 144, ray_trace_depth=2)
+    assert np.array_equal(after, fresh.render(0, want_rgb=True)[1])
+
+
+def test_update_triangles_needs_lbvh(gpu_lib):
+    s = scenes.demo_with_particles(2)
+    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(32, 32)
+    with pytest.raises(abi.RtError):
+        r.update_triangles(0, s.triangles[:4])
+    with pytest.raises(abi.RtError):
+        r.set_option("rebuild", 1)
+
+
+def test_large_forest_c5_shape(gpu_lib):
+    """1,000 particle BLASes (1.02 M triangles, the C5 shape at 1/10 scale): every primitive is in
+    exactly one leaf of its BLAS, and a frame matches the oracle within the FAST tolerance."""
+    from oracle.oracle import OracleScene
+    P = 1000
+    s = scenes.demo_with_particles(P)
+    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(192, 108, ray_trace_depth=2)
+    info = r.info()
+    assert info["blas_count"] == 5 - 1 + P
+    assert info["blas_leaves"] == info["blas_node_pairs"] + info["blas_count"]
+    for b in (4, 500, P + 3):                 # BLAS 4 + p = particle p (triangles p*1024 ...)
+        _, _, refs = r.export_blas(b)
+        assert sorted(refs.tolist()) == list(range((b - 4) * 1024, (b - 3) * 1024))
+    o = OracleScene(s, build_seed=0)
+    o.camera(192, 108, ray_trace_depth=2)
+    _, orgba, _ = o.render(threads=THREADS)
+    rgba, _, _ = r.render(0)
+    f, mx = frac_within(rgba, orgba)
+    assert f >= 0.999, (f, mx)
