@@ -40,8 +40,9 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="C2")
     p.add_argument("--exact", action="store_true", help="time the EXACT (parity) kernel instead of FAST")
-    p.add_argument("--build", default="sah", choices=("sah", "compat"),
-                   help="BVH builder: SAH (default) or the reference's random-axis median split")
+    p.add_argument("--build", default="sah", choices=("sah", "compat", "lbvh"),
+                   help="BVH builder: SAH (default), the reference's random-axis median split, or the GPU LBVH builder")
+    p.add_argument("--rebuild", action="store_true", help="--build lbvh: rebuild every BLAS on the GPU each frame (C5)")
     p.add_argument("--kernel", type=int, default=1, help="1 = persistent megakernel, 0 = grid kernel")
     p.add_argument("--threshold", type=int, default=8)
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -117,6 +118,8 @@ def main():
     r = Renderer(scene, device=local_rank).build_acceleration_structure(0, mode=args.build).configure_camera(
         cfg.width, cfg.height)
     r.set_option("kernel", args.kernel).set_option("threshold", args.threshold)
+    if args.rebuild:
+        r.set_option("rebuild", 1)
     info = r.info()
     stream = torch.cuda.current_stream().cuda_stream
 
@@ -205,7 +208,9 @@ def main():
                 "parallelism": f"screen-tiles{n} ({TILE}x{TILE} interleaved, RCCL gather)" if n > 1 else "single-gpu",
                 "kernel": ("EXACT" if args.exact else "FAST") + (" persistent" if args.kernel else " grid"),
                 "bvh": args.build,
-                "frames": "animated (Main.cu updateInstance), per-frame TLAS rebuild + upload, pipelined",
+                "frames": "animated (Main.cu updateInstance), per-frame TLAS rebuild" +
+                          (" on the GPU" if args.build == "lbvh" else " + upload") +
+                          (", per-frame GPU BLAS rebuild" if args.rebuild else "") + ", pipelined",
             },
             "rays_per_frame": round(rays / args.steps, 1),
             "kernel_ms": round(avg_kernel_ms, 4),

@@ -251,56 +251,118 @@ __global__ void karras_kernel(const LbvhSeg *segs, const unsigned long long *key
     if (i == 0) parent[g] = NONE;
 }
 
-__device__ __forceinline__ float ld_coherent(const float *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_coherent(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// ---- bottom-up box union -------------------------------------------------------------------------
+// Each leaf climbs; the second thread to reach a node finishes it (union of the two child boxes,
+// height) and climbs on.  Trees of <= LOCAL_MAX items (every particle BLAS, small TLASes) are
+// finished by one workgroup with node boxes and arrival counters in LDS, so the hand-off between
+// the two arriving threads is a workgroup-scope one.  Larger trees use the device-wide kernel, where
+// the two threads may sit on different XCDs (per-XCD L2s are not coherent): the finished node is
+// published with write-through (sc1) stores, drained (s_waitcnt vmcnt(0)) before the arrival
+// counter's agent-scope add, and the second arriver reads it with sc1 loads — no __threadfence()
+// (an L2 writeback + invalidate per step, MI355X_MICROARCH.md § visibility).
+constexpr uint32_t LOCAL_MAX = 2048;
+
+__device__ __forceinline__ void union_children(const uint32_t *child, uint32_t g, const uint32_t *vals, const float *item_box,
+                                               float *b, uint32_t &h, const float *node_box_lds, const uint32_t *height_lds,
+                                               uint32_t node_base, bool sc1) {
+    h = 0;
+#pragma unroll
+    for (int c = 0; c < 2; c++) {
+        const uint32_t ch = child[2 * g + c];
+        float cb[6];
+        uint32_t chh = 0;
+        if (ch & LEAF_BIT) {
+            const float2 *src = reinterpret_cast<const float2 *>(item_box + 6 * (size_t)vals[ch & ~LEAF_BIT]);
+#pragma unroll
+            for (int k = 0; k < 3; k++) { const float2 v = src[k]; cb[2 * k] = v.x; cb[2 * k + 1] = v.y; }
+        } else if (!sc1) {
+            const uint32_t l = ch - node_base;
+#pragma unroll
+            for (int k = 0; k < 6; k++) cb[k] = node_box_lds[6 * l + k];
+            chh = height_lds[l];
+        } else {
+            const unsigned long long *src = reinterpret_cast<const unsigned long long *>(node_box_lds + 6 * (size_t)ch);
+#pragma unroll
+            for (int k = 0; k < 3; k++) {
+                const unsigned long long v = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                cb[2 * k] = __uint_as_float((uint32_t)v);
+                cb[2 * k + 1] = __uint_as_float((uint32_t)(v >> 32));
+            }
+            chh = __hip_atomic_load(height_lds + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (c == 0) {
+#pragma unroll
+            for (int k = 0; k < 6; k++) b[k] = cb[k];
+        } else {
+            merge_into(b, cb);
+        }
+        h = chh > h ? chh : h;
+    }
 }
 
-// Bottom-up box union: each leaf climbs; the second thread to reach a node finishes it.
+__global__ __launch_bounds__(BLOCK) void bottom_up_local_kernel(const LbvhSeg *segs, const uint32_t *vals, const float *item_box,
+                                                                const uint32_t *child, const uint32_t *parent,
+                                                                const uint32_t *parent_leaf, const uint32_t *range,
+                                                                float *nbox, uint32_t *height, uint32_t *kept) {
+    __shared__ float sbox[(LOCAL_MAX - 1) * 6];
+    __shared__ uint32_t sheight[LOCAL_MAX - 1];
+    __shared__ uint32_t sflag[LOCAL_MAX - 1];
+    const LbvhSeg S = segs[blockIdx.x];
+    if (S.count < 2 || S.count > LOCAL_MAX) return;                    // block-uniform
+    const uint32_t m = S.count, ni = m - 1;
+    for (uint32_t k = threadIdx.x; k < ni; k += BLOCK) sflag[k] = 0;
+    __syncthreads();
+    for (uint32_t li = threadIdx.x; li < m; li += BLOCK) {
+        uint32_t g = parent_leaf[S.item_base + li];
+        while (g != NONE) {
+            const uint32_t l = g - S.node_base;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (atomicAdd(&sflag[l], 1u) == 0u) break;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            float b[6];
+            uint32_t h;
+            union_children(child, g, vals, item_box, b, h, sbox, sheight, S.node_base, false);
+            const uint32_t size = range[2 * g + 1] - range[2 * g] + 1u;
+#pragma unroll
+            for (int k = 0; k < 6; k++) sbox[6 * l + k] = b[k];
+            sheight[l] = size > S.leaf_cap ? h + 1u : 0u;
+            g = parent[g];
+        }
+    }
+    __syncthreads();
+    for (uint32_t l = threadIdx.x; l < ni; l += BLOCK) {
+        const uint32_t g = S.node_base + l;
+#pragma unroll
+        for (int k = 0; k < 6; k++) nbox[6 * (size_t)g + k] = sbox[6 * l + k];
+        height[g] = sheight[l];
+        kept[g] = (range[2 * g + 1] - range[2 * g] + 1u) > S.leaf_cap ? 1u : 0u;
+    }
+}
+
 __global__ void bottom_up_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals,
                                  const float *item_box, uint32_t n, const uint32_t *child, const uint32_t *parent,
                                  const uint32_t *parent_leaf, const uint32_t *range, uint32_t *flag, float *nbox,
                                  uint32_t *height, uint32_t *kept) {
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
     if (p >= n) return;
+    const LbvhSeg S = segs[seg_of_sorted(keys, p)];
+    if (S.count <= LOCAL_MAX) return;                                  // bottom_up_local_kernel
     uint32_t g = parent_leaf[p];
-    if (g == NONE) return;
-    const uint32_t cap = segs[seg_of_sorted(keys, p)].leaf_cap;
     while (g != NONE) {
-        __threadfence();
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // this lane's sc1 stores have landed
         if (atomicAdd(&flag[g], 1u) == 0u) return;
-        __threadfence();
         float b[6];
-        uint32_t h = 0;
+        uint32_t h;
+        union_children(child, g, vals, item_box, b, h, nbox, height, 0, true);
+        unsigned long long *dst = reinterpret_cast<unsigned long long *>(nbox + 6 * (size_t)g);
 #pragma unroll
-        for (int c = 0; c < 2; c++) {
-            const uint32_t ch = child[2 * g + c];
-            float cb[6];
-            uint32_t chh = 0;
-            if (ch & LEAF_BIT) {
-                const float *src = item_box + 6 * (size_t)vals[ch & ~LEAF_BIT];
-#pragma unroll
-                for (int k = 0; k < 6; k++) cb[k] = src[k];
-            } else {
-#pragma unroll
-                for (int k = 0; k < 6; k++) cb[k] = ld_coherent(nbox + 6 * (size_t)ch + k);
-                chh = ld_coherent(height + ch);
-            }
-            if (c == 0) {
-#pragma unroll
-                for (int k = 0; k < 6; k++) b[k] = cb[k];
-            } else {
-                merge_into(b, cb);
-            }
-            h = chh > h ? chh : h;
-        }
-#pragma unroll
-        for (int k = 0; k < 6; k++) nbox[6 * (size_t)g + k] = b[k];
+        for (int k = 0; k < 3; k++)
+            __hip_atomic_store(dst + k, (unsigned long long)__float_as_uint(b[2 * k]) |
+                                            ((unsigned long long)__float_as_uint(b[2 * k + 1]) << 32),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint32_t size = range[2 * g + 1] - range[2 * g] + 1u;
-        const bool keep = size > cap;
-        height[g] = keep ? h + 1u : 0u;
+        const bool keep = size > S.leaf_cap;
+        __hip_atomic_store(height + g, keep ? h + 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         kept[g] = keep ? 1u : 0u;
         g = parent[g];
     }
@@ -479,6 +541,8 @@ hipError_t LbvhBuilder::init(const std::vector<LbvhSeg> &segs, hipStream_t strea
     if (n >= (1ull << 31) || segs.empty()) return hipErrorInvalidValue;
     n_items_ = (uint32_t)n;
     n_segs_ = (uint32_t)segs.size();
+    max_count_ = 0;
+    for (const LbvhSeg &sg : segs) max_count_ = sg.count > max_count_ ? sg.count : max_count_;
     seg_bits_ = 0;
     while ((1ull << seg_bits_) < n_segs_) seg_bits_++;
     const size_t N = n_items_, NI = max_pairs();
@@ -534,8 +598,11 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
     LB_TRY(rocprim::radix_sort_pairs(tmp_, bytes, k0_, k1_, v0_, v1_, N, 0, 32 + seg_bits_, stream));
     hipLaunchKernelGGL(karras_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, k1_, N, child_, parent_,
                        parent_leaf_, range_, flag_);
-    hipLaunchKernelGGL(bottom_up_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, box_, N, child_,
-                       parent_, parent_leaf_, range_, flag_, nbox_, height_, kept_);
+    hipLaunchKernelGGL(bottom_up_local_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, v1_, box_, child_, parent_,
+                       parent_leaf_, range_, nbox_, height_, kept_);
+    if (max_count_ > LOCAL_MAX)
+        hipLaunchKernelGGL(bottom_up_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, box_, N, child_,
+                           parent_, parent_leaf_, range_, flag_, nbox_, height_, kept_);
     LB_TRY(hipGetLastError());
     if (NI > 0) {
         bytes = tmp_bytes_;

@@ -10,7 +10,7 @@
 // one stream, no host synchronisation:
 //   centroid bounds per segment -> 30-bit Morton key per item, segment id in the high word ->
 //   radix sort (rocPRIM) -> Karras radix-tree hierarchy per segment -> bottom-up box union
-//   (atomic arrival counters) -> subtrees of <= leaf_cap items collapse into leaves, the surviving
+//   (arrival counters; one workgroup per tree of <= 2048 items, LDS hand-offs) -> subtrees of <= leaf_cap items collapse into leaves, the surviving
 //   interior nodes are compacted (exclusive scan) into the node-pair layout of layout.hpp ->
 //   per-segment root {box, ref}.
 // Item boxes are exact unions (min/max) of the ε-expanded primitive boxes the reference builds
@@ -83,7 +83,7 @@ public:
     hipError_t gather_items(uint32_t *slots, hipStream_t stream);
 
 private:
-    uint32_t n_items_ = 0, n_segs_ = 0, seg_bits_ = 0;
+    uint32_t n_items_ = 0, n_segs_ = 0, seg_bits_ = 0, max_count_ = 0;
     LbvhSeg *segs_ = nullptr;
     uint32_t *seg_of_ = nullptr;          // item -> segment
     float *box_ = nullptr;                // 6 floats per item (owned or caller's)

@@ -200,3 +200,30 @@ def test_large_forest_c5_shape(gpu_lib):
     rgba, _, _ = r.render(0)
     f, mx = frac_within(rgba, orgba)
     assert f >= 0.999, (f, mx)
+
+
+def test_large_single_blas_device_wide_path(gpu_lib):
+    """A 65,536-triangle BLAS (> 2048 items) is finished by the device-wide bottom-up kernel
+    (write-through hand-offs across XCDs): still bit-identical to the restatement."""
+    from oracle.oracle import OracleScene
+    tris, inst = scenes.synth_particles(64, 1024, seed=3)
+    s = scenes.demo_scene()
+    s.animated = False
+    s.triangles = np.concatenate([tris, s.triangles])
+    for d in s.instances:
+        if d["type"] == abi.TRIANGLE:
+            d["index"] += tris.shape[0]
+    s.instances.append(dict(type=abi.TRIANGLE, index=0, count=tris.shape[0], shift=(0.0, 4.0, 0.0),
+                            rotate=(90.0, 0.0, 0.0), scale=(3.0, 3.0, 3.0)))
+    r = Renderer(s, update=False).build_acceleration_structure(0, mode="lbvh").configure_camera(200, 120, ray_trace_depth=2)
+    b = len(unique_blas(s)) - 1
+    boxes, cents = prim_items(s, abi.TRIANGLE, 0, tris.shape[0])
+    nb, ci, refs = r.export_blas(b)
+    wb, wci, wrefs = lbvh_tree(boxes, cents, 4)
+    assert np.array_equal(ci, wci) and np.array_equal(refs, wrefs) and np.array_equal(nb, wb)
+    o = OracleScene(s, build_seed=0)
+    o.camera(200, 120, ray_trace_depth=2)
+    _, orgba, _ = o.render(threads=THREADS)
+    rgba, _, _ = r.render(0, exact=True)
+    f, mx = frac_within(rgba, orgba)
+    assert f >= 0.999, (f, mx)
