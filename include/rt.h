@@ -305,6 +305,12 @@ rt_status rt_scene_collect(rt_scene *scene, rt_stats *accumulated, float *kernel
  * their description supplied (has_local_bounds), as the reference keeps the VTK reader's. */
 rt_status rt_scene_update_triangles(rt_scene *scene, size_t first, size_t count, const rt_triangle *triangles);
 
+/* Replace instance descriptions [first, first + count) — local bounds / centroid and the transform
+ * used when no update callback is set (the next VTK frame's particles, VTKReader.cu:203-215).  The
+ * primitives an instance refers to (type, index, count) may not change.  Takes effect with the next
+ * TLAS build (rt_scene_update / rt_render); any build mode. */
+rt_status rt_scene_update_instances(rt_scene *scene, size_t first, size_t count, const rt_instance_desc *instances);
+
 /* Blocks until all work the scene enqueued has finished. */
 rt_status rt_synchronize(rt_scene *scene);
 
@@ -346,6 +352,53 @@ rt_status rt_scene_export_tlas(const rt_scene *scene,
 /* Built-in copy of the demo animation (src/Global/Main.cu:6-42 updateInstance) so that
  * benchmarks do not cross into Python per frame.  Matches rt_update_fn; `user` unused. */
 void rt_demo_update(void *user, rt_xform *xforms, size_t instance_count, uint64_t frame);
+
+/* --- scene ingestion: legacy VTK particle files ------------------------------
+ * VTKReader::readVTKFile (src/Global/VTKReader.cu:16-164): DATASET POLYDATA, ASCII or BINARY,
+ * POINTS + TRIANGLE_STRIPS (one strip = one particle; other cell types are rejected), cell arrays
+ * "id" and "vel".  Vertex normals restate vtkPolyDataNormals (VTKReader.cu:60-70) from its
+ * documented behaviour — parity unpinned at that third-party boundary.
+ * Host-only: no GPU is needed. */
+typedef struct rt_vtk_file rt_vtk_file;
+
+typedef struct rt_vtk_info {
+    uint64_t point_count;
+    uint64_t particle_count;       /* strip cells */
+    uint64_t strip_vertex_count;   /* sum of strip lengths (VTKParticle::vertices, concatenated) */
+    uint64_t triangle_count;       /* sum of (strip length - 2) */
+} rt_vtk_info;
+
+/* VTKParticle (include/Global/VTKReader.cuh:12-30) without its vertex arrays. */
+typedef struct rt_vtk_particle {
+    uint64_t id;
+    rt_vec3 velocity;
+    float bounds[6];               /* [xmin,xmax,ymin,ymax,zmin,zmax] of the cell's points */
+    rt_vec3 centroid;              /* mean of the cell's points (double sum, cast to float) */
+    uint32_t first_vertex;         /* into the concatenated strip vertex stream */
+    uint32_t vertex_count;
+} rt_vtk_particle;
+
+rt_status rt_vtk_read(const char *path, rt_vtk_file **out);
+void rt_vtk_free(rt_vtk_file *file);
+rt_status rt_vtk_get_info(const rt_vtk_file *file, rt_vtk_info *info);
+/* particles[particle_count] */
+rt_status rt_vtk_particles(const rt_vtk_file *file, rt_vtk_particle *particles);
+/* strip vertex stream: positions / normals [strip_vertex_count] (either may be NULL) */
+rt_status rt_vtk_vertices(const rt_vtk_file *file, rt_vec3 *positions, rt_vec3 *normals);
+/* VTKReader::convertToRendererData (VTKReader.cu:166-220): triangles[triangle_count] (METAL 0,
+ * odd strip triangles swap vertices 2/3), instances[particle_count] (local bounds / centroid of the
+ * particle, transform shift (0,4,0) rotate (90,0,0) scale 3).  triangle_index_base = index of the
+ * first particle triangle in the scene's triangle array (0 when prepended, Renderer.cu:13-18). */
+rt_status rt_vtk_convert(const rt_vtk_file *file, uint32_t triangle_index_base, rt_triangle *triangles,
+                         rt_instance_desc *instances);
+
+/* Renderer::configureVTKFiles (src/Global/Renderer.cu:394-443): the .vtk.series JSON index;
+ * entry paths are resolved against the series file's directory. */
+typedef struct rt_vtk_series rt_vtk_series;
+rt_status rt_vtk_series_read(const char *path, rt_vtk_series **out);
+size_t rt_vtk_series_count(const rt_vtk_series *series);
+rt_status rt_vtk_series_entry(const rt_vtk_series *series, size_t index, const char **path, float *time);
+void rt_vtk_series_free(rt_vtk_series *series);
 
 #ifdef __cplusplus
 }

@@ -40,8 +40,12 @@ uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean);
 using namespace rtamd;
 
 namespace {
-
 thread_local std::string g_error;
+}  // namespace
+
+void rtamd_set_error(const std::string &msg) { g_error = msg; }   // shared with vtk_reader.cpp
+
+namespace {
 
 rt_status fail(rt_status s, const std::string &msg) {
     g_error = msg;
@@ -1036,6 +1040,30 @@ rt_status rt_scene_update_triangles(rt_scene *s, size_t first, size_t count, con
         instance_update(in, in.x);
     }
     s->blas_dirty = true;
+    return RT_OK;
+}
+
+rt_status rt_scene_update_instances(rt_scene *s, size_t first, size_t count, const rt_instance_desc *d) {
+    if (!s || (count && !d)) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
+    if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
+    if (first > s->inst.size() || count > s->inst.size() - first) return fail(RT_ERR_INVALID_ARGUMENT, "instance range out of bounds");
+    for (size_t k = 0; k < count; k++) {
+        const rt_instance_desc &o = s->inst_desc[first + k], &n = d[k];
+        if (o.primitive_type != n.primitive_type || o.primitive_index != n.primitive_index ||
+            o.primitive_count != n.primitive_count)
+            return fail(RT_ERR_INVALID_ARGUMENT, "an instance update may not change its primitives (type / index / count)");
+    }
+    for (size_t k = 0; k < count; k++) {
+        const size_t i = first + k;
+        s->inst_desc[i] = d[k];
+        InstState &in = s->inst[i];
+        if (d[k].has_local_bounds) {                                          // VTKReader.cu:204-209
+            in.box = hm::Box::from_ranges({d[k].local_bounds[0], d[k].local_bounds[1]}, {d[k].local_bounds[2], d[k].local_bounds[3]},
+                                          {d[k].local_bounds[4], d[k].local_bounds[5]});
+            in.centroid = hm::of(d[k].local_centroid);
+        }
+        instance_update(in, d[k].xform);
+    }
     return RT_OK;
 }
 

@@ -127,13 +127,25 @@ class SceneInfo(C.Structure):
                 ("tlas_height", C.c_uint32), ("blas_height_max", C.c_uint32)]
 
 
+class VtkInfo(C.Structure):
+    _fields_ = [("point_count", C.c_uint64), ("particle_count", C.c_uint64),
+                ("strip_vertex_count", C.c_uint64), ("triangle_count", C.c_uint64)]
+
+
+class VtkParticle(C.Structure):
+    _fields_ = [("id", C.c_uint64), ("velocity", Vec3), ("bounds", C.c_float * 6), ("centroid", Vec3),
+                ("first_vertex", C.c_uint32), ("vertex_count", C.c_uint32)]
+
+
 # Every symbol include/rt.h declares; tests check the library exports all of them.
 EXPORTED_SYMBOLS = (
     "rt_abi_version", "rt_last_error", "rt_device_count", "rt_scene_create", "rt_scene_build",
     "rt_camera_set", "rt_scene_update", "rt_render", "rt_assemble_tiles", "rt_tiles_for_rank",
     "rt_trace_rays", "rt_synchronize", "rt_scene_destroy", "rt_scene_get_info",
     "rt_scene_export_blas", "rt_scene_export_tlas", "rt_demo_update", "rt_scene_set_option",
-    "rt_scene_collect", "rt_scene_debug_read", "rt_scene_update_triangles",
+    "rt_scene_collect", "rt_scene_debug_read", "rt_scene_update_triangles", "rt_scene_update_instances",
+    "rt_vtk_read", "rt_vtk_free", "rt_vtk_get_info", "rt_vtk_particles", "rt_vtk_vertices", "rt_vtk_convert",
+    "rt_vtk_series_read", "rt_vtk_series_count", "rt_vtk_series_entry", "rt_vtk_series_free",
 )
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -179,6 +191,24 @@ def _declare(lib):
     lib.rt_scene_debug_read.restype = C.c_int
     lib.rt_scene_update_triangles.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, C.c_void_p]
     lib.rt_scene_update_triangles.restype = C.c_int
+    lib.rt_scene_update_instances.argtypes = [C.c_void_p, C.c_size_t, C.c_size_t, P(InstanceDesc)]
+    lib.rt_scene_update_instances.restype = C.c_int
+    lib.rt_vtk_read.argtypes = [C.c_char_p, P(C.c_void_p)]
+    lib.rt_vtk_free.argtypes = [C.c_void_p]
+    lib.rt_vtk_free.restype = None
+    lib.rt_vtk_get_info.argtypes = [C.c_void_p, P(VtkInfo)]
+    lib.rt_vtk_particles.argtypes = [C.c_void_p, P(VtkParticle)]
+    lib.rt_vtk_vertices.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    lib.rt_vtk_convert.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, P(InstanceDesc)]
+    lib.rt_vtk_series_read.argtypes = [C.c_char_p, P(C.c_void_p)]
+    lib.rt_vtk_series_count.argtypes = [C.c_void_p]
+    lib.rt_vtk_series_count.restype = C.c_size_t
+    lib.rt_vtk_series_entry.argtypes = [C.c_void_p, C.c_size_t, P(C.c_char_p), P(C.c_float)]
+    lib.rt_vtk_series_free.argtypes = [C.c_void_p]
+    lib.rt_vtk_series_free.restype = None
+    for name in ("rt_vtk_read", "rt_vtk_get_info", "rt_vtk_particles", "rt_vtk_vertices", "rt_vtk_convert",
+                 "rt_vtk_series_read", "rt_vtk_series_entry"):
+        getattr(lib, name).restype = C.c_int
     lib.rt_demo_update.argtypes = [C.c_void_p, P(Xform), C.c_size_t, C.c_uint64]
     lib.rt_demo_update.restype = None
     return lib

@@ -64,6 +64,13 @@ class Renderer:
         abi.check(self.lib, self.lib.rt_scene_update_triangles(self.h, first, t.shape[0], t.ctypes.data))
         return self
 
+    def update_instances(self, first: int, instances):
+        """Replace instance descriptions [first, first + len) (dicts as in scenes.Scene.instances)."""
+        from .scenes import instance_desc_array
+        arr = instance_desc_array(instances)
+        abi.check(self.lib, self.lib.rt_scene_update_instances(self.h, first, len(instances), arr))
+        return self
+
     def update(self, frame: int):
         abi.check(self.lib, self.lib.rt_scene_update(self.h, frame))
 

@@ -66,14 +66,7 @@ class Scene:
         met = (abi.Metal * max(1, len(self.metals)))()
         for i, (a, f) in enumerate(self.metals):
             met[i] = abi.Metal(abi.Vec3.of(a), float(f))
-        ins = (abi.InstanceDesc * len(self.instances))()
-        for i, d in enumerate(self.instances):
-            x = abi.Xform(abi.Vec3.of(d.get("shift", (0, 0, 0))), abi.Vec3.of(d.get("rotate", (0, 0, 0))),
-                          abi.Vec3.of(d.get("scale", (1, 1, 1))))
-            lb = d.get("bounds")
-            ins[i] = abi.InstanceDesc(d["type"], d["index"], d.get("count", 0), 1 if lb is not None else 0,
-                                      (C.c_float * 6)(*(lb if lb is not None else (0,) * 6)),
-                                      abi.Vec3.of(d.get("centroid", (0, 0, 0))), x)
+        ins = instance_desc_array(self.instances)
         self._keep = [sph, par, tri, rou, met, ins]
         return abi.SceneDesc(
             C.cast(sph, C.POINTER(abi.Sphere)), len(self.spheres),
@@ -90,6 +83,19 @@ class Scene:
         return abi.CameraInput(abi.Vec3.of(c["background"]), abi.Vec3.of(c["center"]), abi.Vec3.of(c["target"]),
                                float(c["fov"]), abi.Vec3.of(c["up"]), float(c["focus_disk_radius"]),
                                float(c["sample_range"]), int(c["sample_count"]), int(c["ray_trace_depth"]))
+
+
+def instance_desc_array(instances):
+    """ctypes rt_instance_desc[] of instance dicts {type, index[, count, bounds, centroid, shift, rotate, scale]}."""
+    ins = (abi.InstanceDesc * max(1, len(instances)))()
+    for i, d in enumerate(instances):
+        x = abi.Xform(abi.Vec3.of(d.get("shift", (0, 0, 0))), abi.Vec3.of(d.get("rotate", (0, 0, 0))),
+                      abi.Vec3.of(d.get("scale", (1, 1, 1))))
+        lb = d.get("bounds")
+        ins[i] = abi.InstanceDesc(d["type"], d["index"], d.get("count", 0), 1 if lb is not None else 0,
+                                  (C.c_float * 6)(*(lb if lb is not None else (0,) * 6)),
+                                  abi.Vec3.of(d.get("centroid", (0, 0, 0))), x)
+    return ins
 
 
 def _demo_triangle():

@@ -18,6 +18,7 @@ STRUCTS = {
     "rt_triangle": abi.Triangle, "rt_rough": abi.Rough, "rt_metal": abi.Metal, "rt_xform": abi.Xform,
     "rt_instance_desc": abi.InstanceDesc, "rt_scene_desc": abi.SceneDesc, "rt_camera_input": abi.CameraInput,
     "rt_render_opts": abi.RenderOpts, "rt_stats": abi.Stats, "rt_hit": abi.Hit, "rt_scene_info": abi.SceneInfo,
+    "rt_vtk_info": abi.VtkInfo, "rt_vtk_particle": abi.VtkParticle,
 }
 
 
