@@ -44,7 +44,7 @@ def parse():
                    help="BVH builder: SAH (default), the reference's random-axis median split, or the GPU LBVH builder")
     p.add_argument("--rebuild", action="store_true", help="--build lbvh: rebuild every BLAS on the GPU each frame (C5)")
     p.add_argument("--kernel", type=int, default=1, help="1 = persistent megakernel, 0 = grid kernel")
-    p.add_argument("--threshold", type=int, default=8)
+    p.add_argument("--threshold", type=int, default=None, help="refill threshold (default: the library's tuned value)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
@@ -117,7 +117,9 @@ def main():
     scene = scenes.config_scene(cfg)
     r = Renderer(scene, device=local_rank).build_acceleration_structure(0, mode=args.build).configure_camera(
         cfg.width, cfg.height)
-    r.set_option("kernel", args.kernel).set_option("threshold", args.threshold)
+    r.set_option("kernel", args.kernel)
+    if args.threshold is not None:
+        r.set_option("threshold", args.threshold)
     if args.rebuild:
         r.set_option("rebuild", 1)
     info = r.info()

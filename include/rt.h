@@ -271,7 +271,10 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 traversal loop to shade / regenerate (1..64)
  *   "variant"   : persistent kernel register budget: 0 = compiler's choice, 4 / 5 = at least
  *                 4 / 5 waves per SIMD
- *   "queue_parts": persistent kernel work-queue bands (1..8, default 4; a wave starts on band XCC_ID % parts)
+ *   "queue_parts": persistent kernel work-queue bands (1..8, default 8; a wave starts on band XCC_ID % parts)
+ *   "reorder"   : 1 (default) = each launch claims its band's 8x8 units heaviest-first, ordered by the
+ *                 traversal work the previous launch of the same layout recorded per unit (schedule.hip);
+ *                 0 = screen order.  Images are identical either way (the RNG is keyed by pixel).
  *   "lean"      : 1 = FAST persistent kernel uses the LDS-only-stack traversal (default 0) when the
  *                 TLAS height + deepest BLAS height + 2 <= 24
  *   "nt_store"  : 1 = non-temporal RGBA8 stores
@@ -279,7 +282,7 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "supertile" : walk each band in supertile x supertile units of 8x8 pixels (default 16; 0 = rows)
  *   "rebuild"   : RT_BUILD_LBVH only: 1 = rebuild every BLAS on the GPU every frame (default 0)
  *   "timeline"  : 1 = record a per-wave timeline of each persistent launch (debug)
- *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal rounds (debug)       */
+ *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal steps (debug)        */
 rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
 
 /* Debug buffers of the last launch that recorded them (synchronises the scene's stream):
@@ -288,7 +291,9 @@ rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
  *               traversal rounds, shade phases, queue grabs, and (diagnostic builds only) shader
  *               cycles spent refilling, descending, testing leaves and shading, descent-loop
  *               iterations, refill-loop iterations, 2 reserved;
- *   "costmap" : 1 u32 per output pixel: traversal rounds the pixel's lane spent on it.
+ *   "costmap" : 1 u32 per output pixel: traversal steps (interior steps + leaf phases) of its path;
+ *   "unit_cost", "unit_order": option "reorder" — per 8x8 unit, the work the last launch recorded, and
+ *               the claim order that launch used (unit claimed at each band position).
  * Copies min(capacity, size) bytes to dst and stores the buffer's full size in *bytes. */
 rt_status rt_scene_debug_read(rt_scene *scene, const char *name, void *dst, size_t capacity, size_t *bytes);
 

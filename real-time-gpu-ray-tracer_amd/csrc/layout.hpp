@@ -142,6 +142,11 @@ struct OutputGPU {
     uint32_t supertile;             // frame mode, grab 64: walk bands in supertile x supertile units (0 = rows)
     unsigned long long *timeline;   // TIMELINE_WORDS per wave (rt.h, rt_scene_debug_read)
     uint32_t *costmap;              // COUNT launches: traversal rounds per output pixel (debug)
+    // option "reorder" (schedule.hip): claim position j of a band takes unit order[j] (heaviest-first
+    // permutation inside the band; null = natural / supertile walk), and unit_cost[u] receives the
+    // largest cost (traversal rounds + 1) of unit u's pixels for the next launch's order
+    const uint32_t *order;
+    uint32_t *unit_cost;
 };
 constexpr uint32_t QUEUE_STRIDE = 32;         // u32 words between partition heads (128 B lines)
 constexpr uint32_t QUEUE_MAX_PARTS = 8;

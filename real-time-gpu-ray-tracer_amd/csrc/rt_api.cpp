@@ -29,9 +29,10 @@ hipError_t launch_trace_rays_exact(const SceneGPU &, const float *, uint32_t, rt
 hipError_t launch_trace_rays_fast(const SceneGPU &, const float *, uint32_t, rt_hit *, hipStream_t);
 hipError_t launch_assemble(const void *, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, void *, hipStream_t);
 hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
-                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
+                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
-                                         uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
+                                         uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
+hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean);
 hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, uint32_t, hipStream_t);
 uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean);
@@ -150,7 +151,7 @@ struct rt_scene {
     uint32_t threshold = 16;
     uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4, 5)
     bool use_persistent = true;
-    uint32_t queue_parts = 4;       // measured: 4 bands beat 1 (global queue) and 8 on C2
+    uint32_t queue_parts = 8;       // one band per XCD (measured with "reorder": 8 beat 4, 2 and 1 on C2)
     uint32_t nt_store = 0;
     uint32_t grab = 64;             // pixels per queue claim
     uint32_t supertile = 16;        // band walk order: st x st-unit supertiles (measured: 16 beats rows, 8 and 32)
@@ -158,6 +159,12 @@ struct rt_scene {
     uint32_t max_blas_height = 0;
     bool timeline_on = false;
     bool costmap_on = false;
+    // option "reorder" (schedule.hip): longest-first claim order from the previous launch's unit costs
+    bool reorder = true;
+    DevBuf<uint32_t> unit_cost, unit_order;
+    uint32_t sched_sig[7] = {};     // launch layout the recorded costs belong to
+    bool sched_valid = false;
+    hipStream_t copy_stream = nullptr;            // per-frame uploads (Renderer.cu:205-206 copyStream)
     DevBuf<uint32_t> costmap;
     size_t costmap_pixels = 0;
     DevBuf<unsigned long long> timeline;
@@ -191,9 +198,10 @@ struct rt_scene {
     ~rt_scene() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
+        if (copy_stream) (void)hipStreamSynchronize(copy_stream);
         blas_pairs.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
         quad_hot.release(); quad_cold.release(); materials.release(); out_rgba.release(); out_rgb.release();
-        timeline.release(); costmap.release();
+        timeline.release(); costmap.release(); unit_cost.release(); unit_order.release();
         delete blas_builder; delete tlas_builder;
         raw_tris.release(); raw_sph.release(); raw_quad.release(); blas_roots.release(); inst_blas.release();
         gpu_counts.release();
@@ -214,6 +222,7 @@ struct rt_scene {
         if (k_start) (void)hipEventDestroy(k_start);
         if (k_stop) (void)hipEventDestroy(k_stop);
         if (stream) (void)hipStreamDestroy(stream);
+        if (copy_stream) (void)hipStreamDestroy(copy_stream);
     }
 };
 
@@ -267,7 +276,10 @@ rt_status frame_update(rt_scene *s, uint64_t frame) {
         std::vector<rt_xform> xs(s->inst.size());
         for (size_t i = 0; i < xs.size(); i++) xs[i] = s->inst[i].x;
         s->update(s->update_user, xs.data(), xs.size(), frame);
-        for (size_t i = 0; i < xs.size(); i++) instance_update(s->inst[i], xs[i]);
+        // matrices are a pure function of (local box, xform): only instances whose xform changed are
+        // recomputed (the demo animates 5 of C2's 73 instances)
+        for (size_t i = 0; i < xs.size(); i++)
+            if (std::memcmp(&xs[i], &s->inst[i].x, sizeof(rt_xform)) != 0) instance_update(s->inst[i], xs[i]);
     }
     uint8_t *st = s->staging[b];
     InstHot *hot = reinterpret_cast<InstHot *>(st + s->off_hot);
@@ -328,9 +340,10 @@ rt_status frame_update(rt_scene *s, uint64_t frame) {
         store_rows(cold[i].fwd, in.fwd);
         store_rows(cold[i].nrm, in.nrm);
     }
-    HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_used[b], 0));        // frame_dev[b] free on device
-    HIP_TRY(hipMemcpyAsync(s->frame_dev[b], st, s->frame_block, hipMemcpyHostToDevice, s->stream));
-    HIP_TRY(hipEventRecord(s->ev_copied[b], s->stream));
+    // the upload runs on the copy stream, overlapping the previous frame's trace (Renderer.cu:281-303)
+    HIP_TRY(hipStreamWaitEvent(s->copy_stream, s->ev_used[b], 0));   // frame_dev[b] free on device
+    HIP_TRY(hipMemcpyAsync(s->frame_dev[b], st, s->frame_block, hipMemcpyHostToDevice, s->copy_stream));
+    HIP_TRY(hipEventRecord(s->ev_copied[b], s->copy_stream));
     s->active = b;
     s->frame = frame;
     return RT_OK;
@@ -573,6 +586,9 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     for (const auto &m : s->metals) { mats.push_back(m.albedo.x); mats.push_back(m.albedo.y); mats.push_back(m.albedo.z); mats.push_back(m.fuzz); }
     rt_status st;
     if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    if (!s->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&s->copy_stream, hipStreamNonBlocking));
+    if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
+    s->sched_valid = false;
     if (mode == RT_BUILD_LBVH) {
         if ((st = gpu_setup_blas(s, segs, slot_base)) != RT_OK) return st;
     } else {
@@ -823,6 +839,31 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             s->costmap_pixels = npix;
         }
     }
+    // launches of one scene never overlap, whatever streams callers pass (queue heads, unit costs)
+    HIP_TRY(hipStreamWaitEvent(stream, s->ev_render_done, 0));
+    bool reset_queue = true;
+    if (s->use_persistent && s->reorder && s->grab == 64u) {
+        if (s->unit_cost.n < out.units) {
+            s->unit_cost.release();
+            s->unit_order.release();
+            HIP_TRY(hipMalloc(&s->unit_cost.p, out.units * sizeof(uint32_t)));
+            s->unit_cost.n = out.units;
+            HIP_TRY(hipMalloc(&s->unit_order.p, out.units * sizeof(uint32_t)));
+            s->unit_order.n = out.units;
+            s->sched_valid = false;
+        }
+        const uint32_t sig[7] = {out.units, out.units_x, out.tile_w, out.tile_h, out.tile_rank, out.tile_count,
+                                 out.queue_parts};
+        const bool do_order = s->sched_valid && std::memcmp(sig, s->sched_sig, sizeof sig) == 0;
+        const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
+        const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
+        HIP_TRY(launch_schedule(s->unit_cost.p, s->unit_order.p, s->queue, rows, upr, out.queue_parts, do_order, stream));
+        std::memcpy(s->sched_sig, sig, sizeof sig);
+        s->sched_valid = true;
+        out.order = do_order ? s->unit_order.p : nullptr;
+        out.unit_cost = s->unit_cost.p;
+        reset_queue = false;
+    }
     HIP_TRY(hipStreamWaitEvent(stream, s->ev_copied[s->active], 0));
     if (!(o.flags & RT_RENDER_KEEP_COUNTERS))
         HIP_TRY(hipMemsetAsync(s->counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
@@ -835,17 +876,17 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     if (s->use_persistent)
         HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, s->counters, s->queue,
                                                        s->cus * persistent_blocks_per_cu_exact(s->variant, false), s->threshold,
-                                                       s->variant, false, stream)
+                                                       s->variant, false, reset_queue, stream)
                       : launch_render_persistent_fast(g, cam, out, count, s->counters, s->queue,
                                                       s->cus * persistent_blocks_per_cu_fast(s->variant, lean), s->threshold,
-                                                      s->variant, lean, stream));
+                                                      s->variant, lean, reset_queue, stream));
     else
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, s->counters, stream)
                       : launch_render_fast(g, cam, out, count, s->counters, stream));
     HIP_TRY(hipEventRecord(s->k_stop, stream));
     HIP_TRY(hipEventRecord(s->ring_stop[slot], stream));
     HIP_TRY(hipEventRecord(s->ev_used[s->active], stream));
-    if (s->ev_render_done) HIP_TRY(hipEventRecord(s->ev_render_done, stream));
+    HIP_TRY(hipEventRecord(s->ev_render_done, stream));
     if (o.flags & RT_RENDER_NO_SYNC) {
         if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; }
         return RT_OK;
@@ -944,6 +985,10 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "costmap") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
         s->costmap_on = value == 1;
+    } else if (k == "reorder") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "reorder must be 0 or 1");
+        if (s->reorder != (value == 1)) s->sched_valid = false;
+        s->reorder = value == 1;
     } else {
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown option " + k);
     }
@@ -962,6 +1007,9 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
     } else if (k == "costmap") {
         src = s->costmap.p;
         size = s->costmap_pixels * sizeof(uint32_t);
+    } else if (k == "unit_cost" || k == "unit_order") {
+        src = k == "unit_cost" ? s->unit_cost.p : s->unit_order.p;
+        size = s->sched_valid ? (size_t)s->sched_sig[0] * sizeof(uint32_t) : 0;
     } else {
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown debug buffer " + k);
     }
@@ -1070,7 +1118,9 @@ rt_status rt_scene_update_instances(rt_scene *s, size_t first, size_t count, con
 rt_status rt_synchronize(rt_scene *s) {
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
     HIP_TRY(hipSetDevice(s->device));
+    if (s->copy_stream) HIP_TRY(hipStreamSynchronize(s->copy_stream));
     if (s->stream) HIP_TRY(hipStreamSynchronize(s->stream));
+    if (s->ev_render_done) HIP_TRY(hipEventSynchronize(s->ev_render_done));
     return RT_OK;
 }
 

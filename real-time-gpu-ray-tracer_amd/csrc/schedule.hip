@@ -1,0 +1,96 @@
+// schedule.hip — claim order of the persistent render kernel's work queue (option "reorder").
+//
+// The persistent kernel (trace_kernel.hip) ends when its last wave does.  A wave claims one 8x8 unit
+// at a time and its lanes refill from that unit, so a unit holds a wave for as long as its 64 paths
+// take, and that is very uneven: a sky unit averages ~5 traversal steps per pixel, a unit over the
+// particle cluster ~100.  Claimed in screen order, the heavy units that sit late in a band start late
+// and the GPU waits for them: measured on C2, the queue ran dry at ~270 us and the last wave ended
+// at ~520 us.  Animated frames change little from one frame to the next, so each launch records the
+// traversal work of every unit (unit_cost, one atomicAdd per unit and shade step) and this kernel
+// orders the next launch's claims heaviest-first (longest-processing-time-first list scheduling).
+// The image does not depend on the order: every pixel's RNG stream is keyed by its global pixel
+// index.
+//
+// One 1024-thread workgroup per band: a stable counting sort of the band's units over 16 cost
+// classes (class order = longest first; equal classes keep screen order, so neighbouring units of
+// one class are still claimed together), then the costs are cleared for the next launch and the
+// queue heads are reset (this replaces the per-frame hipMemsetAsync of the heads).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "layout.hpp"
+
+namespace rtamd {
+namespace {
+
+constexpr int SCHED_THREADS = 1024;     // 16 waves
+constexpr int SCHED_CLASSES = 16;       // one class per wave in the scan
+
+// class 0 = heaviest: half-octaves of the unit's mean traversal steps per pixel, floor(2 log2(c/64 + 1))
+// (a sky unit averages ~5 steps per pixel, a unit over the particle cluster ~100; classes saturate at ~180)
+// in integers: 2 log2(x/64) = log2(x^2) - 12 with x = c + 64
+__device__ __forceinline__ uint32_t cost_class(uint32_t c) {
+    const uint64_t x = (uint64_t)c + 64u;
+    const int k = (63 - __builtin_clzll(x * x)) - 12;
+    return (uint32_t)(SCHED_CLASSES - 1) - (uint32_t)min(max(k, 0), SCHED_CLASSES - 1);
+}
+
+__global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__restrict__ cost, uint32_t *__restrict__ order,
+                                                                 uint32_t *__restrict__ queue, uint32_t rows,
+                                                                 uint32_t upr, uint32_t parts, uint32_t do_order) {
+    __shared__ uint32_t cnt[SCHED_CLASSES][SCHED_THREADS];   // per-thread class counts -> exclusive offsets
+    __shared__ uint32_t total[SCHED_CLASSES];
+    __shared__ uint32_t base[SCHED_CLASSES];
+    const uint32_t part = blockIdx.x, t = threadIdx.x;
+    if (part == 0 && t < QUEUE_MAX_PARTS) queue[t * QUEUE_STRIDE] = 0u;      // every head: `parts` may change
+    // the band's unit range, computed exactly as the render kernel computes it
+    const uint32_t b0 = rows * part / parts * upr, b1 = rows * (part + 1) / parts * upr;
+    const uint32_t n = b1 - b0, per = (n + SCHED_THREADS - 1) / SCHED_THREADS;
+    const uint32_t lo = b0 + min(n, t * per), hi = b0 + min(n, (t + 1) * per);
+    if (do_order) {
+        for (int c = 0; c < SCHED_CLASSES; c++) cnt[c][t] = 0u;
+        for (uint32_t u = lo; u < hi; u++) cnt[cost_class(cost[u])][t]++;
+        __syncthreads();
+        // exclusive scan of each class over the threads (thread order = screen order): wave w scans
+        // class w, each lane 16 consecutive threads' counts
+        const uint32_t w = t >> 6, lane = t & 63u;
+        uint32_t local[16], run = 0;
+#pragma unroll
+        for (int k = 0; k < 16; k++) { local[k] = run; run += cnt[w][lane * 16u + k]; }
+        uint32_t incl = run;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, 64);
+            if (lane >= (uint32_t)off) incl += y;
+        }
+        const uint32_t excl = incl - run;
+#pragma unroll
+        for (int k = 0; k < 16; k++) cnt[w][lane * 16u + k] = excl + local[k];
+        if (lane == 63u) total[w] = incl;
+        __syncthreads();
+        if (t == 0) {
+            uint32_t acc = 0;
+            for (int c = 0; c < SCHED_CLASSES; c++) { base[c] = acc; acc += total[c]; }
+        }
+        __syncthreads();
+        for (uint32_t u = lo; u < hi; u++) {
+            const uint32_t c = cost_class(cost[u]);
+            order[b0 + base[c] + cnt[c][t]++] = u;
+        }
+    }
+    for (uint32_t u = lo; u < hi; u++) cost[u] = 0u;
+}
+
+}  // namespace
+
+// rows x upr units per frame split into `parts` bands as in render_persistent_body; do_order = 0 only
+// clears the costs and the queue heads (first launch of a layout: no costs recorded yet).
+hipError_t launch_schedule(uint32_t *cost, uint32_t *order, uint32_t *queue, uint32_t rows, uint32_t upr,
+                           uint32_t parts, bool do_order, hipStream_t stream) {
+    if (parts == 0 || parts > QUEUE_MAX_PARTS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(schedule_kernel, dim3(parts), dim3(SCHED_THREADS), 0, stream, cost, order, queue, rows, upr, parts,
+                       do_order ? 1u : 0u);
+    return hipGetLastError();
+}
+
+}  // namespace rtamd

@@ -572,19 +572,26 @@ __device__ __forceinline__ unsigned long long stamp() {
 
 // One round: interior loop until every traversing lane holds a leaf, then the leaf phase.
 template <bool COUNT>
+// steps (when `track`): the lane's interior steps + leaf phases, the pixel's cost for the work order
 __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt,
-                                           PhaseCycles &pc) {
+                                           PhaseCycles &pc, uint32_t &steps, bool track) {
     DIAG_T(t0);
     for (;;) {
         if (T.tracing && T.pleaf == REF_NONE && T.cur == REF_NONE) T.tracing = false;   // done, no leaf left
         if (!__any(T.tracing && T.pleaf == REF_NONE)) break;
         const bool active = T.tracing && T.cur != REF_NONE && (!(T.cur & REF_LEAF) || T.pleaf == REF_NONE);
-        if (active) spec_interior_step<COUNT>(T, sc, spill, cnt);
+        if (active) {
+            spec_interior_step<COUNT>(T, sc, spill, cnt);
+            if (track) steps++;
+        }
         if (RT_DIAG) pc.iters++;
     }
     DIAG_ADD(pc.interior, t0);
     DIAG_T(t1);
-    if (T.tracing) spec_leaf_phase<COUNT>(T, sc, spill, cnt);
+    if (T.tracing) {
+        spec_leaf_phase<COUNT>(T, sc, spill, cnt);
+        if (track) steps++;
+    }
     DIAG_ADD(pc.leaf, t1);
 }
 
@@ -722,17 +729,24 @@ __device__ __forceinline__ bool lean_active(const Trav &T) {
 }
 
 template <bool COUNT>
-__device__ __forceinline__ void lean_round(Trav &T, const SceneGPU &sc, LaneCount &cnt, PhaseCycles &pc) {
+__device__ __forceinline__ void lean_round(Trav &T, const SceneGPU &sc, LaneCount &cnt, PhaseCycles &pc,
+                                           uint32_t &steps, bool track) {
     DIAG_T(t0);
     for (;;) {
         if (T.tracing && T.pleaf == REF_NONE && T.cur == REF_NONE) T.tracing = false;   // done, no leaf left
         if (!__any(T.tracing && T.pleaf == REF_NONE)) break;
-        if (lean_active(T)) lean_step<COUNT>(T, sc, cnt);
+        if (lean_active(T)) {
+            lean_step<COUNT>(T, sc, cnt);
+            if (track) steps++;
+        }
         if (RT_DIAG) pc.iters++;
     }
     DIAG_ADD(pc.interior, t0);
     DIAG_T(t1);
-    if (T.tracing) lean_leaf_phase<COUNT>(T, sc, cnt);
+    if (T.tracing) {
+        lean_leaf_phase<COUNT>(T, sc, cnt);
+        if (track) steps++;
+    }
     DIAG_ADD(pc.leaf, t1);
 }
 #endif
@@ -975,6 +989,24 @@ __device__ __forceinline__ void write_pixel(const OutputGPU &out, uint32_t oi, f
     else reinterpret_cast<uint32_t *>(out.rgba)[oi] = packed;
 }
 
+// Option "reorder": a unit's cost for the next launch's claim order (schedule.hip) is the traversal
+// work of its 64 pixels (interior steps + leaf phases + 1 per pixel).  A wave's lanes refill from
+// the unit it claimed, so a unit's total work is the time it holds a wave; units over the particle
+// cluster hold one for up to ~0.4 ms against ~20 us for a sky unit (C2, measured), and the launch
+// ends with whichever wave claimed the last heavy units.  Lanes that finished a pixel in this shade
+// step: one atomicAdd per distinct unit.
+__device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t unit, uint32_t c) {
+    uint64_t m = __ballot(fin);
+    while (m) {
+        const uint32_t first = (uint32_t)__builtin_ctzll(m);
+        const uint32_t u = __shfl(unit, (int)first, 64);
+        const bool mine = fin && unit == u;
+        const uint32_t x = wave_sum(mine ? c : 0u);
+        if ((threadIdx.x & 63u) == first) atomicAdd(cost + u, x);
+        m &= ~(uint64_t)__ballot(mine);
+    }
+}
+
 template <bool COUNT, bool LEAN>
 __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out,
                                                        uint32_t *queue, uint32_t threshold,
@@ -992,7 +1024,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     uint32_t rays = 0, pixels = 0;
 
     bool has = false;                  // lane owns a pixel
-    uint32_t px_rounds = 0;            // COUNT: traversal rounds spent on the lane's pixel
+    uint32_t px_steps = 0;             // traversal steps spent on the lane's pixel (COUNT cost map, reorder)
     uint32_t item = 0, sample = 0, depth = 0;
     Rng rng;
     rng.s = 0;
@@ -1006,6 +1038,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     const uint32_t xcc = xcc_id();
     uint32_t part = xcc % parts, tried = 0;
     const uint32_t grab = out.grab;                 // claim size (pixels)
+    const bool track = out.unit_cost != nullptr;    // record unit costs for the next launch's order
     unsigned long long t_start = 0, t_exhaust = 0;
     uint32_t n_rounds = 0, n_shades = 0, n_grabs = 0;      // wave-uniform (timeline)
     PhaseCycles pc = {0, 0, 0, 0, 0, 0};
@@ -1039,7 +1072,12 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                 }
                 pool_next = b;
                 pool_end = min(b + grab, p_end);
-                if (out.supertile && out.tile_count == 0 && grab == 64u) {
+                if (out.order) {
+                    // heaviest-first walk of the band (schedule.hip; grab == 64: one unit per claim)
+                    const uint32_t u = out.order[__builtin_amdgcn_readfirstlane(b) >> 6];
+                    pool_next = u * 64u;
+                    pool_end = pool_next + 64u;
+                } else if (out.supertile && out.tile_count == 0 && grab == 64u) {
                     // walk the band in st x st-unit supertiles (row-major supertiles, row-major units
                     // inside): the units in flight form a compact screen region, not a full-width strip
                     const uint32_t W = out.units_x, st = out.supertile;
@@ -1068,7 +1106,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     acc = mk(0.0f, 0.0f, 0.0f);
                     thr = mk(1.0f, 1.0f, 1.0f);
                     sample = 0; depth = 0;
-                    px_rounds = 0;
+                    px_steps = 0;
                     f3 o, d;
                     camera_ray(cam, px, py, 0, rng, o, d);
                     trav_init(T, sc, o, d);
@@ -1090,16 +1128,16 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             const uint64_t want = __ballot(!T.tracing && (has || !exhausted));
             if ((uint32_t)__popcll(want) >= threshold) break;
 #if !RT_EXACT
-            if constexpr (LEAN) lean_round<COUNT>(T, sc, cnt, pc);
+            if constexpr (LEAN) lean_round<COUNT>(T, sc, cnt, pc, px_steps, COUNT || track);
             else
 #endif
-                spec_round<COUNT>(T, sc, spill, cnt, pc);
+                spec_round<COUNT>(T, sc, spill, cnt, pc, px_steps, COUNT || track);
             n_rounds++;
-            if (COUNT) px_rounds += T.tracing ? 1u : 0u;
         }
         // ---- shade lanes whose segment finished (rayColor body, Kernel.cu:64-100)
         n_shades++;
         DIAG_T(t_shade);
+        bool fin = false;                    // lane wrote its pixel in this step
         if (has && !T.tracing) {
             rays++;
             bool path_done;
@@ -1140,12 +1178,14 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     camera_ray(cam, px, py, sample, rng, no, nd);
                 } else {
                     write_pixel(out, oi, scl(acc, cam.recip_sqrt * cam.recip_sqrt));   // Kernel.cu:143-146
-                    if (COUNT && out.costmap) out.costmap[oi] = px_rounds;
+                    if (COUNT && out.costmap) out.costmap[oi] = px_steps;
                     has = false;
+                    fin = true;
                 }
             }
             if (has) trav_init(T, sc, no, nd);
         }
+        if (track) unit_cost_add(out.unit_cost, fin, item >> 6, px_steps + 1u);
         DIAG_ADD(pc.shade, t_shade);
     }
 
@@ -1268,10 +1308,13 @@ constexpr bool HAS_LEAN = true;
 // lean: LDS-only-stack traversal (FAST kernel; the caller checks the tree heights).
 hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
                                                unsigned long long *counters, uint32_t *queue, uint32_t blocks,
-                                               uint32_t threshold, uint32_t variant, bool lean, hipStream_t stream) {
+                                               uint32_t threshold, uint32_t variant, bool lean, bool reset_queue,
+                                               hipStream_t stream) {
     if (out.units == 0) return hipSuccess;
-    hipError_t e = hipMemsetAsync(queue, 0, QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t), stream);
-    if (e != hipSuccess) return e;
+    if (reset_queue) {       // else the schedule kernel (schedule.hip) just reset the heads
+        const hipError_t e = hipMemsetAsync(queue, 0, QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t), stream);
+        if (e != hipSuccess) return e;
+    }
     if (lean && HAS_LEAN) {
         if (variant == 4) return launch_persistent_wpe<4, HAS_LEAN>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
         if (variant == 5) return launch_persistent_wpe<5, HAS_LEAN>(sc, cam, out, count, counters, queue, blocks, threshold, stream);

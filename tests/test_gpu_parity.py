@@ -261,3 +261,48 @@ def test_pipelined_frames_collect(gpu_lib):
         r.render(f, sync=False, keep_counters=f > 0, want_rgba=False)
     acc, kms = r.collect()
     assert acc["rays"] == sum(rays) and len(kms) == 5 and all(k > 0 for k in kms)
+
+
+def _sched_class(c):
+    """schedule.hip cost_class: 0 = heaviest (half-octaves of the mean traversal steps per pixel)."""
+    x = c.astype(np.uint64) + 64
+    k = np.array([int(v * v).bit_length() - 1 - 12 for v in x.tolist()], np.int64)
+    return 15 - np.clip(k, 0, 15)
+
+
+@pytest.mark.parametrize("exact", [False, True])
+def test_reorder_schedule_is_byte_identical(gpu_lib, exact):
+    """Option "reorder" (claims ordered heaviest-unit-first from the previous frame's unit costs,
+    csrc/schedule.hip) changes only which wave traces which pixel: every frame is byte-identical
+    to the screen-order walk (whole frame and a tile shard), and each launch's order is a stable,
+    class-sorted permutation of every XCD band's units."""
+    s = scenes.demo_with_particles(12)
+    W, H, parts = 480, 272, 4
+    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(W, H, ray_trace_depth=2)
+    r.set_option("queue_parts", parts)
+    ref = {}
+    r.set_option("reorder", 0)
+    for f in range(4):
+        ref[f] = r.render(f, exact=exact, want_rgb=True)
+    tref = r.render(3, exact=exact, tiles=(64, 64, 1, 3), skip_update=True)[0]
+    r.set_option("reorder", 1)
+    cost_prev = None
+    ux, rows = W // 8, H // 8
+    for f in range(4):
+        rgba, rgb, st = r.render(f, exact=exact, want_rgb=True)
+        assert np.array_equal(rgba, ref[f][0]) and np.array_equal(rgb, ref[f][1]), f
+        assert st["rays"] == ref[f][2]["rays"]
+        order = r.debug_read("unit_order").view(np.uint32)
+        cost = r.debug_read("unit_cost").view(np.uint32)
+        assert (cost > 0).all()                       # every unit's pixels reported
+        if cost_prev is not None:
+            cls = _sched_class(cost_prev)
+            for p in range(parts):
+                b0, b1 = rows * p // parts * ux, rows * (p + 1) // parts * ux
+                band = order[b0:b1].astype(np.int64)
+                assert np.array_equal(np.sort(band), np.arange(b0, b1)), p
+                key = cls[band] * (1 << 32) + band     # class-major, screen order inside a class
+                assert (np.diff(key) > 0).all(), p
+        cost_prev = cost.copy()
+    for _ in range(2):                                # tile shard: first launch of a layout, then ordered
+        assert np.array_equal(r.render(3, exact=exact, tiles=(64, 64, 1, 3), skip_update=True)[0], tref)
