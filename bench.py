@@ -126,15 +126,26 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
 
     tiles = None
+    pending = []                 # N > 1: (gather work, gathered buffer) of the previous frame
     if n > 1:
         tiles = (TILE, TILE, rank, n)
         slab_tiles = max(r.tiles_for_rank(TILE, TILE, k, n) for k in range(n))
         slab_px = slab_tiles * TILE * TILE
-        slab = torch.zeros(slab_px * 4, dtype=torch.uint8, device="cuda")
-        gathered = torch.zeros(n * slab_px * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
+        # double-buffered slabs: frame k's gather (RCCL stream) overlaps frame k+1's trace
+        slabs = [torch.zeros(slab_px * 4, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        gathered = [torch.zeros(n * slab_px * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
+                    for _ in range(2)]
         frame_buf = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
     else:
         frame_buf = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda")
+
+    def finish_gather():
+        """Wait (stream-ordered) for the previous frame's gather; rank 0 assembles it into the frame."""
+        if pending:
+            work, g = pending.pop()
+            work.wait()
+            if rank == 0:
+                r.assemble_tiles(g.data_ptr(), slab_tiles, TILE, TILE, n, frame_buf.data_ptr(), stream)
 
     def step(frame, sync=True, keep=False):
         """One frame; sync=False pipelines it (host TLAS build of the next frame overlaps the GPU)."""
@@ -142,11 +153,14 @@ def main():
             r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=frame_buf.data_ptr(), stream=stream,
                      sync=sync, keep_counters=keep)
             return
-        r.render(frame, exact=args.exact, want_rgba=False, tiles=tiles, rgba8_device=slab.data_ptr(), stream=stream,
+        b = frame % 2
+        r.render(frame, exact=args.exact, want_rgba=False, tiles=tiles, rgba8_device=slabs[b].data_ptr(), stream=stream,
                  sync=sync, keep_counters=keep)
-        dist.gather(slab, list(gathered.chunk(n)) if rank == 0 else None, dst=0)
-        if rank == 0:
-            r.assemble_tiles(gathered.data_ptr(), slab_tiles, TILE, TILE, n, frame_buf.data_ptr(), stream)
+        work = dist.gather(slabs[b], list(gathered[b].chunk(n)) if rank == 0 else None, dst=0, async_op=True)
+        finish_gather()            # frame - 1: its slab is free again before frame + 1 is traced into it
+        pending.append((work, gathered[b]))
+        if sync:
+            finish_gather()
 
     for f in range(args.warmup):
         step(f)
@@ -159,6 +173,7 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k, sync=False, keep=k > 0)
+    finish_gather()
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()
@@ -178,7 +193,7 @@ def main():
 
     # untimed work-counting pass (same frame as the first timed step) for the roofline
     _, _, cst = r.render(args.warmup, exact=args.exact, want_rgba=False, count_work=True,
-                         rgba8_device=(slab if n > 1 else frame_buf).data_ptr(), tiles=tiles, stream=stream)
+                         rgba8_device=(slabs[0] if n > 1 else frame_buf).data_ptr(), tiles=tiles, stream=stream)
     if n > 1:
         dist.barrier()
 
@@ -207,7 +222,7 @@ def main():
                 "width": cfg.width, "height": cfg.height, "spp": cfg.spp, "depth": cfg.depth,
                 "triangles": scene.triangle_count, "instances": len(scene.instances),
                 "blas_node_pairs": info["blas_node_pairs"],
-                "parallelism": f"screen-tiles{n} ({TILE}x{TILE} interleaved, RCCL gather)" if n > 1 else "single-gpu",
+                "parallelism": f"screen-tiles{n} ({TILE}x{TILE} interleaved, RCCL gather overlapping the next frame)" if n > 1 else "single-gpu",
                 "kernel": ("EXACT" if args.exact else "FAST") + (" persistent" if args.kernel else " grid"),
                 "bvh": args.build,
                 "frames": "animated (Main.cu updateInstance), per-frame TLAS rebuild" +

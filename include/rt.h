@@ -275,6 +275,9 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "reorder"   : 1 (default) = each launch claims its band's 8x8 units heaviest-first, ordered by the
  *                 traversal work the previous launch of the same layout recorded per unit (schedule.hip);
  *                 0 = screen order.  Images are identical either way (the RNG is keyed by pixel).
+ *   "split"     : with "reorder", heavy units are claimed in pieces shared by several waves: halves from
+ *                 cost level k_half, quarters from k_quarter (value k_half | k_quarter << 8, levels 0..15 =
+ *                 half-octaves of a unit's mean traversal steps per pixel; 0xFF = never; default 10 | 12 << 8)
  *   "lean"      : 1 = FAST persistent kernel uses the LDS-only-stack traversal (default 0) when the
  *                 TLAS height + deepest BLAS height + 2 <= 24
  *   "nt_store"  : 1 = non-temporal RGBA8 stores

@@ -32,7 +32,8 @@ hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, c
                                           uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
-hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
+hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t, uint32_t,
+                           hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean);
 hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, uint32_t, hipStream_t);
 uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean);
@@ -161,10 +162,10 @@ struct rt_scene {
     bool costmap_on = false;
     // option "reorder" (schedule.hip): longest-first claim order from the previous launch's unit costs
     bool reorder = true;
+    uint32_t split = 10u | 12u << 8;  // heavy-unit pieces: class level for halves | quarters << 8 (0xFF = never)
     DevBuf<uint32_t> unit_cost, unit_order;
     uint32_t sched_sig[7] = {};     // launch layout the recorded costs belong to
     bool sched_valid = false;
-    hipStream_t copy_stream = nullptr;            // per-frame uploads (Renderer.cu:205-206 copyStream)
     DevBuf<uint32_t> costmap;
     size_t costmap_pixels = 0;
     DevBuf<unsigned long long> timeline;
@@ -198,7 +199,6 @@ struct rt_scene {
     ~rt_scene() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
-        if (copy_stream) (void)hipStreamSynchronize(copy_stream);
         blas_pairs.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
         quad_hot.release(); quad_cold.release(); materials.release(); out_rgba.release(); out_rgb.release();
         timeline.release(); costmap.release(); unit_cost.release(); unit_order.release();
@@ -222,7 +222,6 @@ struct rt_scene {
         if (k_start) (void)hipEventDestroy(k_start);
         if (k_stop) (void)hipEventDestroy(k_stop);
         if (stream) (void)hipStreamDestroy(stream);
-        if (copy_stream) (void)hipStreamDestroy(copy_stream);
     }
 };
 
@@ -340,10 +339,12 @@ rt_status frame_update(rt_scene *s, uint64_t frame) {
         store_rows(cold[i].fwd, in.fwd);
         store_rows(cold[i].nrm, in.nrm);
     }
-    // the upload runs on the copy stream, overlapping the previous frame's trace (Renderer.cu:281-303)
-    HIP_TRY(hipStreamWaitEvent(s->copy_stream, s->ev_used[b], 0));   // frame_dev[b] free on device
-    HIP_TRY(hipMemcpyAsync(s->frame_dev[b], st, s->frame_block, hipMemcpyHostToDevice, s->copy_stream));
-    HIP_TRY(hipEventRecord(s->ev_copied[b], s->copy_stream));
+    // Measured: the same upload on a separate copy stream (the reference's copyStream, Renderer.cu:281-303)
+    // goes through an SDMA engine whose first use stalled a frame by ~7.6 ms; on the scene's stream it is
+    // a ~4 us blit kernel between two traces.
+    HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_used[b], 0));        // frame_dev[b] free on device
+    HIP_TRY(hipMemcpyAsync(s->frame_dev[b], st, s->frame_block, hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(hipEventRecord(s->ev_copied[b], s->stream));
     s->active = b;
     s->frame = frame;
     return RT_OK;
@@ -586,7 +587,6 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     for (const auto &m : s->metals) { mats.push_back(m.albedo.x); mats.push_back(m.albedo.y); mats.push_back(m.albedo.z); mats.push_back(m.fuzz); }
     rt_status st;
     if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
-    if (!s->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&s->copy_stream, hipStreamNonBlocking));
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
     s->sched_valid = false;
     if (mode == RT_BUILD_LBVH) {
@@ -679,7 +679,10 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         if (!s->ring_stop[i]) HIP_TRY(hipEventCreate(&s->ring_stop[i]));
     }
     if (!s->counters) HIP_TRY(hipMalloc(&s->counters, CNT_NUM * sizeof(unsigned long long)));
-    if (!s->queue) HIP_TRY(hipMalloc(&s->queue, QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t)));
+    if (!s->queue) {   // band heads, then (option "reorder") band item counts, one 128 B line each
+        HIP_TRY(hipMalloc(&s->queue, 2 * QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t)));
+        HIP_TRY(hipMemset(s->queue, 0, 2 * QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t)));
+    }
     {
         hipDeviceProp_t prop;
         HIP_TRY(hipGetDeviceProperties(&prop, s->device));
@@ -848,8 +851,8 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             s->unit_order.release();
             HIP_TRY(hipMalloc(&s->unit_cost.p, out.units * sizeof(uint32_t)));
             s->unit_cost.n = out.units;
-            HIP_TRY(hipMalloc(&s->unit_order.p, out.units * sizeof(uint32_t)));
-            s->unit_order.n = out.units;
+            HIP_TRY(hipMalloc(&s->unit_order.p, 4 * (size_t)out.units * sizeof(uint32_t)));   // <= 4 items per unit
+            s->unit_order.n = 4 * (size_t)out.units;
             s->sched_valid = false;
         }
         const uint32_t sig[7] = {out.units, out.units_x, out.tile_w, out.tile_h, out.tile_rank, out.tile_count,
@@ -857,7 +860,8 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         const bool do_order = s->sched_valid && std::memcmp(sig, s->sched_sig, sizeof sig) == 0;
         const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
         const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
-        HIP_TRY(launch_schedule(s->unit_cost.p, s->unit_order.p, s->queue, rows, upr, out.queue_parts, do_order, stream));
+        HIP_TRY(launch_schedule(s->unit_cost.p, s->unit_order.p, s->queue, rows, upr, out.queue_parts, do_order,
+                                s->split & 0xFFu, (s->split >> 8) & 0xFFu, stream));
         std::memcpy(s->sched_sig, sig, sizeof sig);
         s->sched_valid = true;
         out.order = do_order ? s->unit_order.p : nullptr;
@@ -985,6 +989,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "costmap") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
         s->costmap_on = value == 1;
+    } else if (k == "split") {
+        if (value < 0 || value > 0xFFFF) return fail(RT_ERR_INVALID_ARGUMENT, "split must be k_half | k_quarter << 8");
+        s->split = (uint32_t)value;
     } else if (k == "reorder") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "reorder must be 0 or 1");
         if (s->reorder != (value == 1)) s->sched_valid = false;
@@ -1009,7 +1016,7 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
         size = s->costmap_pixels * sizeof(uint32_t);
     } else if (k == "unit_cost" || k == "unit_order") {
         src = k == "unit_cost" ? s->unit_cost.p : s->unit_order.p;
-        size = s->sched_valid ? (size_t)s->sched_sig[0] * sizeof(uint32_t) : 0;
+        size = s->sched_valid ? (size_t)s->sched_sig[0] * (k == "unit_cost" ? 1 : 4) * sizeof(uint32_t) : 0;
     } else {
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown debug buffer " + k);
     }
@@ -1118,7 +1125,6 @@ rt_status rt_scene_update_instances(rt_scene *s, size_t first, size_t count, con
 rt_status rt_synchronize(rt_scene *s) {
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
     HIP_TRY(hipSetDevice(s->device));
-    if (s->copy_stream) HIP_TRY(hipStreamSynchronize(s->copy_stream));
     if (s->stream) HIP_TRY(hipStreamSynchronize(s->stream));
     if (s->ev_render_done) HIP_TRY(hipEventSynchronize(s->ev_render_done));
     return RT_OK;

@@ -12,8 +12,11 @@
 // index.
 //
 // One 1024-thread workgroup per band: a stable counting sort of the band's units over 16 cost
-// classes (class order = longest first; equal classes keep screen order, so neighbouring units of
-// one class are still claimed together), then the costs are cleared for the next launch and the
+// classes (class order = heaviest first; equal classes keep screen order, so neighbouring units of
+// one class are still claimed together).  A heavy unit becomes 2 or 4 claim items (32 / 16 pixels)
+// so that its paths spread over several waves instead of holding one wave for the critical path.
+// The band's items go to order[4 b0 ...) as (unit << 4 | piece << 2 | log2 pieces), the item count
+// to the band's count word (a line of its own, away from the atomically updated head); then the costs are cleared for the next launch and the
 // queue heads are reset (this replaces the per-frame hipMemsetAsync of the heads).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -35,9 +38,17 @@ __device__ __forceinline__ uint32_t cost_class(uint32_t c) {
     return (uint32_t)(SCHED_CLASSES - 1) - (uint32_t)min(max(k, 0), SCHED_CLASSES - 1);
 }
 
+// heavy units may be claimed in pieces so that several waves share them: 1/4 of a unit (16 pixels)
+// from class level k_quarter up, 1/2 from k_half up (levels k = 15 - class; > 15 = never)
+__device__ __forceinline__ uint32_t split_log2(uint32_t cls, uint32_t k_half, uint32_t k_quarter) {
+    const uint32_t k = (uint32_t)(SCHED_CLASSES - 1) - cls;
+    return k >= k_quarter ? 2u : (k >= k_half ? 1u : 0u);
+}
+
 __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__restrict__ cost, uint32_t *__restrict__ order,
                                                                  uint32_t *__restrict__ queue, uint32_t rows,
-                                                                 uint32_t upr, uint32_t parts, uint32_t do_order) {
+                                                                 uint32_t upr, uint32_t parts, uint32_t do_order,
+                                                                 uint32_t k_half, uint32_t k_quarter) {
     __shared__ uint32_t cnt[SCHED_CLASSES][SCHED_THREADS];   // per-thread class counts -> exclusive offsets
     __shared__ uint32_t total[SCHED_CLASSES];
     __shared__ uint32_t base[SCHED_CLASSES];
@@ -49,10 +60,13 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
     const uint32_t lo = b0 + min(n, t * per), hi = b0 + min(n, (t + 1) * per);
     if (do_order) {
         for (int c = 0; c < SCHED_CLASSES; c++) cnt[c][t] = 0u;
-        for (uint32_t u = lo; u < hi; u++) cnt[cost_class(cost[u])][t]++;
+        for (uint32_t u = lo; u < hi; u++) {
+            const uint32_t c = cost_class(cost[u]);
+            cnt[c][t] += 1u << split_log2(c, k_half, k_quarter);
+        }
         __syncthreads();
-        // exclusive scan of each class over the threads (thread order = screen order): wave w scans
-        // class w, each lane 16 consecutive threads' counts
+        // exclusive scan of each class's item counts over the threads (thread order = screen order):
+        // wave w scans class w, each lane 16 consecutive threads' counts
         const uint32_t w = t >> 6, lane = t & 63u;
         uint32_t local[16], run = 0;
 #pragma unroll
@@ -71,11 +85,16 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
         if (t == 0) {
             uint32_t acc = 0;
             for (int c = 0; c < SCHED_CLASSES; c++) { base[c] = acc; acc += total[c]; }
+            queue[(QUEUE_MAX_PARTS + part) * QUEUE_STRIDE] = acc;   // items in the band (own line)
         }
         __syncthreads();
+        // items of the band: [4 b0, 4 b0 + items) — at most 4 per unit
+        uint32_t *items = order + 4u * b0;
         for (uint32_t u = lo; u < hi; u++) {
-            const uint32_t c = cost_class(cost[u]);
-            order[b0 + base[c] + cnt[c][t]++] = u;
+            const uint32_t c = cost_class(cost[u]), ls = split_log2(c, k_half, k_quarter);
+            const uint32_t at = base[c] + cnt[c][t];
+            for (uint32_t k = 0; k < (1u << ls); k++) items[at + k] = (u << 4) | (k << 2) | ls;
+            cnt[c][t] = at - base[c] + (1u << ls);
         }
     }
     for (uint32_t u = lo; u < hi; u++) cost[u] = 0u;
@@ -86,10 +105,10 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
 // rows x upr units per frame split into `parts` bands as in render_persistent_body; do_order = 0 only
 // clears the costs and the queue heads (first launch of a layout: no costs recorded yet).
 hipError_t launch_schedule(uint32_t *cost, uint32_t *order, uint32_t *queue, uint32_t rows, uint32_t upr,
-                           uint32_t parts, bool do_order, hipStream_t stream) {
+                           uint32_t parts, bool do_order, uint32_t k_half, uint32_t k_quarter, hipStream_t stream) {
     if (parts == 0 || parts > QUEUE_MAX_PARTS) return hipErrorInvalidValue;
     hipLaunchKernelGGL(schedule_kernel, dim3(parts), dim3(SCHED_THREADS), 0, stream, cost, order, queue, rows, upr, parts,
-                       do_order ? 1u : 0u);
+                       do_order ? 1u : 0u, k_half, k_quarter);
     return hipGetLastError();
 }
 

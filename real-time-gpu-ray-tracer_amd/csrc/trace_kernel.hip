@@ -1030,6 +1030,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     rng.s = 0;
     f3 acc = mk(0.0f, 0.0f, 0.0f), thr = mk(1.0f, 1.0f, 1.0f);
     uint32_t pool_next = 0, pool_end = 0;     // wave-uniform
+    uint32_t limit = 0, limit_part = ~0u;     // wave-uniform: claim positions in band `limit_part`
     bool exhausted = false;                   // wave-uniform
     const uint32_t S2 = cam.sqrt_s * cam.sqrt_s;
     // Work queue: the frame's units are split into `parts` bands; a wave drains the band of its own
@@ -1057,11 +1058,19 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                 const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
                 const uint32_t p_begin = (rows * part / parts) * upr * 64u;
                 const uint32_t p_end = (rows * (part + 1) / parts) * upr * 64u;
+                // ordered walk (schedule.hip): one item per claim, a whole unit or a 1/2, 1/4 of a heavy
+                // one; the band's item count sits next to its head.  Screen walk: `grab` pixels per claim.
+                const uint32_t step = out.order ? 1u : grab;
+                if (part != limit_part) {          // the band's item count: read once per band, off the head's line
+                    limit_part = part;
+                    limit = out.order ? __builtin_amdgcn_readfirstlane(queue[(QUEUE_MAX_PARTS + part) * QUEUE_STRIDE])
+                                      : p_end - p_begin;
+                }
                 uint32_t b = 0;
-                if (lane == 0) b = atomicAdd(queue + part * QUEUE_STRIDE, grab);
-                b = p_begin + __shfl(b, 0, 64);
+                if (lane == 0) b = atomicAdd(queue + part * QUEUE_STRIDE, step);
+                b = __builtin_amdgcn_readfirstlane(__shfl(b, 0, 64));
                 n_grabs++;
-                if (b >= p_end) {
+                if (b >= limit) {
                     if (++tried >= parts) {
                         exhausted = true;
                         if (out.timeline) t_exhaust = __builtin_amdgcn_s_memrealtime();
@@ -1070,14 +1079,17 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     part = part + 1 == parts ? 0 : part + 1;
                     continue;
                 }
-                pool_next = b;
-                pool_end = min(b + grab, p_end);
                 if (out.order) {
-                    // heaviest-first walk of the band (schedule.hip; grab == 64: one unit per claim)
-                    const uint32_t u = out.order[__builtin_amdgcn_readfirstlane(b) >> 6];
-                    pool_next = u * 64u;
-                    pool_end = pool_next + 64u;
-                } else if (out.supertile && out.tile_count == 0 && grab == 64u) {
+                    const uint32_t it = out.order[4u * (p_begin >> 6) + b];
+                    const uint32_t len = 64u >> (it & 3u);
+                    pool_next = (it >> 4) * 64u + ((it >> 2) & 3u) * len;
+                    pool_end = pool_next + len;
+                } else {
+                    b += p_begin;
+                    pool_next = b;
+                    pool_end = min(b + grab, p_end);
+                }
+                if (!out.order && out.supertile && out.tile_count == 0 && grab == 64u) {
                     // walk the band in st x st-unit supertiles (row-major supertiles, row-major units
                     // inside): the units in flight form a compact screen region, not a full-width strip
                     const uint32_t W = out.units_x, st = out.supertile;

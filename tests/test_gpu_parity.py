@@ -285,7 +285,7 @@ def test_reorder_schedule_is_byte_identical(gpu_lib, exact):
     for f in range(4):
         ref[f] = r.render(f, exact=exact, want_rgb=True)
     tref = r.render(3, exact=exact, tiles=(64, 64, 1, 3), skip_update=True)[0]
-    r.set_option("reorder", 1)
+    r.set_option("reorder", 1).set_option("split", 8 | 10 << 8)
     cost_prev = None
     ux, rows = W // 8, H // 8
     for f in range(4):
@@ -297,11 +297,22 @@ def test_reorder_schedule_is_byte_identical(gpu_lib, exact):
         assert (cost > 0).all()                       # every unit's pixels reported
         if cost_prev is not None:
             cls = _sched_class(cost_prev)
+            split = np.where(15 - cls >= 10, 2, np.where(15 - cls >= 8, 1, 0))   # log2 pieces per unit (split 8 | 10 << 8)
             for p in range(parts):
                 b0, b1 = rows * p // parts * ux, rows * (p + 1) // parts * ux
-                band = order[b0:b1].astype(np.int64)
-                assert np.array_equal(np.sort(band), np.arange(b0, b1)), p
-                key = cls[band] * (1 << 32) + band     # class-major, screen order inside a class
+                n_items = int((1 << split[b0:b1]).sum())
+                it = order[4 * b0:4 * b0 + n_items].astype(np.int64)
+                unit, piece, ls = it >> 4, (it >> 2) & 3, it & 3
+                assert np.array_equal(ls, split[unit]), p             # pieces follow the unit's class
+                first = piece == 0
+                units = unit[first]
+                assert np.array_equal(np.sort(units), np.arange(b0, b1)), p
+                # a unit's pieces are consecutive: item i + k is piece k of the same unit
+                starts = np.flatnonzero(first)
+                for k in range(1, 4):
+                    sel = starts[(1 << ls[starts]) > k]
+                    assert np.array_equal(unit[sel + k], unit[sel]) and (piece[sel + k] == k).all(), p
+                key = cls[units] * (1 << 32) + units   # class-major, screen order inside a class
                 assert (np.diff(key) > 0).all(), p
         cost_prev = cost.copy()
     for _ in range(2):                                # tile shard: first launch of a layout, then ordered

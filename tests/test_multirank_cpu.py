@@ -62,6 +62,56 @@ def _worker(rank, world, port, result_path):
     dist.destroy_process_group()
 
 
+def _pipelined_worker(rank, world, port, result_path):
+    """bench.py's N > 1 loop: double-buffered slabs, frame k's gather issued async and completed
+    (then assembled on rank 0) only after frame k + 1 has been rendered into the other slab."""
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "real-time-gpu-ray-tracer_amd")]
+    from oracle.oracle import OracleScene
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    o = OracleScene(scenes.demo_with_particles(4), build_seed=2)
+    o.camera(W, H, ray_trace_depth=1)
+    st = tiles.slab_tiles(W, H, TW, TH, world)
+    slabs = [torch.zeros(st * TW * TH, 4, dtype=torch.uint8) for _ in range(2)]
+    gathered = [[torch.zeros_like(slabs[0]) for _ in range(world)] if rank == 0 else None for _ in range(2)]
+    frames, pending = [], []
+
+    def finish():
+        if pending:
+            work, g, f = pending.pop()
+            work.wait()
+            if rank == 0:
+                frames.append((f, tiles.assemble(torch.stack(g).numpy(), W, H, TW, TH, world)))
+
+    for f in range(3):
+        b = f % 2
+        o.update(f)
+        slabs[b].copy_(torch.from_numpy(_render_slab(o, rank, world)))
+        work = dist.gather(slabs[b], gathered[b], dst=0, async_op=True)
+        finish()
+        pending.append((work, gathered[b], f))
+    finish()
+    if rank == 0:
+        out = []
+        for f, frame in frames:
+            o.update(f)
+            out.append(np.stack([frame, o.render(threads=2, want_rgb=False)[1]]))
+        np.save(result_path, np.stack(out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_pipelined_gather_gloo(tmp_path):
+    out = str(tmp_path / "res.npy")
+    mp.spawn(_pipelined_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    res = np.load(out)
+    assert res.shape[0] == 3
+    for frame, full in res:
+        assert np.array_equal(frame, full)
+
+
 @pytest.mark.parametrize("world", [2])
 def test_tile_gather_assemble_gloo(tmp_path, world):
     out = str(tmp_path / "res.npy")
