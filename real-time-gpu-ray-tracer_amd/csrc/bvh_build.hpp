@@ -12,6 +12,7 @@
 // them unspecified).
 #pragma once
 #include <algorithm>
+#include <limits>
 #include <cstdint>
 #include <vector>
 
@@ -265,6 +266,71 @@ inline FlatTree flatten_tree(const Tree &t, uint32_t pair_base, uint32_t slot_ba
             todo.push_back({nd.index + 1, d + 1});
         }
     }
+    return f;
+}
+
+// Quad form of one tree (FAST kernel, option "wide").  Each quad starts from a binary interior node's
+// two children and repeatedly replaces its largest-area interior child by that child's two children
+// until it holds 4 (or only leaves are left) — the usual BVH2 -> BVH4 collapse; leaves keep their refs
+// (same leaf-ordered slots), so the quad tree holds exactly the binary tree's leaves.
+struct FlatWide {
+    std::vector<NodeQuad> quads;
+    uint32_t root_ref = 0;
+    uint32_t height = 0;           // quad levels on the longest root-to-leaf path
+};
+
+inline FlatWide flatten_tree_wide(const Tree &t, uint32_t quad_base, uint32_t slot_base, uint32_t ptype, bool blas) {
+    FlatWide f;
+    const uint32_t n = (uint32_t)t.nodes.size();
+    if (n == 0) return f;
+    auto leaf_ref = [&](uint32_t j) { return make_leaf_ref(slot_base + t.nodes[j].index, t.nodes[j].count, ptype, blas); };
+    if (t.nodes[0].count > 0) { f.root_ref = leaf_ref(0); return f; }
+    struct Todo { uint32_t node, quad, depth; };
+    std::vector<Todo> todo{{0u, 0u, 1u}};
+    f.quads.emplace_back();
+    while (!todo.empty()) {
+        const Todo w = todo.back();
+        todo.pop_back();
+        f.height = std::max(f.height, w.depth);
+        uint32_t ch[4] = {t.nodes[w.node].index, t.nodes[w.node].index + 1, 0, 0};
+        uint32_t nc = 2;
+        while (nc < 4) {
+            int best = -1;
+            float area = -1.0f;
+            for (uint32_t k = 0; k < nc; k++)
+                if (t.nodes[ch[k]].count == 0 && half_area(t.nodes[ch[k]].box) > area) {
+                    area = half_area(t.nodes[ch[k]].box);
+                    best = (int)k;
+                }
+            if (best < 0) break;
+            const uint32_t left = t.nodes[ch[best]].index;
+            ch[best] = left;
+            ch[nc++] = left + 1;
+        }
+        NodeQuad q;
+        for (uint32_t k = 0; k < 4; k++) {
+            float b[6];
+            if (k < nc) {
+                t.nodes[ch[k]].box.store(b);
+            } else {
+                for (float &x : b) x = std::numeric_limits<float>::infinity();   // rejected by every slab test
+            }
+            q.lo_x[k] = b[0]; q.hi_x[k] = b[1]; q.lo_y[k] = b[2]; q.hi_y[k] = b[3]; q.lo_z[k] = b[4]; q.hi_z[k] = b[5];
+            if (k >= nc) {
+                q.ref[k] = REF_EMPTY;
+            } else if (t.nodes[ch[k]].count > 0) {
+                q.ref[k] = leaf_ref(ch[k]);
+            } else {
+                const uint32_t qi = (uint32_t)f.quads.size();
+                f.quads.emplace_back();
+                q.ref[k] = make_interior_ref(quad_base + qi, blas);
+                todo.push_back({ch[k], qi, w.depth + 1});
+            }
+            q.pad[k] = 0;
+        }
+        f.quads[w.quad] = q;
+    }
+    f.root_ref = make_interior_ref(quad_base, blas);
     return f;
 }
 

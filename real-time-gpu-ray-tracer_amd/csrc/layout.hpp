@@ -26,6 +26,7 @@ constexpr uint32_t REF_LEAF = 1u << 31;
 constexpr uint32_t REF_BLAS = 1u << 30;
 constexpr uint32_t REF_INDEX_MASK = (1u << 30) - 1u;
 constexpr uint32_t REF_START_MASK = (1u << 26) - 1u;
+constexpr uint32_t REF_EMPTY = 0xFFFFFFFFu;       // empty NodeQuad slot (= the kernel's REF_NONE)
 constexpr uint32_t MAX_LEAF_SLOTS = 1u << 26;
 
 __host__ __device__ inline uint32_t make_interior_ref(uint32_t pair, bool blas) {
@@ -47,6 +48,17 @@ struct alignas(16) NodePair {       // 64 B
     uint32_t pad0, pad1;
 };
 static_assert(sizeof(NodePair) == 64, "NodePair must be 64 B");
+
+// FAST kernel, option "wide": the same trees collapsed to 4 children per interior node (each quad
+// absorbs the largest-area interior children of a binary node until it holds 4), so a ray descends
+// half as many dependent levels.  Child boxes are SoA (one dwordx4 per bound) so the 4 slab tests
+// share each load; an empty slot has every bound = +inf, which no slab test accepts.
+struct alignas(16) NodeQuad {       // 128 B
+    float lo_x[4], hi_x[4], lo_y[4], hi_y[4], lo_z[4], hi_z[4];
+    uint32_t ref[4];                // child refs (interior refs index the quad array), REF_NONE = empty
+    uint32_t pad[4];
+};
+static_assert(sizeof(NodeQuad) == 128, "NodeQuad must be 128 B");
 
 struct alignas(16) TriHot {         // 48 B: Moller-Trumbore operands (Triangle.cu:4-44)
     float v0[3]; float pad0;
@@ -76,7 +88,7 @@ struct alignas(16) InstHot {        // 80 B: what Instance::hit needs before BLA
     float inv[12];                  // rows 1..3 of transformInverse (4 cols)  (Instance.cu:26-27)
     float root_box[6];              // BLAS root node box (local space)
     uint32_t root_ref;              // BLAS root ref (leaf or interior, level = BLAS)
-    uint32_t pad;
+    uint32_t root_ref_wide;         // the same root in the quad (option "wide") tree
 };
 static_assert(sizeof(InstHot) == 80, "InstHot must be 80 B");
 struct alignas(16) InstCold {       // 96 B: hit finalisation (Instance.cu:41-45)
@@ -108,6 +120,10 @@ struct SceneGPU {
     const PrimCold *quad_cold;
     const float *materials;         // 4 floats per slot: albedo.xyz, fuzz (roughs then metals)
     const TreeRoot *tlas_root;      // this frame's TLAS root, in the per-frame block (host- or GPU-built)
+    const NodeQuad *blas_quads;     // option "wide" (host-built trees): quad forms of the BLASes / TLAS
+    const NodeQuad *tlas_quads;
+    const TreeRoot *tlas_root_wide;
+    uint32_t wide;                  // 1: the FAST persistent kernel traverses the quad trees
     uint32_t instance_count;
     uint32_t rough_count;           // material slot of metal m = rough_count + m
 };

@@ -642,7 +642,7 @@ __global__ void patch_roots_kernel(InstHot *hot, const uint32_t *inst_blas, cons
 #pragma unroll
     for (int k = 0; k < 6; k++) hot[i].root_box[k] = R.box[k];
     hot[i].root_ref = R.ref;
-    hot[i].pad = 0;
+    hot[i].root_ref_wide = R.ref;       // GPU-built trees have no quad form ("wide" needs host trees)
 }
 }  // namespace lbvh
 

@@ -34,9 +34,9 @@ hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, co
                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
 hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t, uint32_t,
                            hipStream_t);
-uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean);
+uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean, bool wide);
 hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, uint32_t, hipStream_t);
-uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean);
+uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean, bool wide);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -82,6 +82,7 @@ struct BlasHost {
     uint32_t type;
     Tree tree;
     FlatTree flat;
+    FlatWide wide;                 // quad form (option "wide"; host-built modes)
     uint32_t pair_base, slot_base;
 };
 
@@ -112,6 +113,7 @@ struct rt_scene {
     std::vector<BlasHost> blas;
     Tree tlas;
     FlatTree tlas_flat;
+    FlatWide tlas_wide;
     uint64_t build_seed = 0;
     rt_build_mode build_mode = RT_BUILD_COMPAT_MEDIAN;
     bool built = false;
@@ -119,6 +121,8 @@ struct rt_scene {
 
     // HBM: static scene data
     DevBuf<NodePair> blas_pairs;
+    DevBuf<NodeQuad> blas_quads;    // option "wide"
+    bool wide = true;               // FAST persistent kernel traverses the quad trees (host-built modes)
     DevBuf<TriHot> tri_hot;
     DevBuf<TriCold> tri_cold;
     DevBuf<SphereHot> sph_hot;
@@ -132,7 +136,7 @@ struct rt_scene {
     //   [tlas root | tlas pairs | tlas slots | inst hot | inst cold | tlas item boxes | tlas item centroids]
     // (the root and the item arrays are used by GPU-built TLASes only)
     size_t frame_block = 0, off_root = 0, off_pairs = 0, off_slots = 0, off_hot = 0, off_cold = 0, off_tbox = 0,
-           off_tcent = 0;
+           off_tcent = 0, off_root_wide = 0, off_quads = 0;
     uint8_t *staging[2] = {nullptr, nullptr};     // pinned host
     uint8_t *frame_dev[2] = {nullptr, nullptr};   // HBM
     hipEvent_t ev_copied[2] = {nullptr, nullptr}; // upload from staging[b] finished
@@ -199,7 +203,7 @@ struct rt_scene {
     ~rt_scene() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
-        blas_pairs.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
+        blas_pairs.release(); blas_quads.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
         quad_hot.release(); quad_cold.release(); materials.release(); out_rgba.release(); out_rgb.release();
         timeline.release(); costmap.release(); unit_cost.release(); unit_order.release();
         delete blas_builder; delete tlas_builder;
@@ -321,12 +325,17 @@ rt_status frame_update(rt_scene *s, uint64_t frame) {
     s->tlas = s->build_mode == RT_BUILD_SAH ? build_sah_tree(std::move(items), SAH_LEAF_CAP)
                                             : build_median_tree(std::move(items), TLAS_LEAF_CAP, hm::tlas_axis_state(s->build_seed, frame));
     s->tlas_flat = flatten_tree(s->tlas, 0, 0, 0, false);
+    s->tlas_wide = flatten_tree_wide(s->tlas, 0, 0, 0, false);
 
     TreeRoot root{};
     std::memcpy(root.box, s->tlas_flat.root_box, sizeof root.box);
     root.ref = s->tlas_flat.root_ref;
     root.height = s->tlas_flat.height;
     std::memcpy(st + s->off_root, &root, sizeof root);
+    root.ref = s->tlas_wide.root_ref;
+    root.height = s->tlas_wide.height;
+    std::memcpy(st + s->off_root_wide, &root, sizeof root);
+    std::memcpy(st + s->off_quads, s->tlas_wide.quads.data(), s->tlas_wide.quads.size() * sizeof(NodeQuad));
     std::memcpy(st + s->off_pairs, s->tlas_flat.pairs.data(), s->tlas_flat.pairs.size() * sizeof(NodePair));
     std::memcpy(st + s->off_slots, s->tlas.refs.data(), s->tlas.refs.size() * sizeof(uint32_t));
     for (size_t i = 0; i < s->inst.size(); i++) {
@@ -335,7 +344,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame) {
         store_rows(hot[i].inv, in.inv);
         std::memcpy(hot[i].root_box, bl.flat.root_box, sizeof hot[i].root_box);
         hot[i].root_ref = bl.flat.root_ref;
-        hot[i].pad = 0;
+        hot[i].root_ref_wide = bl.wide.root_ref;
         store_rows(cold[i].fwd, in.fwd);
         store_rows(cold[i].nrm, in.nrm);
     }
@@ -356,6 +365,10 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.blas_pairs = s->blas_pairs.p;
     g.tlas_pairs = reinterpret_cast<const NodePair *>(s->frame_dev[b] + s->off_pairs);
     g.tlas_root = reinterpret_cast<const TreeRoot *>(s->frame_dev[b] + s->off_root);
+    g.tlas_root_wide = reinterpret_cast<const TreeRoot *>(s->frame_dev[b] + s->off_root_wide);
+    g.tlas_quads = reinterpret_cast<const NodeQuad *>(s->frame_dev[b] + s->off_quads);
+    g.blas_quads = s->blas_quads.p;
+    g.wide = s->wide && !s->gpu_tlas() && s->blas_quads.p != nullptr ? 1u : 0u;
     g.tlas_slots = reinterpret_cast<const uint32_t *>(s->frame_dev[b] + s->off_slots);
     g.inst_hot = reinterpret_cast<const InstHot *>(s->frame_dev[b] + s->off_hot);
     g.inst_cold = reinterpret_cast<const InstCold *>(s->frame_dev[b] + s->off_cold);
@@ -517,7 +530,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     std::vector<std::pair<uint64_t, uint32_t>> seen;
     std::vector<LbvhSeg> segs;                  // RT_BUILD_LBVH: one tree per unique BLAS
     uint64_t item_total = 0;
-    uint32_t pair_base = 0;
+    uint32_t pair_base = 0, quad_base = 0;
     uint32_t slot_base[3] = {0, 0, 0};
     for (size_t i = 0; i < s->inst_desc.size(); i++) {
         const rt_instance_desc &id = s->inst_desc[i];
@@ -574,6 +587,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             if ((uint64_t)slot_base[in.ptype] + in.pcount >= MAX_LEAF_SLOTS)
                 return fail(RT_ERR_UNSUPPORTED, "too many primitives of one type (2^26 leaf slots)");
             bh.flat = flatten_tree(bh.tree, pair_base, bh.slot_base, in.ptype, true);
+            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, in.ptype, true);
+            quad_base += (uint32_t)bh.wide.quads.size();
             s->max_blas_height = std::max(s->max_blas_height, bh.flat.height);
             pair_base += (uint32_t)bh.flat.pairs.size();
             slot_base[in.ptype] += in.pcount;
@@ -595,6 +610,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     // leaf-ordered primitive arrays + node pairs
     std::vector<NodePair> pairs;
     pairs.reserve(pair_base);
+    std::vector<NodeQuad> quads;
+    quads.reserve(quad_base);
     std::vector<TriHot> th; std::vector<TriCold> tc;
     std::vector<SphereHot> sh; std::vector<PrimCold> sc;
     std::vector<QuadHot> qh; std::vector<PrimCold> qc;
@@ -603,6 +620,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     s->blas_leaf_count = 0;
     for (const BlasHost &bh : s->blas) {
         pairs.insert(pairs.end(), bh.flat.pairs.begin(), bh.flat.pairs.end());
+        quads.insert(quads.end(), bh.wide.quads.begin(), bh.wide.quads.end());
         s->blas_leaf_count += bh.flat.leaves;
         for (uint32_t pi : bh.tree.refs) {
             if (bh.type == RT_PRIM_TRIANGLE) {
@@ -639,6 +657,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     s->blas_pair_count = pairs.size();
 
     if ((st = upload(s->blas_pairs, pairs)) != RT_OK) return st;
+    if ((st = upload(s->blas_quads, quads)) != RT_OK) return st;
     if ((st = upload(s->tri_hot, th)) != RT_OK) return st;
     if ((st = upload(s->tri_cold, tc)) != RT_OK) return st;
     if ((st = upload(s->sph_hot, sh)) != RT_OK) return st;
@@ -657,7 +676,9 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     s->off_cold = align16(s->off_hot + n * sizeof(InstHot));
     s->off_tbox = align16(s->off_cold + n * sizeof(InstCold));
     s->off_tcent = align16(s->off_tbox + n * 6 * sizeof(float));
-    s->frame_block = align16(s->off_tcent + n * 4 * sizeof(float));
+    s->off_root_wide = 32;                                         // second half of the root's 64 B
+    s->off_quads = (s->off_tcent + n * 4 * sizeof(float) + 127) & ~size_t(127);
+    s->frame_block = s->off_quads + n * sizeof(NodeQuad);           // <= n - 1 quads
     if (mode == RT_BUILD_LBVH) {
         delete s->tlas_builder;
         s->tlas_builder = new LbvhBuilder();
@@ -819,8 +840,8 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         out.grab = s->grab;
         out.supertile = s->supertile;
         if (s->timeline_on) {
-            const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false)
-                                                    : persistent_blocks_per_cu_fast(s->variant, lean));
+            const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false, false)
+                                                    : persistent_blocks_per_cu_fast(s->variant, lean, g.wide != 0));
             const size_t words = (size_t)blocks * 4 * TIMELINE_WORDS;
             if (s->timeline.n < words) {
                 s->timeline.release();
@@ -879,10 +900,10 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     HIP_TRY(hipEventRecord(s->k_start, stream));
     if (s->use_persistent)
         HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, s->counters, s->queue,
-                                                       s->cus * persistent_blocks_per_cu_exact(s->variant, false), s->threshold,
+                                                       s->cus * persistent_blocks_per_cu_exact(s->variant, false, false), s->threshold,
                                                        s->variant, false, reset_queue, stream)
                       : launch_render_persistent_fast(g, cam, out, count, s->counters, s->queue,
-                                                      s->cus * persistent_blocks_per_cu_fast(s->variant, lean), s->threshold,
+                                                      s->cus * persistent_blocks_per_cu_fast(s->variant, lean, g.wide != 0), s->threshold,
                                                       s->variant, lean, reset_queue, stream));
     else
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, s->counters, stream)
@@ -989,6 +1010,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "costmap") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
         s->costmap_on = value == 1;
+    } else if (k == "wide") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "wide must be 0 or 1");
+        s->wide = value == 1;
     } else if (k == "split") {
         if (value < 0 || value > 0xFFFF) return fail(RT_ERR_INVALID_ARGUMENT, "split must be k_half | k_quarter << 8");
         s->split = (uint32_t)value;

@@ -358,6 +358,7 @@ struct Trav {
     Stack stk;
 };
 
+template <bool WIDE = false>
 __device__ __forceinline__ void trav_init(Trav &T, const SceneGPU &sc, const f3 &o, const f3 &d) {
     T.wr.o = o; T.wr.d = d; prep(T.wr);
     T.lr = T.wr;
@@ -365,7 +366,7 @@ __device__ __forceinline__ void trav_init(Trav &T, const SceneGPU &sc, const f3 
     T.found = false;
     T.stk.sp = 0;
     T.stk.spilled = 0;
-    const TreeRoot &R = *sc.tlas_root;                                    // this frame's TLAS root (HBM)
+    const TreeRoot &R = WIDE ? *sc.tlas_root_wide : *sc.tlas_root;      // this frame's TLAS root (HBM)
     T.cur = R.ref;
     T.cur_inst = 0;
     T.in_blas = false;
@@ -471,9 +472,78 @@ __device__ __forceinline__ void pop_next(Trav &T, const SEnt *spill) {
 }
 
 // One interior-loop step of a lane whose cur is an interior node, or a leaf to postpone.
+#if !RT_EXACT
+// Quad node (option "wide"): 4 slab tests on SoA bounds, hits sorted by entry t; the nearest is visited
+// next and the others are pushed farthest first (popped nearest first).  Not the reference's visit
+// order (FAST tolerance): the closest hit only differs on ties within the 1e-6 window.
+__device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float oinv, float4 &tn, float4 &tf) {
+    const float a0 = fmaf(lo.x, inv, -oinv), b0 = fmaf(hi.x, inv, -oinv);
+    const float a1 = fmaf(lo.y, inv, -oinv), b1 = fmaf(hi.y, inv, -oinv);
+    const float a2 = fmaf(lo.z, inv, -oinv), b2 = fmaf(hi.z, inv, -oinv);
+    const float a3 = fmaf(lo.w, inv, -oinv), b3 = fmaf(hi.w, inv, -oinv);
+    tn = make_float4(fmaxf(tn.x, fminf(a0, b0)), fmaxf(tn.y, fminf(a1, b1)), fmaxf(tn.z, fminf(a2, b2)), fmaxf(tn.w, fminf(a3, b3)));
+    tf = make_float4(fminf(tf.x, fmaxf(a0, b0)), fminf(tf.y, fmaxf(a1, b1)), fminf(tf.z, fmaxf(a2, b2)), fminf(tf.w, fmaxf(a3, b3)));
+}
+__device__ __forceinline__ void cswap(float &ta, uint32_t &ra, float &tb, uint32_t &rb) {
+    const bool sw = tb < ta;
+    const float t = sw ? tb : ta, u = sw ? ta : tb;
+    const uint32_t r = sw ? rb : ra, q = sw ? ra : rb;
+    ta = t; tb = u; ra = r; rb = q;
+}
 template <bool COUNT>
+__device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
+    const uint32_t cur = T.cur;
+    const bool blas = (cur & REF_BLAS) != 0;
+    const float4 *Q = reinterpret_cast<const float4 *>((blas ? sc.blas_quads : sc.tlas_quads) + (cur & REF_INDEX_MASK));
+    const float4 lx = Q[0], hx = Q[1], ly = Q[2], hy = Q[3], lz = Q[4], hz = Q[5];
+    const uint4 R = reinterpret_cast<const uint4 *>(Q)[6];
+    if (COUNT) cnt.pairs += 2;                       // 4 child boxes = 2 node-pair equivalents
+    const RayP &r = blas ? T.lr : T.wr;
+    float t[4];
+    bool h[4];
+    if (!r.tiny) {
+        float4 tn = make_float4(TMIN, TMIN, TMIN, TMIN), tf = make_float4(T.tmax, T.tmax, T.tmax, T.tmax);
+        slab4(lx, hx, r.inv.x, r.oinv.x, tn, tf);
+        slab4(ly, hy, r.inv.y, r.oinv.y, tn, tf);
+        slab4(lz, hz, r.inv.z, r.oinv.z, tn, tf);
+        t[0] = tn.x; t[1] = tn.y; t[2] = tn.z; t[3] = tn.w;
+        h[0] = tn.x < tf.x; h[1] = tn.y < tf.y; h[2] = tn.z < tf.z; h[3] = tn.w < tf.w;
+    } else {                                          // some |d_axis| < 1e-6: the reference's slab per child
+        const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+        const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
+        const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const float b[6] = {LX[k], HX[k], LY[k], HY[k], LZ[k], HZ[k]};
+            t[k] = 0.0f;
+            h[k] = slab_ref(b, r.o, r.d, TMIN, T.tmax, t[k]);
+        }
+    }
+    float t0 = h[0] ? t[0] : __builtin_huge_valf(), t1 = h[1] ? t[1] : __builtin_huge_valf();
+    float t2 = h[2] ? t[2] : __builtin_huge_valf(), t3 = h[3] ? t[3] : __builtin_huge_valf();
+    uint32_t r0 = R.x, r1 = R.y, r2 = R.z, r3 = R.w;
+    const uint32_t nh = (uint32_t)h[0] + (uint32_t)h[1] + (uint32_t)h[2] + (uint32_t)h[3];
+    if (nh == 0) { pop_next(T, spill); return; }
+    // sort the 4 (t, ref) ascending; misses (t = inf) sink to the end
+    cswap(t0, r0, t1, r1); cswap(t2, r2, t3, r3); cswap(t0, r0, t2, r2); cswap(t1, r1, t3, r3); cswap(t1, r1, t2, r2);
+    if (nh > 3) stack_push(T.stk, spill, r3, t3, cnt);
+    if (nh > 2) stack_push(T.stk, spill, r2, t2, cnt);
+    if (nh > 1) stack_push(T.stk, spill, r1, t1, cnt);
+    T.cur = r0;
+    T.curT = t0;
+}
+#endif
+
+template <bool COUNT, bool WIDE = false>
 __device__ __forceinline__ void spec_interior_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
     const uint32_t cur = T.cur;
+#if !RT_EXACT
+    if (WIDE) {
+        if (!(cur & REF_LEAF)) wide_interior_step<COUNT>(T, sc, spill, cnt);
+        else { T.pleaf = cur; pop_next(T, spill); }        // postpone, keep walking
+        return;
+    }
+#endif
     if (!(cur & REF_LEAF)) {
         const bool blas = (cur & REF_BLAS) != 0;
         const NodePair *P = (blas ? sc.blas_pairs : sc.tlas_pairs) + (cur & REF_INDEX_MASK);
@@ -507,7 +577,7 @@ __device__ __forceinline__ void spec_interior_step(Trav &T, const SceneGPU &sc, 
 }
 
 // Process the postponed leaf, then resume at cur (re-tested) — TLAS.cu:157-173 / BLAS.cu:153-176.
-template <bool COUNT>
+template <bool COUNT, bool WIDE = false>
 __device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
     const uint32_t leaf = T.pleaf;
     T.pleaf = REF_NONE;
@@ -524,7 +594,7 @@ __device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEn
         T.lr.d = xf_vector(I.inv, T.wr.d);
         prep(T.lr);
         float te = 0.0f;
-        if (slab(I.root_box, T.lr, TMIN, T.tmax, te)) { T.cur = I.root_ref; T.curT = te; }
+        if (slab(I.root_box, T.lr, TMIN, T.tmax, te)) { T.cur = WIDE ? I.root_ref_wide : I.root_ref; T.curT = te; }
         else pop_next(T, spill);
     } else {
         const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf), type = ref_leaf_type(leaf);
@@ -571,8 +641,8 @@ __device__ __forceinline__ unsigned long long stamp() {
 #endif
 
 // One round: interior loop until every traversing lane holds a leaf, then the leaf phase.
-template <bool COUNT>
 // steps (when `track`): the lane's interior steps + leaf phases, the pixel's cost for the work order
+template <bool COUNT, bool WIDE = false>
 __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt,
                                            PhaseCycles &pc, uint32_t &steps, bool track) {
     DIAG_T(t0);
@@ -581,7 +651,7 @@ __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *sp
         if (!__any(T.tracing && T.pleaf == REF_NONE)) break;
         const bool active = T.tracing && T.cur != REF_NONE && (!(T.cur & REF_LEAF) || T.pleaf == REF_NONE);
         if (active) {
-            spec_interior_step<COUNT>(T, sc, spill, cnt);
+            spec_interior_step<COUNT, WIDE>(T, sc, spill, cnt);
             if (track) steps++;
         }
         if (RT_DIAG) pc.iters++;
@@ -589,7 +659,7 @@ __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *sp
     DIAG_ADD(pc.interior, t0);
     DIAG_T(t1);
     if (T.tracing) {
-        spec_leaf_phase<COUNT>(T, sc, spill, cnt);
+        spec_leaf_phase<COUNT, WIDE>(T, sc, spill, cnt);
         if (track) steps++;
     }
     DIAG_ADD(pc.leaf, t1);
@@ -1007,7 +1077,7 @@ __device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t
     }
 }
 
-template <bool COUNT, bool LEAN>
+template <bool COUNT, bool LEAN, bool WIDE>
 __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out,
                                                        uint32_t *queue, uint32_t threshold,
                                                        unsigned long long *counters) {
@@ -1121,7 +1191,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     px_steps = 0;
                     f3 o, d;
                     camera_ray(cam, px, py, 0, rng, o, d);
-                    trav_init(T, sc, o, d);
+                    trav_init<WIDE>(T, sc, o, d);
                     pixels++;
                 }
             }
@@ -1143,7 +1213,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             if constexpr (LEAN) lean_round<COUNT>(T, sc, cnt, pc, px_steps, COUNT || track);
             else
 #endif
-                spec_round<COUNT>(T, sc, spill, cnt, pc, px_steps, COUNT || track);
+                spec_round<COUNT, WIDE>(T, sc, spill, cnt, pc, px_steps, COUNT || track);
             n_rounds++;
         }
         // ---- shade lanes whose segment finished (rayColor body, Kernel.cu:64-100)
@@ -1195,7 +1265,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     fin = true;
                 }
             }
-            if (has) trav_init(T, sc, no, nd);
+            if (has) trav_init<WIDE>(T, sc, no, nd);
         }
         if (track) unit_cost_add(out.unit_cost, fin, item >> 6, px_steps + 1u);
         DIAG_ADD(pc.shade, t_shade);
@@ -1240,11 +1310,11 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
 }
 
 // Register budget variants: WPE = minimum waves per SIMD the compiler must allow (0 = its choice).
-template <bool COUNT, int WPE, bool LEAN>
+template <bool COUNT, int WPE, bool LEAN, bool WIDE = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
 void render_persistent_kernel(SceneGPU sc, CameraGPU cam, OutputGPU out, uint32_t *queue, uint32_t threshold,
                               unsigned long long *counters) {
-    render_persistent_body<COUNT, LEAN>(sc, cam, out, queue, threshold, counters);
+    render_persistent_body<COUNT, LEAN, WIDE>(sc, cam, out, queue, threshold, counters);
 }
 
 __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const float *rays, uint32_t n, rt_hit *hits) {
@@ -1289,7 +1359,7 @@ hipError_t RT_SUFFIX(launch_render)(const SceneGPU &sc, const CameraGPU &cam, co
 }
 
 namespace {
-template <int WPE, bool LEAN>
+template <int WPE, bool LEAN, bool WIDE = false>
 hipError_t launch_persistent_wpe(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
                                  unsigned long long *counters, uint32_t *queue, uint32_t blocks_per_cu_cus,
                                  uint32_t threshold, hipStream_t stream) {
@@ -1297,22 +1367,24 @@ hipError_t launch_persistent_wpe(const SceneGPU &sc, const CameraGPU &cam, const
     const uint32_t need = (out.units + (BLOCK / 64) - 1) / (BLOCK / 64);
     const dim3 grid(blocks_per_cu_cus < need ? blocks_per_cu_cus : need);
     if (count)
-        hipLaunchKernelGGL((render_persistent_kernel<true, WPE, LEAN>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
+        hipLaunchKernelGGL((render_persistent_kernel<true, WPE, LEAN, WIDE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
     else
-        hipLaunchKernelGGL((render_persistent_kernel<false, WPE, LEAN>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
+        hipLaunchKernelGGL((render_persistent_kernel<false, WPE, LEAN, WIDE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
     return hipGetLastError();
 }
-template <int WPE, bool LEAN>
+template <int WPE, bool LEAN, bool WIDE = false>
 uint32_t blocks_per_cu_wpe() {
     using namespace RT_SUFFIX(dev);
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false, WPE, LEAN>, BLOCK, 0) != hipSuccess) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false, WPE, LEAN, WIDE>, BLOCK, 0) != hipSuccess) return 1;
     return n > 0 ? (uint32_t)n : 1u;
 }
 #if RT_EXACT
 constexpr bool HAS_LEAN = false;
+constexpr bool HAS_WIDE = false;      // EXACT keeps the reference's binary trees and visit order
 #else
 constexpr bool HAS_LEAN = true;
+constexpr bool HAS_WIDE = true;
 #endif
 }  // namespace
 
@@ -1332,17 +1404,20 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
         if (variant == 5) return launch_persistent_wpe<5, HAS_LEAN>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
         return launch_persistent_wpe<3, HAS_LEAN>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     }
+    if (sc.wide && HAS_WIDE)
+        return launch_persistent_wpe<0, false, HAS_WIDE>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     if (variant == 4) return launch_persistent_wpe<4, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     if (variant == 5) return launch_persistent_wpe<5, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     return launch_persistent_wpe<0, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
 }
 
-uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, bool lean) {
+uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, bool lean, bool wide) {
     if (lean && HAS_LEAN) {
         if (variant == 4) return blocks_per_cu_wpe<4, HAS_LEAN>();
         if (variant == 5) return blocks_per_cu_wpe<5, HAS_LEAN>();
         return blocks_per_cu_wpe<3, HAS_LEAN>();
     }
+    if (wide && HAS_WIDE) return blocks_per_cu_wpe<0, false, HAS_WIDE>();
     if (variant == 4) return blocks_per_cu_wpe<4, false>();
     if (variant == 5) return blocks_per_cu_wpe<5, false>();
     return blocks_per_cu_wpe<0, false>();

@@ -317,3 +317,51 @@ def test_reorder_schedule_is_byte_identical(gpu_lib, exact):
         cost_prev = cost.copy()
     for _ in range(2):                                # tile shard: first launch of a layout, then ordered
         assert np.array_equal(r.render(3, exact=exact, tiles=(64, 64, 1, 3), skip_update=True)[0], tref)
+
+
+@pytest.mark.parametrize("depth,need", [(1, 0.999), (2, 0.999), (4, 0.995)])
+def test_wide_trees_within_tolerance(gpu_lib, depth, need):
+    """Option "wide" (FAST persistent kernel on the 4-child collapse of the same trees): the leaves and
+    boxes are the binary tree's, only the visit order changes, so images stay within the FAST
+    tolerance of the oracle and of the binary-tree traversal, with the same number of rays."""
+    from oracle.oracle import OracleScene
+    s = scenes.demo_with_particles(16)
+    o = OracleScene(s, build_seed=0)
+    o.camera(320, 180, ray_trace_depth=depth)
+    orgb, orgba, ocnt = o.render(threads=THREADS)
+    for mode in ("compat", "sah"):
+        r = Renderer(s).build_acceleration_structure(0, mode=mode).configure_camera(320, 180, ray_trace_depth=depth)
+        out = {}
+        for wide in (0, 1):
+            r.set_option("wide", wide)
+            out[wide] = r.render(0, want_rgb=True, count_work=True)
+            f, mx = frac_within(out[wide][0], orgba)
+            assert f >= need, (mode, wide, f, mx)
+            assert abs(out[wide][2]["rays"] - ocnt["rays"]) <= 0.001 * ocnt["rays"]
+        f, _ = frac_within(out[0][0], out[1][0])
+        assert f >= need, (mode, f)
+        r.cleanup()
+
+
+def test_wide_large_blas_stack(gpu_lib):
+    """A 65k-triangle BLAS under the TLAS through the quad traversal: deep trees push up to 3 entries
+    per quad; the result stays within the FAST tolerance of the oracle and never overflows."""
+    from oracle.oracle import OracleScene
+    tris, inst = scenes.synth_particles(64, 1024, seed=3)
+    s = scenes.demo_scene()
+    s.triangles = np.concatenate([tris, s.triangles])
+    for d in s.instances:
+        if d["type"] == 2:
+            d["index"] += tris.shape[0]
+    lo = np.minimum.reduce([np.asarray(d["bounds"][0::2]) for d in inst])
+    hi = np.maximum.reduce([np.asarray(d["bounds"][1::2]) for d in inst])
+    s.instances.append(dict(type=2, index=0, count=tris.shape[0],
+                            bounds=(lo[0], hi[0], lo[1], hi[1], lo[2], hi[2]), centroid=tuple((lo + hi) / 2),
+                            shift=(0.0, 4.0, 0.0), rotate=(90.0, 0.0, 0.0), scale=(3.0, 3.0, 3.0)))
+    r, o = pair(s, 4, 200, 120, ray_trace_depth=2)
+    r.set_option("wide", 1)
+    rgba, _, st = r.render(0, count_work=True)          # raises on a stack overflow
+    _, orgba, ocnt = o.render(threads=THREADS)
+    f, mx = frac_within(rgba, orgba)
+    assert f >= 0.999, (f, mx)
+    assert abs(st["rays"] - ocnt["rays"]) <= 0.001 * ocnt["rays"]
