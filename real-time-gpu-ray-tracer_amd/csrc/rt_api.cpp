@@ -33,7 +33,8 @@ hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, c
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
 hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t, uint32_t,
-                           hipStream_t);
+                           void *, const void *, size_t, hipStream_t);
+hipError_t launch_frame_copy(void *, const void *, size_t, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean, bool wide);
 hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, uint32_t, hipStream_t);
 uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean, bool wide);
@@ -138,13 +139,14 @@ struct rt_scene {
     size_t frame_block = 0, off_root = 0, off_pairs = 0, off_slots = 0, off_hot = 0, off_cold = 0, off_tbox = 0,
            off_tcent = 0, off_root_wide = 0, off_quads = 0;
     uint8_t *staging[2] = {nullptr, nullptr};     // pinned host
+    uint8_t *staging_dev[2] = {nullptr, nullptr}; // the same, as device-visible pointers
+    int pending_copy = -1;                        // rt_render: block whose upload the next launch performs
     uint8_t *frame_dev[2] = {nullptr, nullptr};   // HBM
     hipEvent_t ev_copied[2] = {nullptr, nullptr}; // upload from staging[b] finished
     hipEvent_t ev_used[2] = {nullptr, nullptr};   // last kernel reading frame_dev[b] finished
     int active = -1;
 
     hipStream_t stream = nullptr;
-    hipEvent_t k_start = nullptr, k_stop = nullptr;
     // per-frame kernel timing ring for pipelined frames (rt_scene_collect)
     static constexpr uint32_t RING = 256;
     hipEvent_t ring_start[RING] = {}, ring_stop[RING] = {};
@@ -223,8 +225,6 @@ struct rt_scene {
             if (ring_start[i]) (void)hipEventDestroy(ring_start[i]);
             if (ring_stop[i]) (void)hipEventDestroy(ring_stop[i]);
         }
-        if (k_start) (void)hipEventDestroy(k_start);
-        if (k_stop) (void)hipEventDestroy(k_stop);
         if (stream) (void)hipStreamDestroy(stream);
     }
 };
@@ -272,7 +272,11 @@ rt_status gpu_build_blas(rt_scene *s);
 // Host half of one frame: update callback, instance matrices, TLAS rebuild, staging, upload.
 // RT_BUILD_LBVH: the host stages matrices and transformed instance boxes only; the BLAS roots are
 // patched into the instance records and the TLAS is built by kernels on the scene's stream.
-rt_status frame_update(rt_scene *s, uint64_t frame) {
+// `upload` (host-built trees): the stream the upload is enqueued on — rt_render passes the stream the
+// trace will run on, so upload -> schedule -> trace stay in one queue (a wait on an event of another
+// queue cost ~35 us per frame, measured).
+// defer (rt_render): the copy itself is left to the next launch on `upload` (pending_copy).
+rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool defer = false) {
     const int b = s->active < 0 ? 0 : 1 - s->active;
     HIP_TRY(hipEventSynchronize(s->ev_copied[b]));     // staging[b] no longer read by a pending copy
     if (s->update) {                                  // Renderer.cu:269
@@ -348,12 +352,16 @@ rt_status frame_update(rt_scene *s, uint64_t frame) {
         store_rows(cold[i].fwd, in.fwd);
         store_rows(cold[i].nrm, in.nrm);
     }
-    // Measured: the same upload on a separate copy stream (the reference's copyStream, Renderer.cu:281-303)
-    // goes through an SDMA engine whose first use stalled a frame by ~7.6 ms; on the scene's stream it is
-    // a ~4 us blit kernel between two traces.
-    HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_used[b], 0));        // frame_dev[b] free on device
-    HIP_TRY(hipMemcpyAsync(s->frame_dev[b], st, s->frame_block, hipMemcpyHostToDevice, s->stream));
-    HIP_TRY(hipEventRecord(s->ev_copied[b], s->stream));
+    // Measured: the upload on a dedicated copy stream (the reference's copyStream, Renderer.cu:281-303)
+    // went through an SDMA engine whose first use stalled a frame by ~7.6 ms; enqueued on the trace's
+    // stream it is a ~4 us blit kernel between two traces.
+    HIP_TRY(hipStreamWaitEvent(upload, s->ev_used[b], 0));           // frame_dev[b] free on device
+    if (defer) {
+        s->pending_copy = b;
+    } else {
+        HIP_TRY(hipMemcpyAsync(s->frame_dev[b], st, s->frame_block, hipMemcpyHostToDevice, upload));
+        HIP_TRY(hipEventRecord(s->ev_copied[b], upload));
+    }
     s->active = b;
     s->frame = frame;
     return RT_OK;
@@ -689,12 +697,11 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         if (s->staging[b]) { (void)hipHostFree(s->staging[b]); s->staging[b] = nullptr; }
         if (s->frame_dev[b]) { (void)hipFree(s->frame_dev[b]); s->frame_dev[b] = nullptr; }
         HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->staging[b]), s->frame_block, hipHostMallocDefault));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s->staging_dev[b]), s->staging[b], 0));
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->frame_dev[b]), s->frame_block));
         if (!s->ev_copied[b]) HIP_TRY(hipEventCreateWithFlags(&s->ev_copied[b], hipEventDisableTiming));
         if (!s->ev_used[b]) HIP_TRY(hipEventCreateWithFlags(&s->ev_used[b], hipEventDisableTiming));
     }
-    if (!s->k_start) HIP_TRY(hipEventCreate(&s->k_start));
-    if (!s->k_stop) HIP_TRY(hipEventCreate(&s->k_stop));
     for (uint32_t i = 0; i < rt_scene::RING; i++) {
         if (!s->ring_start[i]) HIP_TRY(hipEventCreate(&s->ring_start[i]));
         if (!s->ring_stop[i]) HIP_TRY(hipEventCreate(&s->ring_stop[i]));
@@ -721,7 +728,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     // initial transforms, then the frame-0 update + TLAS (Renderer.cu:110-111, 148-150)
     for (size_t i = 0; i < n; i++) instance_update(s->inst[i], s->inst_desc[i].xform);
     s->built = true;
-    return frame_update(s, 0);
+    return frame_update(s, 0, s->stream);
 }
 
 rt_status rt_camera_set(rt_scene *s, const rt_camera_input *c, uint32_t w, uint32_t h) {
@@ -762,7 +769,7 @@ rt_status rt_scene_update(rt_scene *s, uint64_t frame) {
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
     if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
     HIP_TRY(hipSetDevice(s->device));
-    return frame_update(s, frame);
+    return frame_update(s, frame, s->stream);
 }
 
 uint32_t rt_tiles_for_rank(const rt_scene *s, uint32_t tw, uint32_t th, uint32_t rank, uint32_t count) {
@@ -780,14 +787,14 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     if (opts) o = *opts;
     if (o.frame_seed == 0) o.frame_seed = 0x5EED;
     HIP_TRY(hipSetDevice(s->device));
+    hipStream_t stream = o.stream ? static_cast<hipStream_t>(o.stream) : s->stream;
     double update_ms = 0.0;
     if (!(o.flags & RT_RENDER_SKIP_UPDATE)) {
         const auto u0 = std::chrono::steady_clock::now();
-        const rt_status st = frame_update(s, frame);
+        const rt_status st = frame_update(s, frame, stream, /*defer=*/true);
         if (st != RT_OK) return st;
         update_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - u0).count();
     }
-    hipStream_t stream = o.stream ? static_cast<hipStream_t>(o.stream) : s->stream;
 
     OutputGPU out{};
     out.nt_store = s->nt_store;
@@ -881,13 +888,22 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         const bool do_order = s->sched_valid && std::memcmp(sig, s->sched_sig, sizeof sig) == 0;
         const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
         const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
+        const int pc = s->pending_copy;
         HIP_TRY(launch_schedule(s->unit_cost.p, s->unit_order.p, s->queue, rows, upr, out.queue_parts, do_order,
-                                s->split & 0xFFu, (s->split >> 8) & 0xFFu, stream));
+                                s->split & 0xFFu, (s->split >> 8) & 0xFFu, pc >= 0 ? s->frame_dev[pc] : nullptr,
+                                pc >= 0 ? s->staging_dev[pc] : nullptr, pc >= 0 ? s->frame_block : 0, stream));
+        if (pc >= 0) HIP_TRY(hipEventRecord(s->ev_copied[pc], stream));
+        s->pending_copy = -1;
         std::memcpy(s->sched_sig, sig, sizeof sig);
         s->sched_valid = true;
         out.order = do_order ? s->unit_order.p : nullptr;
         out.unit_cost = s->unit_cost.p;
         reset_queue = false;
+    }
+    if (s->pending_copy >= 0) {                // no schedule launch carried the upload
+        HIP_TRY(launch_frame_copy(s->frame_dev[s->pending_copy], s->staging_dev[s->pending_copy], s->frame_block, stream));
+        HIP_TRY(hipEventRecord(s->ev_copied[s->pending_copy], stream));
+        s->pending_copy = -1;
     }
     HIP_TRY(hipStreamWaitEvent(stream, s->ev_copied[s->active], 0));
     if (!(o.flags & RT_RENDER_KEEP_COUNTERS))
@@ -897,7 +913,6 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     if (s->ring_pending < rt_scene::RING) s->ring_pending++;
     s->last_stream = stream;
     HIP_TRY(hipEventRecord(s->ring_start[slot], stream));
-    HIP_TRY(hipEventRecord(s->k_start, stream));
     if (s->use_persistent)
         HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, s->counters, s->queue,
                                                        s->cus * persistent_blocks_per_cu_exact(s->variant, false, false), s->threshold,
@@ -908,7 +923,6 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     else
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, s->counters, stream)
                       : launch_render_fast(g, cam, out, count, s->counters, stream));
-    HIP_TRY(hipEventRecord(s->k_stop, stream));
     HIP_TRY(hipEventRecord(s->ring_stop[slot], stream));
     HIP_TRY(hipEventRecord(s->ev_used[s->active], stream));
     HIP_TRY(hipEventRecord(s->ev_render_done, stream));
@@ -923,7 +937,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     if (rgb_host) HIP_TRY(hipMemcpy(rgb_host, out.rgb, npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
     if (stats) {
         float kms = 0.0f;
-        HIP_TRY(hipEventElapsedTime(&kms, s->k_start, s->k_stop));
+        HIP_TRY(hipEventElapsedTime(&kms, s->ring_start[slot], s->ring_stop[slot]));
         fill_stats(stats, s->counters_host);
         stats->kernel_ms = kms;
         stats->update_ms = update_ms;

@@ -48,12 +48,15 @@ __device__ __forceinline__ uint32_t split_log2(uint32_t cls, uint32_t k_half, ui
 __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__restrict__ cost, uint32_t *__restrict__ order,
                                                                  uint32_t *__restrict__ queue, uint32_t rows,
                                                                  uint32_t upr, uint32_t parts, uint32_t do_order,
-                                                                 uint32_t k_half, uint32_t k_quarter) {
+                                                                 uint32_t k_half, uint32_t k_quarter, uint4 *copy_dst,
+                                                                 const uint4 *copy_src, uint32_t copy_n16) {
     __shared__ uint32_t cnt[SCHED_CLASSES][SCHED_THREADS];   // per-thread class counts -> exclusive offsets
     __shared__ uint32_t total[SCHED_CLASSES];
     __shared__ uint32_t base[SCHED_CLASSES];
     const uint32_t part = blockIdx.x, t = threadIdx.x;
     if (part == 0 && t < QUEUE_MAX_PARTS) queue[t * QUEUE_STRIDE] = 0u;      // every head: `parts` may change
+    // the frame's TLAS / instance block, read from pinned host staging (see launch_frame_copy)
+    for (uint32_t i = part * SCHED_THREADS + t; i < copy_n16; i += parts * SCHED_THREADS) copy_dst[i] = copy_src[i];
     // the band's unit range, computed exactly as the render kernel computes it
     const uint32_t b0 = rows * part / parts * upr, b1 = rows * (part + 1) / parts * upr;
     const uint32_t n = b1 - b0, per = (n + SCHED_THREADS - 1) / SCHED_THREADS;
@@ -105,10 +108,29 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
 // rows x upr units per frame split into `parts` bands as in render_persistent_body; do_order = 0 only
 // clears the costs and the queue heads (first launch of a layout: no costs recorded yet).
 hipError_t launch_schedule(uint32_t *cost, uint32_t *order, uint32_t *queue, uint32_t rows, uint32_t upr,
-                           uint32_t parts, bool do_order, uint32_t k_half, uint32_t k_quarter, hipStream_t stream) {
-    if (parts == 0 || parts > QUEUE_MAX_PARTS) return hipErrorInvalidValue;
+                           uint32_t parts, bool do_order, uint32_t k_half, uint32_t k_quarter, void *copy_dst,
+                           const void *copy_src, size_t copy_bytes, hipStream_t stream) {
+    if (parts == 0 || parts > QUEUE_MAX_PARTS || copy_bytes % 16) return hipErrorInvalidValue;
     hipLaunchKernelGGL(schedule_kernel, dim3(parts), dim3(SCHED_THREADS), 0, stream, cost, order, queue, rows, upr, parts,
-                       do_order ? 1u : 0u, k_half, k_quarter);
+                       do_order ? 1u : 0u, k_half, k_quarter, static_cast<uint4 *>(copy_dst),
+                       static_cast<const uint4 *>(copy_src), (uint32_t)(copy_bytes / 16));
+    return hipGetLastError();
+}
+
+// Per-frame upload of the TLAS / instance block by a kernel reading the pinned staging buffer over
+// PCIe.  hipMemcpyAsync of the same ~35 KB is handed to an SDMA engine and, between two traces on
+// one stream, cost ~35 us of idle GPU per frame (rocprofv3 trace); the schedule kernel does this copy
+// itself when option "reorder" is on.
+__global__ __launch_bounds__(256) void frame_copy_kernel(uint4 *__restrict__ dst, const uint4 *__restrict__ src, uint32_t n16) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n16; i += gridDim.x * 256u) dst[i] = src[i];
+}
+hipError_t launch_frame_copy(void *dst, const void *src, size_t bytes, hipStream_t stream) {
+    if (bytes % 16) return hipErrorInvalidValue;
+    const uint32_t n16 = (uint32_t)(bytes / 16);
+    if (n16 == 0) return hipSuccess;
+    const uint32_t blocks = n16 / 256u + 1u < 64u ? n16 / 256u + 1u : 64u;
+    hipLaunchKernelGGL(frame_copy_kernel, dim3(blocks), dim3(256), 0, stream, static_cast<uint4 *>(dst),
+                       static_cast<const uint4 *>(src), n16);
     return hipGetLastError();
 }
 
