@@ -365,3 +365,16 @@ def test_wide_large_blas_stack(gpu_lib):
     f, mx = frac_within(rgba, orgba)
     assert f >= 0.999, (f, mx)
     assert abs(st["rays"] - ocnt["rays"]) <= 0.001 * ocnt["rays"]
+
+
+@pytest.mark.parametrize("split", [0x0000, 0x0C00, 0xFFFF])
+def test_split_claims_are_byte_identical(gpu_lib, split):
+    """Heavy units claimed as 1/2 or 1/4 items (option "split"; 0x0000 quarters every unit, 0xFFFF
+    never splits) only change which wave traces which pixel: frames equal the screen-order walk."""
+    s = scenes.demo_with_particles(8)
+    r = Renderer(s).build_acceleration_structure(1, mode="sah").configure_camera(264, 152, ray_trace_depth=3)
+    r.set_option("reorder", 0)
+    ref = [r.render(f)[0] for f in range(3)]
+    r.set_option("reorder", 1).set_option("split", split)
+    for f in range(3):
+        assert np.array_equal(r.render(f)[0], ref[f]), (split, f)
