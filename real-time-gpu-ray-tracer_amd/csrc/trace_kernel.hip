@@ -1404,8 +1404,10 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
         if (variant == 5) return launch_persistent_wpe<5, HAS_LEAN>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
         return launch_persistent_wpe<3, HAS_LEAN>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     }
-    if (sc.wide && HAS_WIDE)
+    if (sc.wide && HAS_WIDE) {
+        if (variant == 4) return launch_persistent_wpe<4, false, HAS_WIDE>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
         return launch_persistent_wpe<0, false, HAS_WIDE>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+    }
     if (variant == 4) return launch_persistent_wpe<4, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     if (variant == 5) return launch_persistent_wpe<5, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     return launch_persistent_wpe<0, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
@@ -1417,7 +1419,7 @@ uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, bool lean, bool w
         if (variant == 5) return blocks_per_cu_wpe<5, HAS_LEAN>();
         return blocks_per_cu_wpe<3, HAS_LEAN>();
     }
-    if (wide && HAS_WIDE) return blocks_per_cu_wpe<0, false, HAS_WIDE>();
+    if (wide && HAS_WIDE) return variant == 4 ? blocks_per_cu_wpe<4, false, HAS_WIDE>() : blocks_per_cu_wpe<0, false, HAS_WIDE>();
     if (variant == 4) return blocks_per_cu_wpe<4, false>();
     if (variant == 5) return blocks_per_cu_wpe<5, false>();
     return blocks_per_cu_wpe<0, false>();
