@@ -1,0 +1,66 @@
+// Host check of flatten_tree_wide (csrc/bvh_build.hpp): the quad form of a binary tree holds exactly
+// the binary tree's leaves and child boxes.  Built and run by tests/test_wide_collapse.py (g++, CPU).
+#include <cstdio>
+#include <map>
+#include <random>
+#include <set>
+
+#include "../../real-time-gpu-ray-tracer_amd/csrc/bvh_build.hpp"
+
+using namespace rtamd;
+
+int main(int argc, char **argv) {
+    const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 1000;
+    const int sah = argc > 2 ? atoi(argv[2]) : 1;
+    std::mt19937 rng(n * 7 + sah);
+    std::uniform_real_distribution<float> U(-10.0f, 10.0f), S(0.01f, 1.0f);
+    std::vector<BuildItem> items(n);
+    for (uint32_t i = 0; i < n; i++) {
+        const float x = U(rng), y = U(rng), z = U(rng), s = S(rng);
+        items[i].box = hm::Box::from_ranges({x, x + s}, {y, y + s}, {z, z + s});
+        items[i].centroid = hm::v3(x + s / 2, y + s / 2, z + s / 2);
+        items[i].index = i;
+    }
+    const Tree t = sah ? build_sah_tree(items, 4) : build_median_tree(items, 4, 12345);
+    const FlatTree f2 = flatten_tree(t, 0, 100, 2, true);
+    const FlatWide f4 = flatten_tree_wide(t, 0, 100, 2, true);
+    // leaves and boxes reachable from each form
+    std::multiset<uint32_t> leaves2, leaves4;
+    std::set<std::vector<float>> boxes2, boxes4;
+    std::vector<uint32_t> todo{f2.root_ref};
+    while (!todo.empty()) {
+        const uint32_t r = todo.back(); todo.pop_back();
+        if (r & REF_LEAF) { leaves2.insert(r); continue; }
+        const NodePair &p = f2.pairs[r & REF_INDEX_MASK];
+        boxes2.insert(std::vector<float>(p.c0, p.c0 + 6)); boxes2.insert(std::vector<float>(p.c1, p.c1 + 6));
+        todo.push_back(p.ref0); todo.push_back(p.ref1);
+    }
+    int bad = 0, quads = 0, children = 0, min_children = 4;
+    todo = {f4.root_ref};
+    while (!todo.empty()) {
+        const uint32_t r = todo.back(); todo.pop_back();
+        if (r & REF_LEAF) { leaves4.insert(r); continue; }
+        const NodeQuad &q = f4.quads[r & REF_INDEX_MASK];
+        quads++;
+        int nc = 0;
+        for (int k = 0; k < 4; k++) {
+            if (q.ref[k] == REF_EMPTY) {
+                bad += !(q.lo_x[k] == INFINITY && q.hi_x[k] == INFINITY && q.lo_z[k] == INFINITY && q.hi_z[k] == INFINITY);
+                continue;
+            }
+            nc++;
+            const float b[6] = {q.lo_x[k], q.hi_x[k], q.lo_y[k], q.hi_y[k], q.lo_z[k], q.hi_z[k]};
+            const std::vector<float> v(b, b + 6);
+            bad += boxes2.count(v) == 0;          // every quad child box is a binary node box
+            boxes4.insert(v);
+            todo.push_back(q.ref[k]);
+        }
+        children += nc;
+        min_children = nc < min_children ? nc : min_children;
+    }
+    printf("{\"n\": %u, \"sah\": %d, \"leaves_equal\": %d, \"bad_boxes\": %d, \"quads\": %d, \"pairs\": %zu, "
+           "\"mean_children\": %.3f, \"min_children\": %d, \"height2\": %u, \"height4\": %u}\n",
+           n, sah, (int)(leaves2 == leaves4), bad, quads, f2.pairs.size(), quads ? (double)children / quads : 0.0,
+           min_children, f2.height, f4.height);
+    return 0;
+}
