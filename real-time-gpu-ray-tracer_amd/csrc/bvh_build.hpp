@@ -279,12 +279,24 @@ struct FlatWide {
     uint32_t height = 0;           // quad levels on the longest root-to-leaf path
 };
 
-inline FlatWide flatten_tree_wide(const Tree &t, uint32_t quad_base, uint32_t slot_base, uint32_t ptype, bool blas) {
+// merge_cap > 0: a binary subtree holding <= merge_cap items (<= 4, the leaf ref's count field) becomes
+// one leaf — its leaves are contiguous slots (the builders emit leaves depth-first, left first).  Fewer,
+// fuller leaves mean fewer leaf rounds per ray for the same primitive tests.
+inline FlatWide flatten_tree_wide(const Tree &t, uint32_t quad_base, uint32_t slot_base, uint32_t ptype, bool blas,
+                                  uint32_t merge_cap = 0) {
     FlatWide f;
     const uint32_t n = (uint32_t)t.nodes.size();
     if (n == 0) return f;
-    auto leaf_ref = [&](uint32_t j) { return make_leaf_ref(slot_base + t.nodes[j].index, t.nodes[j].count, ptype, blas); };
-    if (t.nodes[0].count > 0) { f.root_ref = leaf_ref(0); return f; }
+    // subtree item counts and first slots (children have larger indices than their parent)
+    std::vector<uint32_t> items(n), first(n);
+    for (uint32_t j = n; j-- > 0;) {
+        const TreeNode &nd = t.nodes[j];
+        if (nd.count > 0) { items[j] = nd.count; first[j] = nd.index; }
+        else { items[j] = items[nd.index] + items[nd.index + 1]; first[j] = first[nd.index]; }
+    }
+    auto is_leaf = [&](uint32_t j) { return t.nodes[j].count > 0 || (merge_cap && items[j] <= merge_cap); };
+    auto leaf_ref = [&](uint32_t j) { return make_leaf_ref(slot_base + first[j], items[j], ptype, blas); };
+    if (is_leaf(0)) { f.root_ref = leaf_ref(0); return f; }
     struct Todo { uint32_t node, quad, depth; };
     std::vector<Todo> todo{{0u, 0u, 1u}};
     f.quads.emplace_back();
@@ -298,7 +310,7 @@ inline FlatWide flatten_tree_wide(const Tree &t, uint32_t quad_base, uint32_t sl
             int best = -1;
             float area = -1.0f;
             for (uint32_t k = 0; k < nc; k++)
-                if (t.nodes[ch[k]].count == 0 && half_area(t.nodes[ch[k]].box) > area) {
+                if (!is_leaf(ch[k]) && half_area(t.nodes[ch[k]].box) > area) {
                     area = half_area(t.nodes[ch[k]].box);
                     best = (int)k;
                 }
@@ -318,7 +330,7 @@ inline FlatWide flatten_tree_wide(const Tree &t, uint32_t quad_base, uint32_t sl
             q.lo_x[k] = b[0]; q.hi_x[k] = b[1]; q.lo_y[k] = b[2]; q.hi_y[k] = b[3]; q.lo_z[k] = b[4]; q.hi_z[k] = b[5];
             if (k >= nc) {
                 q.ref[k] = REF_EMPTY;
-            } else if (t.nodes[ch[k]].count > 0) {
+            } else if (is_leaf(ch[k])) {
                 q.ref[k] = leaf_ref(ch[k]);
             } else {
                 const uint32_t qi = (uint32_t)f.quads.size();

@@ -124,6 +124,7 @@ struct rt_scene {
     DevBuf<NodePair> blas_pairs;
     DevBuf<NodeQuad> blas_quads;    // option "wide"
     bool wide = true;               // FAST persistent kernel traverses the quad trees (host-built modes)
+    uint32_t wide_merge = 0;        // quad trees: binary subtrees of <= wide_merge items become one leaf (set before build)
     DevBuf<TriHot> tri_hot;
     DevBuf<TriCold> tri_cold;
     DevBuf<SphereHot> sph_hot;
@@ -329,7 +330,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
     s->tlas = s->build_mode == RT_BUILD_SAH ? build_sah_tree(std::move(items), SAH_LEAF_CAP)
                                             : build_median_tree(std::move(items), TLAS_LEAF_CAP, hm::tlas_axis_state(s->build_seed, frame));
     s->tlas_flat = flatten_tree(s->tlas, 0, 0, 0, false);
-    s->tlas_wide = flatten_tree_wide(s->tlas, 0, 0, 0, false);
+    s->tlas_wide = flatten_tree_wide(s->tlas, 0, 0, 0, false, s->wide_merge);
 
     TreeRoot root{};
     std::memcpy(root.box, s->tlas_flat.root_box, sizeof root.box);
@@ -595,7 +596,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             if ((uint64_t)slot_base[in.ptype] + in.pcount >= MAX_LEAF_SLOTS)
                 return fail(RT_ERR_UNSUPPORTED, "too many primitives of one type (2^26 leaf slots)");
             bh.flat = flatten_tree(bh.tree, pair_base, bh.slot_base, in.ptype, true);
-            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, in.ptype, true);
+            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, in.ptype, true, s->wide_merge);
             quad_base += (uint32_t)bh.wide.quads.size();
             s->max_blas_height = std::max(s->max_blas_height, bh.flat.height);
             pair_base += (uint32_t)bh.flat.pairs.size();
@@ -1027,6 +1028,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "wide") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "wide must be 0 or 1");
         s->wide = value == 1;
+    } else if (k == "wide_merge") {
+        if (value != 0 && (value < 2 || value > 4)) return fail(RT_ERR_INVALID_ARGUMENT, "wide_merge must be 0 or 2..4");
+        s->wide_merge = (uint32_t)value;          // BLAS quads: next rt_scene_build; TLAS: next frame
     } else if (k == "split") {
         if (value < 0 || value > 0xFFFF) return fail(RT_ERR_INVALID_ARGUMENT, "split must be k_half | k_quarter << 8");
         s->split = (uint32_t)value;

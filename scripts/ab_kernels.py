@@ -33,19 +33,25 @@ def main():
         opts = dict(x.split("=") for x in kv.split(",") if x)
         variants.append((name, {k: (x if k == "build" else int(x)) for k, x in opts.items()}))
     renderers = {}
+
+    def rkey(opts):      # one renderer per build mode and set of pre-build options ("pre_<key>=v")
+        return (opts.get("build", "compat"),) + tuple(sorted((k, v) for k, v in opts.items() if k.startswith("pre_")))
+
     for _, opts in variants:
-        b = opts.get("build", "compat")
-        if b not in renderers:
-            renderers[b] = Renderer(scenes.config_scene(cfg)).build_acceleration_structure(0, mode=b).configure_camera(
-                cfg.width, cfg.height)
+        key = rkey(opts)
+        if key not in renderers:
+            r = Renderer(scenes.config_scene(cfg))
+            for k, v in key[1:]:
+                r.set_option(k[4:], v)
+            renderers[key] = r.build_acceleration_structure(0, mode=key[0]).configure_camera(cfg.width, cfg.height)
     res = {n: [] for n, _ in variants}
     rays = {}
     for rnd in range(a.rounds + 1):
         for name, opts in variants:
             exact = bool(opts.get("exact", 0))
-            r = renderers[opts.get("build", "compat")]
+            r = renderers[rkey(opts)]
             for k, x in opts.items():
-                if k not in ("exact", "build"):
+                if k not in ("exact", "build") and not k.startswith("pre_"):
                     r.set_option(k, x)
             for f in range(a.frames):
                 _, _, st = r.render(f, exact=exact, want_rgba=False, rgba8_device=fb.data_ptr())

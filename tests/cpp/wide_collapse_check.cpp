@@ -1,5 +1,5 @@
-// Host check of flatten_tree_wide (csrc/bvh_build.hpp): the quad form of a binary tree holds exactly
-// the binary tree's leaves and child boxes.  Built and run by tests/test_wide_collapse.py (g++, CPU).
+// Host check of flatten_tree_wide (csrc/bvh_build.hpp): the quad form of a binary tree covers exactly
+// the binary tree's leaf slots (each once) and its child boxes are binary node boxes.  Built and run by tests/test_wide_collapse.py (g++, CPU).
 #include <cstdio>
 #include <map>
 #include <random>
@@ -12,6 +12,7 @@ using namespace rtamd;
 int main(int argc, char **argv) {
     const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 1000;
     const int sah = argc > 2 ? atoi(argv[2]) : 1;
+    const uint32_t merge = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;
     std::mt19937 rng(n * 7 + sah);
     std::uniform_real_distribution<float> U(-10.0f, 10.0f), S(0.01f, 1.0f);
     std::vector<BuildItem> items(n);
@@ -23,14 +24,14 @@ int main(int argc, char **argv) {
     }
     const Tree t = sah ? build_sah_tree(items, 4) : build_median_tree(items, 4, 12345);
     const FlatTree f2 = flatten_tree(t, 0, 100, 2, true);
-    const FlatWide f4 = flatten_tree_wide(t, 0, 100, 2, true);
+    const FlatWide f4 = flatten_tree_wide(t, 0, 100, 2, true, merge);
     // leaves and boxes reachable from each form
     std::multiset<uint32_t> leaves2, leaves4;
     std::set<std::vector<float>> boxes2, boxes4;
     std::vector<uint32_t> todo{f2.root_ref};
     while (!todo.empty()) {
         const uint32_t r = todo.back(); todo.pop_back();
-        if (r & REF_LEAF) { leaves2.insert(r); continue; }
+        if (r & REF_LEAF) { for (uint32_t k = 0; k < ref_leaf_count(r); k++) leaves2.insert(ref_leaf_start(r) + k); continue; }
         const NodePair &p = f2.pairs[r & REF_INDEX_MASK];
         boxes2.insert(std::vector<float>(p.c0, p.c0 + 6)); boxes2.insert(std::vector<float>(p.c1, p.c1 + 6));
         todo.push_back(p.ref0); todo.push_back(p.ref1);
@@ -39,7 +40,7 @@ int main(int argc, char **argv) {
     todo = {f4.root_ref};
     while (!todo.empty()) {
         const uint32_t r = todo.back(); todo.pop_back();
-        if (r & REF_LEAF) { leaves4.insert(r); continue; }
+        if (r & REF_LEAF) { for (uint32_t k = 0; k < ref_leaf_count(r); k++) leaves4.insert(ref_leaf_start(r) + k); continue; }
         const NodeQuad &q = f4.quads[r & REF_INDEX_MASK];
         quads++;
         int nc = 0;
@@ -58,7 +59,7 @@ int main(int argc, char **argv) {
         children += nc;
         min_children = nc < min_children ? nc : min_children;
     }
-    printf("{\"n\": %u, \"sah\": %d, \"leaves_equal\": %d, \"bad_boxes\": %d, \"quads\": %d, \"pairs\": %zu, "
+    printf("{\"n\": %u, \"sah\": %d, \"slots_equal\": %d, \"bad_boxes\": %d, \"quads\": %d, \"pairs\": %zu, "
            "\"mean_children\": %.3f, \"min_children\": %d, \"height2\": %u, \"height4\": %u}\n",
            n, sah, (int)(leaves2 == leaves4), bad, quads, f2.pairs.size(), quads ? (double)children / quads : 0.0,
            min_children, f2.height, f4.height);
