@@ -45,6 +45,11 @@ def parse():
     p.add_argument("--rebuild", action="store_true", help="--build lbvh: rebuild every BLAS on the GPU each frame (C5)")
     p.add_argument("--kernel", type=int, default=1, help="1 = persistent megakernel, 0 = grid kernel")
     p.add_argument("--threshold", type=int, default=None, help="refill threshold (default: the library's tuned value)")
+    p.add_argument("--overlap", type=int, default=2,
+                   help="L >= 2: consecutive frames cycle L streams / library lanes so frame k+1 fills the CUs "
+                        "frame k's tail leaves idle; 0 or 1: frames are serialised (default 2)")
+    p.add_argument("--shard", default=None, help="R/N: trace only rank R's tiles of an N-rank split on this one GPU "
+                                                 "(per-rank cost study; no gather)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
@@ -122,8 +127,17 @@ def main():
         r.set_option("threshold", args.threshold)
     if args.rebuild:
         r.set_option("rebuild", 1)
+    L = max(1, args.overlap)
+    overlap = L > 1
+    if overlap:
+        r.set_option("overlap", L)
     info = r.info()
     stream = torch.cuda.current_stream().cuda_stream
+    # "overlap": frame k runs on lanes[k % L]; each lane is a self-contained trace -> gather -> assemble chain
+    lanes = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(L - 1)] if overlap else None
+    shard = tuple(int(v) for v in args.shard.split("/")) if args.shard else None
+    if shard and n > 1:
+        raise SystemExit("--shard is a one-GPU study")
 
     tiles = None
     pending = []                 # N > 1: (gather work, gathered buffer) of the previous frame
@@ -132,12 +146,17 @@ def main():
         slab_tiles = max(r.tiles_for_rank(TILE, TILE, k, n) for k in range(n))
         slab_px = slab_tiles * TILE * TILE
         # double-buffered slabs: frame k's gather (RCCL stream) overlaps frame k+1's trace
-        slabs = [torch.zeros(slab_px * 4, dtype=torch.uint8, device="cuda") for _ in range(2)]
+        slabs = [torch.zeros(slab_px * 4, dtype=torch.uint8, device="cuda") for _ in range(max(2, L))]
         gathered = [torch.zeros(n * slab_px * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
-                    for _ in range(2)]
+                    for _ in range(max(2, L))]
         frame_buf = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
+        frame_bufs = [frame_buf] + [torch.zeros_like(frame_buf) if overlap else frame_buf for _ in range(L - 1)] \
+            if rank == 0 else None
     else:
+        if shard:
+            tiles = (TILE, TILE, shard[0], shard[1])
         frame_buf = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda")
+        frame_bufs = [frame_buf] + [torch.zeros_like(frame_buf) if overlap else frame_buf for _ in range(L - 1)]
 
     def finish_gather():
         """Wait (stream-ordered) for the previous frame's gather; rank 0 assembles it into the frame."""
@@ -149,11 +168,22 @@ def main():
 
     def step(frame, sync=True, keep=False):
         """One frame; sync=False pipelines it (host TLAS build of the next frame overlaps the GPU)."""
+        b = frame % L if overlap else frame % 2
         if n == 1:
-            r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=frame_buf.data_ptr(), stream=stream,
-                     sync=sync, keep_counters=keep)
+            st = lanes[b].cuda_stream if overlap else stream
+            r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=frame_bufs[b % len(frame_bufs)].data_ptr(), stream=st,
+                     sync=sync, keep_counters=keep, tiles=tiles)
             return
-        b = frame % 2
+        if overlap:
+            with torch.cuda.stream(lanes[b]):
+                r.render(frame, exact=args.exact, want_rgba=False, tiles=tiles, rgba8_device=slabs[b].data_ptr(),
+                         stream=lanes[b].cuda_stream, sync=sync, keep_counters=keep)
+                work = dist.gather(slabs[b], list(gathered[b].chunk(n)) if rank == 0 else None, dst=0, async_op=True)
+                work.wait()        # stream-ordered: this lane's next frame reuses slabs[b] after the gather
+                if rank == 0:
+                    r.assemble_tiles(gathered[b].data_ptr(), slab_tiles, TILE, TILE, n, frame_bufs[b].data_ptr(),
+                                     lanes[b].cuda_stream)
+            return
         r.render(frame, exact=args.exact, want_rgba=False, tiles=tiles, rgba8_device=slabs[b].data_ptr(), stream=stream,
                  sync=sync, keep_counters=keep)
         work = dist.gather(slabs[b], list(gathered[b].chunk(n)) if rank == 0 else None, dst=0, async_op=True)
@@ -172,7 +202,7 @@ def main():
     r.collect()                                            # drop warm-up timings
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(args.warmup + k, sync=False, keep=k > 0)
+        step(args.warmup + k, sync=False, keep=True)      # counters were zeroed by collect()
     finish_gather()
     torch.cuda.synchronize()
     if n > 1:
@@ -192,6 +222,7 @@ def main():
         elapsed, rays = float(tmax[0]), int(t[1])
 
     # untimed work-counting pass (same frame as the first timed step) for the roofline
+    torch.cuda.synchronize()
     _, _, cst = r.render(args.warmup, exact=args.exact, want_rgba=False, count_work=True,
                          rgba8_device=(slabs[0] if n > 1 else frame_buf).data_ptr(), tiles=tiles, stream=stream)
     if n > 1:
@@ -222,7 +253,9 @@ def main():
                 "width": cfg.width, "height": cfg.height, "spp": cfg.spp, "depth": cfg.depth,
                 "triangles": scene.triangle_count, "instances": len(scene.instances),
                 "blas_node_pairs": info["blas_node_pairs"],
-                "parallelism": f"screen-tiles{n} ({TILE}x{TILE} interleaved, RCCL gather overlapping the next frame)" if n > 1 else "single-gpu",
+                "parallelism": (f"screen-tiles{n} ({TILE}x{TILE} interleaved, RCCL gather overlapping the next frame)"
+                                if n > 1 else (f"single-gpu, shard {args.shard} only" if shard else "single-gpu")),
+                "overlap_lanes": L,
                 "kernel": ("EXACT" if args.exact else "FAST") + (" persistent" if args.kernel else " grid"),
                 "bvh": args.build,
                 "frames": "animated (Main.cu updateInstance), per-frame TLAS rebuild" +

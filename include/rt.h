@@ -285,7 +285,12 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "supertile" : walk each band in supertile x supertile units of 8x8 pixels (default 16; 0 = rows)
  *   "rebuild"   : RT_BUILD_LBVH only: 1 = rebuild every BLAS on the GPU every frame (default 0)
  *   "timeline"  : 1 = record a per-wave timeline of each persistent launch (debug)
- *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal steps (debug)        */
+ *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal steps (debug)
+ *   "overlap"   : L = consecutive rt_render calls cycle through L (2..4) internal lanes (work-queue
+ *                 heads, unit costs, schedule); a launch waits only for the previous launch of its own
+ *                 lane and for its frame block, so a caller that cycles L streams runs frame
+ *                 k+1's launch in the CUs frame k's tail leaves idle.  The caller orders its own output
+ *                 buffers (default 0 = 1 lane: every launch of the scene is serialised)                    */
 rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
 
 /* Debug buffers of the last launch that recorded them (synchronises the scene's stream):

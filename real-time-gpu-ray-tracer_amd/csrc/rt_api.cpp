@@ -139,12 +139,14 @@ struct rt_scene {
     // (the root and the item arrays are used by GPU-built TLASes only)
     size_t frame_block = 0, off_root = 0, off_pairs = 0, off_slots = 0, off_hot = 0, off_cold = 0, off_tbox = 0,
            off_tcent = 0, off_root_wide = 0, off_quads = 0;
-    uint8_t *staging[2] = {nullptr, nullptr};     // pinned host
-    uint8_t *staging_dev[2] = {nullptr, nullptr}; // the same, as device-visible pointers
+    // frame blocks cycle through NLANE buffers, so "overlap" lanes never wait on each other's block
+    static constexpr int NLANE = 4;
+    uint8_t *staging[NLANE] = {};                 // pinned host
+    uint8_t *staging_dev[NLANE] = {};             // the same, as device-visible pointers
     int pending_copy = -1;                        // rt_render: block whose upload the next launch performs
-    uint8_t *frame_dev[2] = {nullptr, nullptr};   // HBM
-    hipEvent_t ev_copied[2] = {nullptr, nullptr}; // upload from staging[b] finished
-    hipEvent_t ev_used[2] = {nullptr, nullptr};   // last kernel reading frame_dev[b] finished
+    uint8_t *frame_dev[NLANE] = {};               // HBM
+    hipEvent_t ev_copied[NLANE] = {};             // upload from staging[b] finished
+    hipEvent_t ev_used[NLANE] = {};               // last kernel reading frame_dev[b] finished
     int active = -1;
 
     hipStream_t stream = nullptr;
@@ -154,7 +156,15 @@ struct rt_scene {
     uint32_t ring_head = 0, ring_pending = 0;
     hipStream_t last_stream = nullptr;
     // persistent megakernel: work-queue head, grid size (#CUs x resident blocks), refill threshold
-    uint32_t *queue = nullptr;
+    // option "overlap" = L lanes: consecutive frames cycle through L lanes (queue heads, unit costs,
+    // schedule), so frame k+1's persistent launch fills the CUs frame k's tail leaves idle when the caller
+    // cycles L streams; with L <= 1 every frame uses lane 0 and launches of one scene are serialised.
+    uint32_t *queue[NLANE] = {};
+    bool overlap = false;
+    uint32_t lanes = 1;
+    uint32_t lane = 0;              // lane of the next rt_render (overlap)
+    int last_lane = 0;              // lane of the last rt_render
+    hipEvent_t ev_lane_done[NLANE] = {};   // last trace launch of each lane finished
     uint32_t cus = 0;
     uint32_t threshold = 16;
     uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4, 5)
@@ -170,9 +180,9 @@ struct rt_scene {
     // option "reorder" (schedule.hip): longest-first claim order from the previous launch's unit costs
     bool reorder = true;
     uint32_t split = 10u | 12u << 8;  // heavy-unit pieces: class level for halves | quarters << 8 (0xFF = never)
-    DevBuf<uint32_t> unit_cost, unit_order;
-    uint32_t sched_sig[7] = {};     // launch layout the recorded costs belong to
-    bool sched_valid = false;
+    DevBuf<uint32_t> unit_cost[NLANE], unit_order[NLANE];
+    uint32_t sched_sig[NLANE][7] = {};  // launch layout the recorded costs belong to
+    bool sched_valid[NLANE] = {};
     DevBuf<uint32_t> costmap;
     size_t costmap_pixels = 0;
     DevBuf<unsigned long long> timeline;
@@ -208,19 +218,23 @@ struct rt_scene {
         if (stream) (void)hipStreamSynchronize(stream);
         blas_pairs.release(); blas_quads.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
         quad_hot.release(); quad_cold.release(); materials.release(); out_rgba.release(); out_rgb.release();
-        timeline.release(); costmap.release(); unit_cost.release(); unit_order.release();
+        timeline.release(); costmap.release();
+        for (int q = 0; q < NLANE; q++) { unit_cost[q].release(); unit_order[q].release(); }
         delete blas_builder; delete tlas_builder;
         raw_tris.release(); raw_sph.release(); raw_quad.release(); blas_roots.release(); inst_blas.release();
         gpu_counts.release();
         if (ev_render_done) (void)hipEventDestroy(ev_render_done);
-        for (int b = 0; b < 2; b++) {
+        for (int b = 0; b < NLANE; b++) {
             if (staging[b]) (void)hipHostFree(staging[b]);
             if (frame_dev[b]) (void)hipFree(frame_dev[b]);
             if (ev_copied[b]) (void)hipEventDestroy(ev_copied[b]);
             if (ev_used[b]) (void)hipEventDestroy(ev_used[b]);
         }
         if (counters) (void)hipFree(counters);
-        if (queue) (void)hipFree(queue);
+        for (int q = 0; q < NLANE; q++) {
+            if (queue[q]) (void)hipFree(queue[q]);
+            if (ev_lane_done[q]) (void)hipEventDestroy(ev_lane_done[q]);
+        }
         if (counters_host) (void)hipHostFree(counters_host);
         for (uint32_t i = 0; i < RING; i++) {
             if (ring_start[i]) (void)hipEventDestroy(ring_start[i]);
@@ -270,6 +284,16 @@ void store_rows(float *dst, const hm::Mat &m) {   // rows 1..3, cols 1..4
 
 rt_status gpu_build_blas(rt_scene *s);
 
+// Wait for every enqueued launch of the scene: its own stream, the last caller stream, both lanes.
+hipError_t drain(rt_scene *s) {
+    hipError_t e = hipSuccess;
+    if (s->last_stream) e = hipStreamSynchronize(s->last_stream);
+    if (e == hipSuccess && s->stream) e = hipStreamSynchronize(s->stream);
+    for (int q = 0; q < rt_scene::NLANE && e == hipSuccess; q++)
+        if (s->ev_lane_done[q]) e = hipEventSynchronize(s->ev_lane_done[q]);
+    return e;
+}
+
 // Host half of one frame: update callback, instance matrices, TLAS rebuild, staging, upload.
 // RT_BUILD_LBVH: the host stages matrices and transformed instance boxes only; the BLAS roots are
 // patched into the instance records and the TLAS is built by kernels on the scene's stream.
@@ -278,7 +302,7 @@ rt_status gpu_build_blas(rt_scene *s);
 // queue cost ~35 us per frame, measured).
 // defer (rt_render): the copy itself is left to the next launch on `upload` (pending_copy).
 rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool defer = false) {
-    const int b = s->active < 0 ? 0 : 1 - s->active;
+    const int b = s->active < 0 ? 0 : (s->active + 1) % rt_scene::NLANE;
     HIP_TRY(hipEventSynchronize(s->ev_copied[b]));     // staging[b] no longer read by a pending copy
     if (s->update) {                                  // Renderer.cu:269
         std::vector<rt_xform> xs(s->inst.size());
@@ -412,6 +436,8 @@ rt_status alloc_buf(DevBuf<T> &buf, size_t n) {
 // leaf-ordered primitive records), on the scene stream, after the last trace that read them.
 rt_status gpu_build_blas(rt_scene *s) {
     if (s->blas_builds && s->ev_render_done) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_render_done, 0));
+    for (int q = 0; q < rt_scene::NLANE; q++)           // "overlap": the other lane's trace may still be running
+        if (s->blas_builds && s->ev_lane_done[q]) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_lane_done[q], 0));
     const RawPrimsGPU raw{s->raw_tris.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
     const PrimOutGPU out{s->tri_hot.p, s->tri_cold.p, s->sph_hot.p, s->sph_cold.p, s->quad_hot.p, s->quad_cold.p};
     HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
@@ -458,7 +484,7 @@ rt_status gpu_setup_blas(rt_scene *s, const std::vector<LbvhSeg> &segs, const ui
     // one-time readback for introspection (rt_scene_get_info)
     uint32_t pairs = 0;
     std::vector<TreeRoot> roots(segs.size());
-    HIP_TRY(hipStreamSynchronize(s->stream));
+    HIP_TRY(drain(s));
     HIP_TRY(hipMemcpy(&pairs, s->gpu_counts.p, sizeof pairs, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(roots.data(), s->blas_roots.p, roots.size() * sizeof(TreeRoot), hipMemcpyDeviceToHost));
     s->blas_pair_count = pairs;
@@ -612,7 +638,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     rt_status st;
     if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
-    s->sched_valid = false;
+    for (bool &v : s->sched_valid) v = false;
     if (mode == RT_BUILD_LBVH) {
         if ((st = gpu_setup_blas(s, segs, slot_base)) != RT_OK) return st;
     } else {
@@ -694,7 +720,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         const std::vector<LbvhSeg> tseg{LbvhSeg{0u, (uint32_t)n, 0u, 0u, 0u, 0u, LBVH_TLAS_LEAF_CAP, 0u}};
         HIP_TRY(s->tlas_builder->init(tseg, s->stream));
     }
-    for (int b = 0; b < 2; b++) {
+    for (int b = 0; b < rt_scene::NLANE; b++) {
         if (s->staging[b]) { (void)hipHostFree(s->staging[b]); s->staging[b] = nullptr; }
         if (s->frame_dev[b]) { (void)hipFree(s->frame_dev[b]); s->frame_dev[b] = nullptr; }
         HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->staging[b]), s->frame_block, hipHostMallocDefault));
@@ -708,9 +734,12 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         if (!s->ring_stop[i]) HIP_TRY(hipEventCreate(&s->ring_stop[i]));
     }
     if (!s->counters) HIP_TRY(hipMalloc(&s->counters, CNT_NUM * sizeof(unsigned long long)));
-    if (!s->queue) {   // band heads, then (option "reorder") band item counts, one 128 B line each
-        HIP_TRY(hipMalloc(&s->queue, 2 * QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t)));
-        HIP_TRY(hipMemset(s->queue, 0, 2 * QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t)));
+    for (int q = 0; q < rt_scene::NLANE; q++) {
+        if (!s->queue[q]) {   // band heads, then (option "reorder") band item counts, one 128 B line each
+            HIP_TRY(hipMalloc(&s->queue[q], 2 * QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t)));
+            HIP_TRY(hipMemset(s->queue[q], 0, 2 * QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t)));
+        }
+        if (!s->ev_lane_done[q]) HIP_TRY(hipEventCreateWithFlags(&s->ev_lane_done[q], hipEventDisableTiming));
     }
     {
         hipDeviceProp_t prop;
@@ -871,34 +900,41 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             s->costmap_pixels = npix;
         }
     }
-    // launches of one scene never overlap, whatever streams callers pass (queue heads, unit costs)
-    HIP_TRY(hipStreamWaitEvent(stream, s->ev_render_done, 0));
+    // Launches of one lane never overlap, whatever streams callers pass (queue heads, unit costs).
+    // Without "overlap" every launch is lane 0.  With it, frames alternate lanes: a launch waits only
+    // for the previous launch of its own lane (and, below, for its frame block), so the caller can run
+    // consecutive frames concurrently on two streams.
+    const int q = s->overlap ? (int)s->lane : 0;
+    s->lane = s->overlap ? (s->lane + 1) % s->lanes : 0u;
+    s->last_lane = q;
+    HIP_TRY(hipStreamWaitEvent(stream, s->overlap ? s->ev_lane_done[q] : s->ev_render_done, 0));
     bool reset_queue = true;
     if (s->use_persistent && s->reorder && s->grab == 64u) {
-        if (s->unit_cost.n < out.units) {
-            s->unit_cost.release();
-            s->unit_order.release();
-            HIP_TRY(hipMalloc(&s->unit_cost.p, out.units * sizeof(uint32_t)));
-            s->unit_cost.n = out.units;
-            HIP_TRY(hipMalloc(&s->unit_order.p, 4 * (size_t)out.units * sizeof(uint32_t)));   // <= 4 items per unit
-            s->unit_order.n = 4 * (size_t)out.units;
-            s->sched_valid = false;
+        DevBuf<uint32_t> &unit_cost = s->unit_cost[q], &unit_order = s->unit_order[q];
+        if (unit_cost.n < out.units) {
+            unit_cost.release();
+            unit_order.release();
+            HIP_TRY(hipMalloc(&unit_cost.p, out.units * sizeof(uint32_t)));
+            unit_cost.n = out.units;
+            HIP_TRY(hipMalloc(&unit_order.p, 4 * (size_t)out.units * sizeof(uint32_t)));   // <= 4 items per unit
+            unit_order.n = 4 * (size_t)out.units;
+            s->sched_valid[q] = false;
         }
         const uint32_t sig[7] = {out.units, out.units_x, out.tile_w, out.tile_h, out.tile_rank, out.tile_count,
                                  out.queue_parts};
-        const bool do_order = s->sched_valid && std::memcmp(sig, s->sched_sig, sizeof sig) == 0;
+        const bool do_order = s->sched_valid[q] && std::memcmp(sig, s->sched_sig[q], sizeof sig) == 0;
         const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
         const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
         const int pc = s->pending_copy;
-        HIP_TRY(launch_schedule(s->unit_cost.p, s->unit_order.p, s->queue, rows, upr, out.queue_parts, do_order,
+        HIP_TRY(launch_schedule(unit_cost.p, unit_order.p, s->queue[q], rows, upr, out.queue_parts, do_order,
                                 s->split & 0xFFu, (s->split >> 8) & 0xFFu, pc >= 0 ? s->frame_dev[pc] : nullptr,
                                 pc >= 0 ? s->staging_dev[pc] : nullptr, pc >= 0 ? s->frame_block : 0, stream));
         if (pc >= 0) HIP_TRY(hipEventRecord(s->ev_copied[pc], stream));
         s->pending_copy = -1;
-        std::memcpy(s->sched_sig, sig, sizeof sig);
-        s->sched_valid = true;
-        out.order = do_order ? s->unit_order.p : nullptr;
-        out.unit_cost = s->unit_cost.p;
+        std::memcpy(s->sched_sig[q], sig, sizeof sig);
+        s->sched_valid[q] = true;
+        out.order = do_order ? unit_order.p : nullptr;
+        out.unit_cost = unit_cost.p;
         reset_queue = false;
     }
     if (s->pending_copy >= 0) {                // no schedule launch carried the upload
@@ -907,18 +943,20 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         s->pending_copy = -1;
     }
     HIP_TRY(hipStreamWaitEvent(stream, s->ev_copied[s->active], 0));
-    if (!(o.flags & RT_RENDER_KEEP_COUNTERS))
+    if (!(o.flags & RT_RENDER_KEEP_COUNTERS)) {
+        if (s->overlap) HIP_TRY(hipStreamWaitEvent(stream, s->ev_render_done, 0));   // the other lane adds to them
         HIP_TRY(hipMemsetAsync(s->counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
+    }
     const uint32_t slot = s->ring_head;
     s->ring_head = (s->ring_head + 1) % rt_scene::RING;
     if (s->ring_pending < rt_scene::RING) s->ring_pending++;
     s->last_stream = stream;
     HIP_TRY(hipEventRecord(s->ring_start[slot], stream));
     if (s->use_persistent)
-        HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, s->counters, s->queue,
+        HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, s->counters, s->queue[q],
                                                        s->cus * persistent_blocks_per_cu_exact(s->variant, false, false), s->threshold,
                                                        s->variant, false, reset_queue, stream)
-                      : launch_render_persistent_fast(g, cam, out, count, s->counters, s->queue,
+                      : launch_render_persistent_fast(g, cam, out, count, s->counters, s->queue[q],
                                                       s->cus * persistent_blocks_per_cu_fast(s->variant, lean, g.wide != 0), s->threshold,
                                                       s->variant, lean, reset_queue, stream));
     else
@@ -927,6 +965,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     HIP_TRY(hipEventRecord(s->ring_stop[slot], stream));
     HIP_TRY(hipEventRecord(s->ev_used[s->active], stream));
     HIP_TRY(hipEventRecord(s->ev_render_done, stream));
+    HIP_TRY(hipEventRecord(s->ev_lane_done[q], stream));
     if (o.flags & RT_RENDER_NO_SYNC) {
         if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; }
         return RT_OK;
@@ -1034,9 +1073,15 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "split") {
         if (value < 0 || value > 0xFFFF) return fail(RT_ERR_INVALID_ARGUMENT, "split must be k_half | k_quarter << 8");
         s->split = (uint32_t)value;
+    } else if (k == "overlap") {
+        if (value < 0 || value > rt_scene::NLANE) return fail(RT_ERR_INVALID_ARGUMENT, "overlap must be 0..4 lanes");
+        HIP_TRY(drain(s));
+        s->lanes = value < 1 ? 1u : (uint32_t)value;
+        s->overlap = s->lanes > 1;
+        s->lane = 0;
     } else if (k == "reorder") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "reorder must be 0 or 1");
-        if (s->reorder != (value == 1)) s->sched_valid = false;
+        if (s->reorder != (value == 1)) for (bool &v : s->sched_valid) v = false;
         s->reorder = value == 1;
     } else {
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown option " + k);
@@ -1057,15 +1102,15 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
         src = s->costmap.p;
         size = s->costmap_pixels * sizeof(uint32_t);
     } else if (k == "unit_cost" || k == "unit_order") {
-        src = k == "unit_cost" ? s->unit_cost.p : s->unit_order.p;
-        size = s->sched_valid ? (size_t)s->sched_sig[0] * (k == "unit_cost" ? 1 : 4) * sizeof(uint32_t) : 0;
+        const int q = s->last_lane;
+        src = k == "unit_cost" ? s->unit_cost[q].p : s->unit_order[q].p;
+        size = s->sched_valid[q] ? (size_t)s->sched_sig[q][0] * (k == "unit_cost" ? 1 : 4) * sizeof(uint32_t) : 0;
     } else {
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown debug buffer " + k);
     }
     if (!src || size == 0) return fail(RT_ERR_STATE, "debug buffer " + k + " not recorded (set the option first)");
     HIP_TRY(hipSetDevice(s->device));
-    if (s->last_stream) HIP_TRY(hipStreamSynchronize(s->last_stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
+    HIP_TRY(drain(s));
     if (capacity) HIP_TRY(hipMemcpy(dst, src, capacity < size ? capacity : size, hipMemcpyDeviceToHost));
     *bytes = size;
     return RT_OK;
@@ -1087,10 +1132,11 @@ rt_status rt_scene_collect(rt_scene *s, rt_stats *acc, float *kernel_ms, uint32_
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
     if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
     HIP_TRY(hipSetDevice(s->device));
-    if (s->last_stream) HIP_TRY(hipStreamSynchronize(s->last_stream));
-    HIP_TRY(hipStreamSynchronize(s->stream));
+    HIP_TRY(drain(s));
     HIP_TRY(hipMemcpy(s->counters_host, s->counters, CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     if (acc) fill_stats(acc, s->counters_host);
+    // collected: the next KEEP_COUNTERS frames accumulate from zero
+    HIP_TRY(hipMemset(s->counters, 0, CNT_NUM * sizeof(unsigned long long)));
     const uint32_t n = s->ring_pending;
     uint32_t written = 0;
     for (uint32_t k = 0; k < n; k++) {
@@ -1115,7 +1161,7 @@ rt_status rt_scene_update_triangles(rt_scene *s, size_t first, size_t count, con
     for (size_t k = 0; k < count; k++) material_slot(s, tris[k].material_type, tris[k].material_index, ok);
     if (!ok) return fail(RT_ERR_INVALID_ARGUMENT, "triangle references a material out of range");
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(hipStreamSynchronize(s->stream));        // a pending BLAS build may still read the raw array
+    HIP_TRY(drain(s));        // a pending BLAS build may still read the raw array
     std::memcpy(s->tris.data() + first, tris, count * sizeof(rt_triangle));
     HIP_TRY(hipMemcpy(s->raw_tris.p + first, tris, count * sizeof(rt_triangle), hipMemcpyHostToDevice));
     // instance boxes derived from the triangles (RenderPin.cu:124-139); VTK-style bounds stay as given
@@ -1167,7 +1213,7 @@ rt_status rt_scene_update_instances(rt_scene *s, size_t first, size_t count, con
 rt_status rt_synchronize(rt_scene *s) {
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
     HIP_TRY(hipSetDevice(s->device));
-    if (s->stream) HIP_TRY(hipStreamSynchronize(s->stream));
+    HIP_TRY(drain(s));
     if (s->ev_render_done) HIP_TRY(hipEventSynchronize(s->ev_render_done));
     return RT_OK;
 }

@@ -103,6 +103,47 @@ def _pipelined_worker(rank, world, port, result_path):
     dist.destroy_process_group()
 
 
+def _lanes_worker(rank, world, port, result_path, nl=3):
+    """bench.py's N > 1 loop with option "overlap" = nl lanes: frame f runs on lane f % nl, whose
+    chain is trace into slabs[lane] -> gather into gathered[lane] (waited in lane order) -> assemble
+    into frame_bufs[lane] on rank 0; a lane's buffers are reused only by its next frame."""
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "real-time-gpu-ray-tracer_amd")]
+    from oracle.oracle import OracleScene
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    o = OracleScene(scenes.demo_with_particles(4), build_seed=2)
+    o.camera(W, H, ray_trace_depth=1)
+    st = tiles.slab_tiles(W, H, TW, TH, world)
+    slabs = [torch.zeros(st * TW * TH, 4, dtype=torch.uint8) for _ in range(nl)]
+    gathered = [[torch.zeros_like(slabs[0]) for _ in range(world)] if rank == 0 else None for _ in range(nl)]
+    frame_bufs = [np.zeros((H, W, 4), np.uint8) for _ in range(nl)]
+    out = []
+    for f in range(2 * nl):
+        b = f % nl
+        o.update(f)
+        slabs[b].copy_(torch.from_numpy(_render_slab(o, rank, world)))
+        dist.gather(slabs[b], gathered[b], dst=0, async_op=True).wait()
+        if rank == 0:
+            frame_bufs[b][:] = tiles.assemble(torch.stack(gathered[b]).numpy(), W, H, TW, TH, world)
+            if f >= nl:       # lane b's previous frame has been replaced by frame f
+                out.append(np.stack([frame_bufs[b].copy(), o.render(threads=2, want_rgb=False)[1]]))
+    if rank == 0:
+        np.save(result_path, np.stack(out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_overlap_lanes_gather_gloo(tmp_path):
+    out = str(tmp_path / "res.npy")
+    mp.spawn(_lanes_worker, args=(2, _free_port(), out), nprocs=2, join=True)
+    res = np.load(out)
+    assert res.shape[0] == 3
+    for frame, full in res:
+        assert np.array_equal(frame, full)
+
+
 def test_pipelined_gather_gloo(tmp_path):
     out = str(tmp_path / "res.npy")
     mp.spawn(_pipelined_worker, args=(2, _free_port(), out), nprocs=2, join=True)
