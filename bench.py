@@ -45,11 +45,13 @@ def parse():
     p.add_argument("--rebuild", action="store_true", help="--build lbvh: rebuild every BLAS on the GPU each frame (C5)")
     p.add_argument("--kernel", type=int, default=1, help="1 = persistent megakernel, 0 = grid kernel")
     p.add_argument("--threshold", type=int, default=None, help="refill threshold (default: the library's tuned value)")
-    p.add_argument("--overlap", type=int, default=2,
+    p.add_argument("--overlap", type=int, default=None,
                    help="L >= 2: consecutive frames cycle L streams / library lanes so frame k+1 fills the CUs "
-                        "frame k's tail leaves idle; 0 or 1: frames are serialised (default 2)")
+                        "frame k's tail leaves idle; 0 or 1: frames are serialised (default 2; 1 with --build lbvh, "
+                        "measured slower overlapped: DESIGN.md 4)")
     p.add_argument("--shard", default=None, help="R/N: trace only rank R's tiles of an N-rank split on this one GPU "
                                                  "(per-rank cost study; no gather)")
+    p.add_argument("--tile", type=int, default=64, help="N > 1 screen-tile edge in pixels (multiple of 8)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
@@ -102,6 +104,10 @@ def load_traffic(kname):
 
 def main():
     args = parse()
+    global TILE
+    TILE = args.tile
+    if TILE % 8 or TILE <= 0:
+        raise SystemExit("--tile must be a positive multiple of 8")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -127,7 +133,7 @@ def main():
         r.set_option("threshold", args.threshold)
     if args.rebuild:
         r.set_option("rebuild", 1)
-    L = max(1, args.overlap)
+    L = max(1, args.overlap if args.overlap is not None else (1 if args.build == "lbvh" else 2))
     overlap = L > 1
     if overlap:
         r.set_option("overlap", L)
@@ -256,6 +262,7 @@ def main():
                 "parallelism": (f"screen-tiles{n} ({TILE}x{TILE} interleaved, RCCL gather overlapping the next frame)"
                                 if n > 1 else (f"single-gpu, shard {args.shard} only" if shard else "single-gpu")),
                 "overlap_lanes": L,
+                "tile": TILE,
                 "kernel": ("EXACT" if args.exact else "FAST") + (" persistent" if args.kernel else " grid"),
                 "bvh": args.build,
                 "frames": "animated (Main.cu updateInstance), per-frame TLAS rebuild" +

@@ -380,8 +380,9 @@ def test_split_claims_are_byte_identical(gpu_lib, split):
         assert np.array_equal(r.render(f)[0], ref[f]), (split, f)
 
 
-@pytest.mark.parametrize("tiles,nl", [(None, 2), ((64, 64, 1, 3), 2), (None, 3), ((64, 64, 0, 2), 4)])
-def test_overlap_lanes_byte_identical(gpu_lib, tiles, nl):
+@pytest.mark.parametrize("tiles,nl,mode", [(None, 2, "sah"), ((64, 64, 1, 3), 2, "sah"), (None, 3, "sah"),
+                                           ((64, 64, 0, 2), 4, "sah"), (None, 2, "lbvh"), (None, 3, "lbvh-rebuild")])
+def test_overlap_lanes_byte_identical(gpu_lib, tiles, nl, mode):
     """Option "overlap": frames alternate two library lanes on two caller streams and may run
     concurrently (frame k+1 fills frame k's tail).  Every frame is byte-identical to the serial
     render, the accumulated counters equal the sum of the serial frames', and one kernel time per
@@ -389,7 +390,9 @@ def test_overlap_lanes_byte_identical(gpu_lib, tiles, nl):
     import torch
     s = scenes.demo_with_particles(12)
     W, H, F = 480, 272, 6
-    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(W, H, ray_trace_depth=2)
+    r = Renderer(s).build_acceleration_structure(0, mode=mode.split("-")[0]).configure_camera(W, H, ray_trace_depth=2)
+    if mode.endswith("rebuild"):
+        r.set_option("rebuild", 1)            # every BLAS rebuilt each frame: waits for every lane's trace
     npix = (r.tiles_for_rank(*tiles) * tiles[0] * tiles[1]) if tiles else W * H
     # zeroed device outputs: a tile slab's pixels outside the frame are never written
     zero = [torch.zeros(npix * 4, dtype=torch.uint8, device="cuda") for _ in range(F)]
