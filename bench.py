@@ -47,8 +47,8 @@ def parse():
     p.add_argument("--threshold", type=int, default=None, help="refill threshold (default: the library's tuned value)")
     p.add_argument("--overlap", type=int, default=None,
                    help="L >= 2: consecutive frames cycle L streams / library lanes so frame k+1 fills the CUs "
-                        "frame k's tail leaves idle; 0 or 1: frames are serialised (default 2; 1 with --build lbvh, "
-                        "measured slower overlapped: DESIGN.md 4)")
+                        "frame k's tail leaves idle; 0 or 1: frames are serialised (default 2 at N=1, 3 at N>1; "
+                        "1 with --build lbvh, measured slower overlapped: DESIGN.md 4)")
     p.add_argument("--shard", default=None, help="R/N: trace only rank R's tiles of an N-rank split on this one GPU "
                                                  "(per-rank cost study; no gather)")
     p.add_argument("--tile", type=int, default=64, help="N > 1 screen-tile edge in pixels (multiple of 8)")
@@ -133,7 +133,8 @@ def main():
         r.set_option("threshold", args.threshold)
     if args.rebuild:
         r.set_option("rebuild", 1)
-    L = max(1, args.overlap if args.overlap is not None else (1 if args.build == "lbvh" else 2))
+    # measured: 2 lanes best at N=1, 3 lanes for a rank's 1/N share, 1 with GPU-built trees
+    L = max(1, args.overlap if args.overlap is not None else (1 if args.build == "lbvh" else (3 if n > 1 else 2)))
     overlap = L > 1
     if overlap:
         r.set_option("overlap", L)
@@ -263,6 +264,7 @@ def main():
                                 if n > 1 else (f"single-gpu, shard {args.shard} only" if shard else "single-gpu")),
                 "overlap_lanes": L,
                 "tile": TILE,
+                "threshold": args.threshold if args.threshold is not None else 32,
                 "kernel": ("EXACT" if args.exact else "FAST") + (" persistent" if args.kernel else " grid"),
                 "bvh": args.build,
                 "frames": "animated (Main.cu updateInstance), per-frame TLAS rebuild" +

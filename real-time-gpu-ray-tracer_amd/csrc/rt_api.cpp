@@ -161,12 +161,13 @@ struct rt_scene {
     // cycles L streams; with L <= 1 every frame uses lane 0 and launches of one scene are serialised.
     uint32_t *queue[NLANE] = {};
     bool overlap = false;
+    bool lbvh_priority = true;      // env RTAMD_SCENE_PRIORITY=0: scene stream at normal priority (A/B)
     uint32_t lanes = 1;
     uint32_t lane = 0;              // lane of the next rt_render (overlap)
     int last_lane = 0;              // lane of the last rt_render
     hipEvent_t ev_lane_done[NLANE] = {};   // last trace launch of each lane finished
     uint32_t cus = 0;
-    uint32_t threshold = 16;
+    uint32_t threshold = 32;          // measured with "reorder" + "wide" + 2 overlap lanes: 32-48 beat 16
     uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4, 5)
     bool use_persistent = true;
     uint32_t queue_parts = 8;       // one band per XCD (measured with "reorder": 8 beat 4, 2 and 1 on C2)
@@ -529,6 +530,7 @@ rt_status rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     auto *s = new (std::nothrow) rt_scene();
     if (!s) return fail(RT_ERR_OUT_OF_MEMORY, "host allocation failed");
     s->device = device;
+    if (const char *p = std::getenv("RTAMD_SCENE_PRIORITY")) s->lbvh_priority = std::string(p) != "0";
     s->spheres.assign(d->spheres, d->spheres + d->sphere_count);
     s->quads.assign(d->parallelograms, d->parallelograms + d->parallelogram_count);
     s->tris.assign(d->triangles, d->triangles + d->triangle_count);
@@ -636,7 +638,13 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     for (const auto &r : s->roughs) { mats.push_back(r.albedo.x); mats.push_back(r.albedo.y); mats.push_back(r.albedo.z); mats.push_back(0.0f); }
     for (const auto &m : s->metals) { mats.push_back(m.albedo.x); mats.push_back(m.albedo.y); mats.push_back(m.albedo.z); mats.push_back(m.fuzz); }
     rt_status st;
-    if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    if (!s->stream) {
+        // highest priority: the GPU TLAS build of frame k+1 (a chain of small dependent kernels) is
+        // dispatched ahead of queued trace workgroups when "overlap" keeps every CU slot busy
+        int lo = 0, hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, s->lbvh_priority ? hi : lo));
+    }
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
     for (bool &v : s->sched_valid) v = false;
     if (mode == RT_BUILD_LBVH) {
