@@ -228,6 +228,17 @@ def main():
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed, rays = float(tmax[0]), int(t[1])
 
+    # SURVEY 8d latency definition: wall time from the call to the framebuffer being ready (rank 0: the
+    # assembled frame), synchronous frames, median of 20 after the timed region (untimed for `value`)
+    lat = []
+    for k in range(20):
+        t1 = time.perf_counter()
+        step(args.warmup + args.steps + k, sync=True)
+        torch.cuda.synchronize()
+        lat.append((time.perf_counter() - t1) * 1e3)
+    if n > 1:
+        dist.barrier()
+
     # untimed work-counting pass (same frame as the first timed step) for the roofline
     torch.cuda.synchronize()
     _, _, cst = r.render(args.warmup, exact=args.exact, want_rgba=False, count_work=True,
@@ -272,6 +283,7 @@ def main():
                           (", per-frame GPU BLAS rebuild" if args.rebuild else "") + ", pipelined",
             },
             "rays_per_frame": round(rays / args.steps, 1),
+            "frame_latency_ms_median": round(float(np.median(lat)), 4),
             "kernel_ms": round(avg_kernel_ms, 4),
             "roofline": {
                 "bound": "hbm",

@@ -161,7 +161,6 @@ struct rt_scene {
     // cycles L streams; with L <= 1 every frame uses lane 0 and launches of one scene are serialised.
     uint32_t *queue[NLANE] = {};
     bool overlap = false;
-    bool lbvh_priority = true;      // env RTAMD_SCENE_PRIORITY=0: scene stream at normal priority (A/B)
     uint32_t lanes = 1;
     uint32_t lane = 0;              // lane of the next rt_render (overlap)
     int last_lane = 0;              // lane of the last rt_render
@@ -530,7 +529,6 @@ rt_status rt_scene_create(const rt_scene_desc *d, int device, rt_scene **out) {
     auto *s = new (std::nothrow) rt_scene();
     if (!s) return fail(RT_ERR_OUT_OF_MEMORY, "host allocation failed");
     s->device = device;
-    if (const char *p = std::getenv("RTAMD_SCENE_PRIORITY")) s->lbvh_priority = std::string(p) != "0";
     s->spheres.assign(d->spheres, d->spheres + d->sphere_count);
     s->quads.assign(d->parallelograms, d->parallelograms + d->parallelogram_count);
     s->tris.assign(d->triangles, d->triangles + d->triangle_count);
@@ -638,13 +636,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     for (const auto &r : s->roughs) { mats.push_back(r.albedo.x); mats.push_back(r.albedo.y); mats.push_back(r.albedo.z); mats.push_back(0.0f); }
     for (const auto &m : s->metals) { mats.push_back(m.albedo.x); mats.push_back(m.albedo.y); mats.push_back(m.albedo.z); mats.push_back(m.fuzz); }
     rt_status st;
-    if (!s->stream) {
-        // highest priority: the GPU TLAS build of frame k+1 (a chain of small dependent kernels) is
-        // dispatched ahead of queued trace workgroups when "overlap" keeps every CU slot busy
-        int lo = 0, hi = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIP_TRY(hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, s->lbvh_priority ? hi : lo));
-    }
+    if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
     for (bool &v : s->sched_valid) v = false;
     if (mode == RT_BUILD_LBVH) {
