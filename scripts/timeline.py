@@ -60,7 +60,9 @@ def main():
     ap.add_argument("--threshold", type=int, default=8)
     ap.add_argument("--out", default="gpurun_out/timeline.npz")
     ap.add_argument("--opt", action="append", default=[], help="extra scene option key=value")
+    ap.add_argument("--shard", default=None, help="R/N: time rank R's 64x64-tile share of an N-rank split")
     a = ap.parse_args()
+    tiles = (64, 64) + tuple(int(v) for v in a.shard.split("/")) if a.shard else None
     import torch
     from rtamd import Renderer, scenes
     torch.cuda.set_device(0)
@@ -77,15 +79,18 @@ def main():
         r.set_option("queue_parts", parts)
         r.set_option("timeline", 0)
         for f in range(5):
-            r.render(f, want_rgba=False, rgba8_device=fb.data_ptr())
+            r.render(f, want_rgba=False, rgba8_device=fb.data_ptr(), tiles=tiles)
         r.set_option("timeline", 1)
-        _, _, stt = r.render(5, want_rgba=False, rgba8_device=fb.data_ptr())
+        _, _, stt = r.render(5, want_rgba=False, rgba8_device=fb.data_ptr(), tiles=tiles)
         tl = r.timeline()
         saved[f"parts{parts}"] = tl
         s = summarize(tl, f"parts={parts}")
         s["kernel_ms_event"] = round(stt["kernel_ms"], 4)
         print(json.dumps(s), flush=True)
     r.set_option("timeline", 0)
+    if tiles:
+        np.savez(a.out, **saved)
+        return
     # per-pixel traversal rounds (COUNT_WORK launch)
     r.set_option("costmap", 1)
     r.render(6, count_work=True, want_rgba=False, rgba8_device=fb.data_ptr())
