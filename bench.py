@@ -51,6 +51,7 @@ def parse():
                         "1 with --build lbvh, measured slower overlapped: DESIGN.md 4)")
     p.add_argument("--shard", default=None, help="R/N: trace only rank R's tiles of an N-rank split on this one GPU "
                                                  "(per-rank cost study; no gather)")
+    p.add_argument("--opt", action="append", default=[], help="extra rt_scene_set_option key=value (A/B studies)")
     p.add_argument("--tile", type=int, default=64, help="N > 1 screen-tile edge in pixels (multiple of 8)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -133,6 +134,9 @@ def main():
         r.set_option("threshold", args.threshold)
     if args.rebuild:
         r.set_option("rebuild", 1)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        r.set_option(k, int(v, 0))
     # measured: 2 lanes best at N=1, 3 lanes for a rank's 1/N share, 1 with GPU-built trees
     L = max(1, args.overlap if args.overlap is not None else (1 if args.build == "lbvh" else (3 if n > 1 else 2)))
     overlap = L > 1
@@ -276,6 +280,7 @@ def main():
                 "overlap_lanes": L,
                 "tile": TILE,
                 "threshold": args.threshold if args.threshold is not None else 32,
+                "options": args.opt,
                 "kernel": ("EXACT" if args.exact else "FAST") + (" persistent" if args.kernel else " grid"),
                 "bvh": args.build,
                 "frames": "animated (Main.cu updateInstance), per-frame TLAS rebuild" +
