@@ -36,8 +36,8 @@ B_PAIR, B_TRI, B_SPH, B_QUAD, B_INST, B_HIT, B_PIXEL = 64, 48, 16, 80, 80, 208, 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="C2")
     p.add_argument("--exact", action="store_true", help="time the EXACT (parity) kernel instead of FAST")
     p.add_argument("--build", default="sah", choices=("sah", "compat", "lbvh"),
@@ -105,6 +105,8 @@ def load_traffic(kname):
 
 def main():
     args = parse()
+    if not 1 <= args.steps <= 256:
+        raise SystemExit("--steps must be in 1..256 (the library's per-frame kernel-time ring)")
     global TILE
     TILE = args.tile
     if TILE % 8 or TILE <= 0:

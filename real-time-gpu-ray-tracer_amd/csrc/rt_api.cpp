@@ -216,6 +216,9 @@ struct rt_scene {
     ~rt_scene() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
+        for (int q = 0; q < NLANE; q++)          // launches still running on caller streams
+            if (ev_lane_done[q]) (void)hipEventSynchronize(ev_lane_done[q]);
+        if (ev_render_done) (void)hipEventSynchronize(ev_render_done);
         blas_pairs.release(); blas_quads.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
         quad_hot.release(); quad_cold.release(); materials.release(); out_rgba.release(); out_rgb.release();
         timeline.release(); costmap.release();
@@ -284,7 +287,7 @@ void store_rows(float *dst, const hm::Mat &m) {   // rows 1..3, cols 1..4
 
 rt_status gpu_build_blas(rt_scene *s);
 
-// Wait for every enqueued launch of the scene: its own stream, the last caller stream, both lanes.
+// Wait for every enqueued launch of the scene: its own stream, the last caller stream, every lane.
 hipError_t drain(rt_scene *s) {
     hipError_t e = hipSuccess;
     if (s->last_stream) e = hipStreamSynchronize(s->last_stream);
