@@ -21,7 +21,7 @@ STEPS=${STEPS:-smoke,tests,bench,prof}
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py
 if [[ $STEPS == *prof* ]]; then
   export TMPDIR=/tmp
-  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline
+  run prof 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --no-cpu-baseline
 fi
 if [[ $STEPS == *pmc* ]]; then
   KSUB=${KSUB:-"dev_fast::render_persistent_kernel<false"}
