@@ -124,6 +124,9 @@ struct SceneGPU {
     const NodeQuad *tlas_quads;
     const TreeRoot *tlas_root_wide;
     uint32_t wide;                  // 1: the FAST persistent kernel traverses the quad trees
+    uint32_t inst_by_slot;          // 1 (host-built TLAS): inst_hot / inst_cold are stored in TLAS leaf-slot
+                                    // order, so entering an instance needs no tlas_slots load (the slot
+                                    // is the record index; tlas_slots maps it back to the instance id)
     uint32_t instance_count;
     uint32_t rough_count;           // material slot of metal m = rough_count + m
 };

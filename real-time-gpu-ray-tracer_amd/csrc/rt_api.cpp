@@ -161,6 +161,8 @@ struct rt_scene {
     // cycles L streams; with L <= 1 every frame uses lane 0 and launches of one scene are serialised.
     uint32_t *queue[NLANE] = {};
     bool overlap = false;
+    bool inst_by_slot = true;       // option "inst_by_slot": host-built TLAS stages instance records in slot order
+    bool block_by_slot[NLANE] = {};  // per frame block: staged in slot order
     uint32_t lanes = 1;
     uint32_t lane = 0;              // lane of the next rt_render (overlap)
     int last_lane = 0;              // lane of the last rt_render
@@ -370,15 +372,18 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
     std::memcpy(st + s->off_quads, s->tlas_wide.quads.data(), s->tlas_wide.quads.size() * sizeof(NodeQuad));
     std::memcpy(st + s->off_pairs, s->tlas_flat.pairs.data(), s->tlas_flat.pairs.size() * sizeof(NodePair));
     std::memcpy(st + s->off_slots, s->tlas.refs.data(), s->tlas.refs.size() * sizeof(uint32_t));
-    for (size_t i = 0; i < s->inst.size(); i++) {
-        const InstState &in = s->inst[i];
+    // instance records in TLAS leaf-slot order (SceneGPU::inst_by_slot): record j = the instance in slot j
+    const size_t nrec = s->inst_by_slot ? s->tlas.refs.size() : s->inst.size();
+    s->block_by_slot[b] = s->inst_by_slot;
+    for (size_t j = 0; j < nrec; j++) {
+        const InstState &in = s->inst[s->inst_by_slot ? s->tlas.refs[j] : j];
         const BlasHost &bl = s->blas[in.blas];
-        store_rows(hot[i].inv, in.inv);
-        std::memcpy(hot[i].root_box, bl.flat.root_box, sizeof hot[i].root_box);
-        hot[i].root_ref = bl.flat.root_ref;
-        hot[i].root_ref_wide = bl.wide.root_ref;
-        store_rows(cold[i].fwd, in.fwd);
-        store_rows(cold[i].nrm, in.nrm);
+        store_rows(hot[j].inv, in.inv);
+        std::memcpy(hot[j].root_box, bl.flat.root_box, sizeof hot[j].root_box);
+        hot[j].root_ref = bl.flat.root_ref;
+        hot[j].root_ref_wide = bl.wide.root_ref;
+        store_rows(cold[j].fwd, in.fwd);
+        store_rows(cold[j].nrm, in.nrm);
     }
     // Measured: the upload on a dedicated copy stream (the reference's copyStream, Renderer.cu:281-303)
     // went through an SDMA engine whose first use stalled a frame by ~7.6 ms; enqueued on the trace's
@@ -408,6 +413,7 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.tlas_slots = reinterpret_cast<const uint32_t *>(s->frame_dev[b] + s->off_slots);
     g.inst_hot = reinterpret_cast<const InstHot *>(s->frame_dev[b] + s->off_hot);
     g.inst_cold = reinterpret_cast<const InstCold *>(s->frame_dev[b] + s->off_cold);
+    g.inst_by_slot = s->block_by_slot[b] ? 1u : 0u;   // how frame block b's instance records were staged
     g.tri_hot = s->tri_hot.p; g.tri_cold = s->tri_cold.p;
     g.sph_hot = s->sph_hot.p; g.sph_cold = s->sph_cold.p;
     g.quad_hot = s->quad_hot.p; g.quad_cold = s->quad_cold.p;
@@ -1076,6 +1082,10 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "split") {
         if (value < 0 || value > 0xFFFF) return fail(RT_ERR_INVALID_ARGUMENT, "split must be k_half | k_quarter << 8");
         s->split = (uint32_t)value;
+    } else if (k == "inst_by_slot") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "inst_by_slot must be 0 or 1");
+        HIP_TRY(drain(s));
+        s->inst_by_slot = value == 1;            // takes effect with the next frame's staging
     } else if (k == "overlap") {
         if (value < 0 || value > rt_scene::NLANE) return fail(RT_ERR_INVALID_ARGUMENT, "overlap must be 0..4 lanes");
         HIP_TRY(drain(s));

@@ -408,7 +408,7 @@ __device__ __forceinline__ void trav_step(Trav &T, const SceneGPU &sc, SEnt *spi
         // TLAS leaf: its instances in order (TLAS.cu:157-173)
         const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur);
         if (count > 1) stack_push(T.stk, spill, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
-        T.cur_inst = sc.tlas_slots[start];
+        T.cur_inst = sc.inst_by_slot ? start : sc.tlas_slots[start];
         const InstHot &I = sc.inst_hot[T.cur_inst];
         if (COUNT) cnt.inst++;
         // Instance::hit: ray into local space, d' not renormalised (Instance.cu:26-27)
@@ -587,7 +587,7 @@ __device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEn
         const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf);
         if (T.cur != REF_NONE) stack_push(T.stk, spill, T.cur, T.curT, cnt);
         if (count > 1) stack_push(T.stk, spill, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
-        T.cur_inst = sc.tlas_slots[start];
+        T.cur_inst = sc.inst_by_slot ? start : sc.tlas_slots[start];
         const InstHot &I = sc.inst_hot[T.cur_inst];
         if (COUNT) cnt.inst++;
         T.lr.o = xf_point(I.inv, T.wr.o);                      // Instance.cu:26-27
@@ -754,7 +754,7 @@ __device__ __forceinline__ void lean_leaf_phase(Trav &T, const SceneGPU &sc, Lan
         const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf);
         lean_push(T, T.cur, T.curT, !ref_is_marker(T.cur), cnt);
         lean_push(T, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), count > 1, cnt);
-        T.cur_inst = sc.tlas_slots[start];
+        T.cur_inst = sc.inst_by_slot ? start : sc.tlas_slots[start];
         const InstHot &I = sc.inst_hot[T.cur_inst];
         if (COUNT) cnt.inst++;
         T.lr.o = xf_point(I.inv, T.wr.o);                      // Instance.cu:26-27
@@ -1331,7 +1331,7 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const fl
     rt_hit r;
     if (trace<false>(sc, o, d, h, T, spill, cnt)) {
         const Surface s = finalize(sc, o, d, h);
-        r.t = h.t; r.instance = h.inst; r.primitive_type = h.ptype; r.primitive_index = s.orig;
+        r.t = h.t; r.instance = sc.inst_by_slot ? sc.tlas_slots[h.inst] : h.inst; r.primitive_type = h.ptype; r.primitive_index = s.orig;
         r.point.x = s.p.x; r.point.y = s.p.y; r.point.z = s.p.z;
         r.normal.x = s.n.x; r.normal.y = s.n.y; r.normal.z = s.n.z;
         const bool metal = (s.material & MAT_METAL_BIT) != 0;
