@@ -335,7 +335,8 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         }
         uint8_t *fd = s->frame_dev[b];
         HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_used[b], 0));
-        HIP_TRY(hipMemcpyAsync(fd, st, s->frame_block, hipMemcpyHostToDevice, s->stream));
+        // a blit kernel reading the pinned staging block, not an SDMA copy (see the host-built path below)
+        HIP_TRY(launch_frame_copy(fd, s->staging_dev[b], s->frame_block, s->stream));
         if (s->rebuild_blas || s->blas_dirty) {
             const rt_status bs = gpu_build_blas(s);
             if (bs != RT_OK) return bs;
