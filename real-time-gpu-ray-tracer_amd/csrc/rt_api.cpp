@@ -161,6 +161,7 @@ struct rt_scene {
     // cycles L streams; with L <= 1 every frame uses lane 0 and launches of one scene are serialised.
     uint32_t *queue[NLANE] = {};
     bool overlap = false;
+    uint32_t tlas_leaf = 1;   // option "tlas_leaf": RT_BUILD_SAH per-frame TLAS leaf size (1..4; 1 measured best)
     bool inst_by_slot = true;       // option "inst_by_slot": host-built TLAS stages instance records in slot order
     bool block_by_slot[NLANE] = {};  // per frame block: staged in slot order
     uint32_t lanes = 1;
@@ -357,7 +358,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
     // TLAS::constructTLAS over transformed instance boxes (Renderer.cu:275, TLAS.cu:4-129)
     std::vector<BuildItem> items(s->inst.size());
     for (size_t i = 0; i < items.size(); i++) items[i] = {s->inst[i].tbox, s->inst[i].tcentroid, (uint32_t)i};
-    s->tlas = s->build_mode == RT_BUILD_SAH ? build_sah_tree(std::move(items), SAH_LEAF_CAP)
+    s->tlas = s->build_mode == RT_BUILD_SAH ? build_sah_tree(std::move(items), s->tlas_leaf)
                                             : build_median_tree(std::move(items), TLAS_LEAF_CAP, hm::tlas_axis_state(s->build_seed, frame));
     s->tlas_flat = flatten_tree(s->tlas, 0, 0, 0, false);
     s->tlas_wide = flatten_tree_wide(s->tlas, 0, 0, 0, false, s->wide_merge);
@@ -1083,6 +1084,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "split") {
         if (value < 0 || value > 0xFFFF) return fail(RT_ERR_INVALID_ARGUMENT, "split must be k_half | k_quarter << 8");
         s->split = (uint32_t)value;
+    } else if (k == "tlas_leaf") {
+        if (value < 1 || value > (int64_t)SAH_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_leaf must be in 1..4");
+        s->tlas_leaf = (uint32_t)value;          // next frame's TLAS
     } else if (k == "inst_by_slot") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "inst_by_slot must be 0 or 1");
         HIP_TRY(drain(s));
