@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--shard", default=None, help="R/N: trace only rank R's tiles of an N-rank split on this one GPU "
                                                  "(per-rank cost study; no gather)")
     p.add_argument("--opt", action="append", default=[], help="extra rt_scene_set_option key=value (A/B studies)")
+    p.add_argument("--pre-opt", action="append", default=[], help="rt_scene_set_option key=value before the build")
     p.add_argument("--tile", type=int, default=64, help="N > 1 screen-tile edge in pixels (multiple of 8)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -128,8 +129,11 @@ def main():
 
     cfg = scenes.CONFIGS[args.config]
     scene = scenes.config_scene(cfg)
-    r = Renderer(scene, device=local_rank).build_acceleration_structure(0, mode=args.build).configure_camera(
-        cfg.width, cfg.height)
+    r = Renderer(scene, device=local_rank)
+    for kv in args.pre_opt:
+        k, v = kv.split("=")
+        r.set_option(k, int(v, 0))
+    r.build_acceleration_structure(0, mode=args.build).configure_camera(cfg.width, cfg.height)
     r.set_option("kernel", args.kernel)
     if args.threshold is not None:
         r.set_option("threshold", args.threshold)
@@ -281,7 +285,7 @@ def main():
                 "overlap_lanes": L,
                 "tile": TILE,
                 "threshold": args.threshold if args.threshold is not None else 32,
-                "options": args.opt,
+                "options": args.pre_opt + args.opt,
                 "kernel": ("EXACT" if args.exact else "FAST") + (" persistent" if args.kernel else " grid"),
                 "bvh": args.build,
                 "frames": "animated (Main.cu updateInstance), per-frame TLAS rebuild" +

@@ -287,6 +287,7 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "timeline"  : 1 = record a per-wave timeline of each persistent launch (debug)
  *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal steps (debug)
  *   "tlas_leaf" : RT_BUILD_SAH: instances per leaf of the per-frame TLAS (1..4, default 1)
+ *   "blas_leaf" : RT_BUILD_SAH: primitives per BLAS leaf (1..4, default 4; set before rt_scene_build)
  *   "inst_by_slot": 1 = host-built TLAS: stage the per-frame instance records in TLAS leaf-slot order
  *                 (default 1; 0 = instance order, for A/B — results are identical)
  *   "overlap"   : L = consecutive rt_render calls cycle through L (2..4) internal lanes (work-queue

@@ -161,6 +161,7 @@ struct rt_scene {
     // cycles L streams; with L <= 1 every frame uses lane 0 and launches of one scene are serialised.
     uint32_t *queue[NLANE] = {};
     bool overlap = false;
+    uint32_t blas_leaf = SAH_LEAF_CAP;   // option "blas_leaf": RT_BUILD_SAH BLAS leaf size (1..4), next rt_scene_build
     uint32_t tlas_leaf = 1;   // option "tlas_leaf": RT_BUILD_SAH per-frame TLAS leaf size (1..4; 1 measured best)
     bool inst_by_slot = true;       // option "inst_by_slot": host-built TLAS stages instance records in slot order
     bool block_by_slot[NLANE] = {};  // per frame block: staged in slot order
@@ -626,7 +627,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             std::vector<BuildItem> items(in.pcount);
             for (uint32_t k = 0; k < in.pcount; k++)
                 items[k] = {prim_box(s, in.ptype, in.pindex + k), prim_centroid(s, in.ptype, in.pindex + k), in.pindex + k};
-            bh.tree = mode == RT_BUILD_SAH ? build_sah_tree(std::move(items), SAH_LEAF_CAP)
+            bh.tree = mode == RT_BUILD_SAH ? build_sah_tree(std::move(items), s->blas_leaf)
                                            : build_median_tree(std::move(items), BLAS_LEAF_CAP, hm::blas_axis_state(seed, in.blas));
             bh.pair_base = pair_base;
             bh.slot_base = slot_base[in.ptype];
@@ -1084,6 +1085,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "split") {
         if (value < 0 || value > 0xFFFF) return fail(RT_ERR_INVALID_ARGUMENT, "split must be k_half | k_quarter << 8");
         s->split = (uint32_t)value;
+    } else if (k == "blas_leaf") {
+        if (value < 1 || value > (int64_t)SAH_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "blas_leaf must be in 1..4");
+        s->blas_leaf = (uint32_t)value;
     } else if (k == "tlas_leaf") {
         if (value < 1 || value > (int64_t)SAH_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_leaf must be in 1..4");
         s->tlas_leaf = (uint32_t)value;          // next frame's TLAS
