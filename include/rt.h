@@ -290,6 +290,8 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "blas_leaf" : RT_BUILD_SAH: primitives per BLAS leaf (1..4, default 4; set before rt_scene_build)
  *   "inst_by_slot": 1 = host-built TLAS: stage the per-frame instance records in TLAS leaf-slot order
  *                 (default 1; 0 = instance order, for A/B — results are identical)
+ *   "reserve"   : with "overlap", the persistent grid leaves this many workgroup slots free (default 8, one
+ *                 per XCD) so the next lane's schedule / upload / GPU TLAS kernels start beside the running launch
  *   "overlap"   : L = consecutive rt_render calls cycle through L (2..4) internal lanes (work-queue
  *                 heads, unit costs, schedule); a launch waits only for the previous launch of its own
  *                 lane and for its frame block, so a caller that cycles L streams runs frame
@@ -305,7 +307,9 @@ rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
  *               iterations, refill-loop iterations, 2 reserved;
  *   "costmap" : 1 u32 per output pixel: traversal steps (interior steps + leaf phases) of its path;
  *   "unit_cost", "unit_order": option "reorder" — per 8x8 unit, the work the last launch recorded, and
- *               the claim order that launch used (unit claimed at each band position).
+ *               the claim order that launch used (unit claimed at each band position);
+ *   "leaf_prims": 1 u32 per leaf-ordered triangle slot: the caller's triangle index stored there (each
+ *               BLAS owns the contiguous slots of its primitives, in leaf order).
  * Copies min(capacity, size) bytes to dst and stores the buffer's full size in *bytes. */
 rt_status rt_scene_debug_read(rt_scene *scene, const char *name, void *dst, size_t capacity, size_t *bytes);
 

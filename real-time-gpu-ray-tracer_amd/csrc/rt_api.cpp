@@ -9,7 +9,9 @@
 // with a thread-local message instead of exit() (Global.cu:34-41).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -166,6 +168,10 @@ struct rt_scene {
     bool inst_by_slot = true;       // option "inst_by_slot": host-built TLAS stages instance records in slot order
     bool block_by_slot[NLANE] = {};  // per frame block: staged in slot order
     uint32_t lanes = 1;
+    // option "reserve": with overlapped lanes the persistent grid leaves this many workgroup slots free (one
+    // per XCD at 8), so the next lane's schedule / upload kernels and GPU TLAS builds run beside a launch
+    // that holds the rest of the GPU instead of waiting for its drain
+    uint32_t reserve = 8;
     uint32_t lane = 0;              // lane of the next rt_render (overlap)
     int last_lane = 0;              // lane of the last rt_render
     hipEvent_t ev_lane_done[NLANE] = {};   // last trace launch of each lane finished
@@ -191,8 +197,10 @@ struct rt_scene {
     size_t costmap_pixels = 0;
     DevBuf<unsigned long long> timeline;
     uint32_t timeline_waves = 0;    // waves of the last launch that recorded a timeline
-    unsigned long long *counters = nullptr;       // HBM CNT_NUM
-    unsigned long long *counters_host = nullptr;  // pinned
+    // device counters, one CNT_NUM block per lane: a launch only adds to its own lane's block, so resetting
+    // or reading it never races with another lane's launch still in flight (rt_scene_collect sums the lanes)
+    unsigned long long *counters = nullptr;       // HBM NLANE x CNT_NUM
+    unsigned long long *counters_host = nullptr;  // pinned NLANE x CNT_NUM
 
     // camera
     bool cam_ok = false;
@@ -324,6 +332,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
     InstHot *hot = reinterpret_cast<InstHot *>(st + s->off_hot);
     InstCold *cold = reinterpret_cast<InstCold *>(st + s->off_cold);
     if (s->gpu_tlas()) {
+        s->block_by_slot[b] = false;                  // GPU-built TLASes keep instance order
         float *tbox = reinterpret_cast<float *>(st + s->off_tbox);
         float *tcent = reinterpret_cast<float *>(st + s->off_tcent);
         for (size_t i = 0; i < s->inst.size(); i++) {
@@ -565,11 +574,13 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     if (mode != RT_BUILD_COMPAT_MEDIAN && mode != RT_BUILD_SAH && mode != RT_BUILD_LBVH)
         return fail(RT_ERR_UNSUPPORTED, "unsupported build mode");
     HIP_TRY(hipSetDevice(s->device));
+    if (s->built) HIP_TRY(drain(s));              // a rebuild frees buffers earlier frames may still read
     s->build_seed = seed;
     s->build_mode = mode;
     s->inst.clear();
     s->blas.clear();
     s->max_blas_height = 0;
+    for (bool &v : s->block_by_slot) v = false;    // a rebuild may change the mode: no block is slot-ordered yet
 
     // buildBLASPinMem (RenderPin.cu:99-201): complete instances, one BLAS per unique (type, index).
     // The reference's map stores the instance index instead of the BLAS index (RenderPin.cu:151);
@@ -745,7 +756,10 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         if (!s->ring_start[i]) HIP_TRY(hipEventCreate(&s->ring_start[i]));
         if (!s->ring_stop[i]) HIP_TRY(hipEventCreate(&s->ring_stop[i]));
     }
-    if (!s->counters) HIP_TRY(hipMalloc(&s->counters, CNT_NUM * sizeof(unsigned long long)));
+    if (!s->counters) {
+        HIP_TRY(hipMalloc(&s->counters, rt_scene::NLANE * CNT_NUM * sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(s->counters, 0, rt_scene::NLANE * CNT_NUM * sizeof(unsigned long long)));
+    }
     for (int q = 0; q < rt_scene::NLANE; q++) {
         if (!s->queue[q]) {   // band heads, then (option "reorder") band item counts, one 128 B line each
             HIP_TRY(hipMalloc(&s->queue[q], 2 * QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t)));
@@ -764,7 +778,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         }
     }
     if (!s->counters_host)
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->counters_host), CNT_NUM * sizeof(unsigned long long), hipHostMallocDefault));
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->counters_host), rt_scene::NLANE * CNT_NUM * sizeof(unsigned long long),
+                              hipHostMallocDefault));
     s->active = -1;
 
     // initial transforms, then the frame-0 update + TLAS (Renderer.cu:110-111, 148-150)
@@ -955,25 +970,34 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         s->pending_copy = -1;
     }
     HIP_TRY(hipStreamWaitEvent(stream, s->ev_copied[s->active], 0));
+    unsigned long long *lane_counters = s->counters + (size_t)q * CNT_NUM;   // only this lane's launches add here
     if (!(o.flags & RT_RENDER_KEEP_COUNTERS)) {
-        if (s->overlap) HIP_TRY(hipStreamWaitEvent(stream, s->ev_render_done, 0));   // the other lane adds to them
-        HIP_TRY(hipMemsetAsync(s->counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
+        // every lane's block: the counters restart from this frame (other lanes' blocks are reset behind
+        // their own last launch, so no in-flight add is lost into a cleared block)
+        HIP_TRY(hipMemsetAsync(lane_counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
+        for (int l = 0; l < rt_scene::NLANE; l++) {
+            if (l == q || !s->overlap) continue;
+            HIP_TRY(hipStreamWaitEvent(stream, s->ev_lane_done[l], 0));
+            HIP_TRY(hipMemsetAsync(s->counters + (size_t)l * CNT_NUM, 0, CNT_NUM * sizeof(unsigned long long), stream));
+        }
     }
     const uint32_t slot = s->ring_head;
     s->ring_head = (s->ring_head + 1) % rt_scene::RING;
     if (s->ring_pending < rt_scene::RING) s->ring_pending++;
     s->last_stream = stream;
     HIP_TRY(hipEventRecord(s->ring_start[slot], stream));
-    if (s->use_persistent)
-        HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, s->counters, s->queue[q],
-                                                       s->cus * persistent_blocks_per_cu_exact(s->variant, false, false), s->threshold,
+    if (s->use_persistent) {
+        const uint32_t cap = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false, false)
+                                             : persistent_blocks_per_cu_fast(s->variant, lean, g.wide != 0));
+        const uint32_t blocks = s->overlap && cap > 2 * s->reserve ? cap - s->reserve : cap;
+        HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, lane_counters, s->queue[q], blocks, s->threshold,
                                                        s->variant, false, reset_queue, stream)
-                      : launch_render_persistent_fast(g, cam, out, count, s->counters, s->queue[q],
-                                                      s->cus * persistent_blocks_per_cu_fast(s->variant, lean, g.wide != 0), s->threshold,
+                      : launch_render_persistent_fast(g, cam, out, count, lane_counters, s->queue[q], blocks, s->threshold,
                                                       s->variant, lean, reset_queue, stream));
+    }
     else
-        HIP_TRY(exact ? launch_render_exact(g, cam, out, count, s->counters, stream)
-                      : launch_render_fast(g, cam, out, count, s->counters, stream));
+        HIP_TRY(exact ? launch_render_exact(g, cam, out, count, lane_counters, stream)
+                      : launch_render_fast(g, cam, out, count, lane_counters, stream));
     HIP_TRY(hipEventRecord(s->ring_stop[slot], stream));
     HIP_TRY(hipEventRecord(s->ev_used[s->active], stream));
     HIP_TRY(hipEventRecord(s->ev_render_done, stream));
@@ -982,7 +1006,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; }
         return RT_OK;
     }
-    HIP_TRY(hipMemcpyAsync(s->counters_host, s->counters, CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+    HIP_TRY(hipMemcpyAsync(s->counters_host, lane_counters, CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     s->ring_pending = 0;
     if (rgba_host) HIP_TRY(hipMemcpy(rgba_host, out.rgba, npix * 4, hipMemcpyDeviceToHost));
@@ -1101,6 +1125,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         s->lanes = value < 1 ? 1u : (uint32_t)value;
         s->overlap = s->lanes > 1;
         s->lane = 0;
+    } else if (k == "reserve") {
+        if (value < 0 || value > 256) return fail(RT_ERR_INVALID_ARGUMENT, "reserve must be in 0..256");
+        s->reserve = (uint32_t)value;
     } else if (k == "reorder") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "reorder must be 0 or 1");
         if (s->reorder != (value == 1)) for (bool &v : s->sched_valid) v = false;
@@ -1123,6 +1150,19 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
     } else if (k == "costmap") {
         src = s->costmap.p;
         size = s->costmap_pixels * sizeof(uint32_t);
+    } else if (k == "leaf_prims") {
+        // caller triangle index of every leaf-ordered triangle slot (TriCold::orig_index): BLAS b owns
+        // the slots [slot_base, slot_base + count) of its primitives, in leaf order
+        HIP_TRY(hipSetDevice(s->device));
+        HIP_TRY(drain(s));
+        const size_t n = s->tri_cold.n;
+        *bytes = n * sizeof(uint32_t);
+        if (capacity && n) {
+            const size_t m = std::min(capacity / sizeof(uint32_t), n);
+            HIP_TRY(hipMemcpy2D(dst, sizeof(uint32_t), reinterpret_cast<const uint8_t *>(s->tri_cold.p) + offsetof(TriCold, orig_index),
+                                sizeof(TriCold), sizeof(uint32_t), m, hipMemcpyDeviceToHost));
+        }
+        return RT_OK;
     } else if (k == "unit_cost" || k == "unit_order") {
         const int q = s->last_lane;
         src = k == "unit_cost" ? s->unit_cost[q].p : s->unit_order[q].p;
@@ -1155,10 +1195,12 @@ rt_status rt_scene_collect(rt_scene *s, rt_stats *acc, float *kernel_ms, uint32_
     if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(drain(s));
-    HIP_TRY(hipMemcpy(s->counters_host, s->counters, CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(s->counters_host, s->counters, rt_scene::NLANE * CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (int l = 1; l < rt_scene::NLANE; l++)          // sum the lanes' blocks into lane 0's slot
+        for (uint32_t k = 0; k < CNT_NUM; k++) s->counters_host[k] += s->counters_host[(size_t)l * CNT_NUM + k];
     if (acc) fill_stats(acc, s->counters_host);
     // collected: the next KEEP_COUNTERS frames accumulate from zero
-    HIP_TRY(hipMemset(s->counters, 0, CNT_NUM * sizeof(unsigned long long)));
+    HIP_TRY(hipMemset(s->counters, 0, rt_scene::NLANE * CNT_NUM * sizeof(unsigned long long)));
     const uint32_t n = s->ring_pending;
     uint32_t written = 0;
     for (uint32_t k = 0; k < n; k++) {

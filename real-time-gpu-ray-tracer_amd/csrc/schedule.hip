@@ -11,13 +11,19 @@
 // The image does not depend on the order: every pixel's RNG stream is keyed by its global pixel
 // index.
 //
-// One 1024-thread workgroup per band: a stable counting sort of the band's units over 16 cost
-// classes (class order = heaviest first; equal classes keep screen order, so neighbouring units of
-// one class are still claimed together).  A heavy unit becomes 2 or 4 claim items (32 / 16 pixels)
-// so that its paths spread over several waves instead of holding one wave for the critical path.
-// The band's items go to order[4 b0 ...) as (unit << 4 | piece << 2 | log2 pieces), the item count
-// to the band's count word (a line of its own, away from the atomically updated head); then the costs are cleared for the next launch and the
-// queue heads are reset (this replaces the per-frame hipMemsetAsync of the heads).
+// One 256-thread workgroup per band: a stable counting sort of the band's units over 16 cost classes
+// (class order = heaviest first; equal classes keep screen order, so neighbouring units of one class are
+// still claimed together).  A heavy unit becomes 2 or 4 claim items (32 / 16 pixels) so that its paths
+// spread over several waves instead of holding one wave for the critical path.  The band's items go to
+// order[4 b0 ...) as (unit << 4 | piece << 2 | log2 pieces), the item count to the band's count word (a
+// line of its own, away from the atomically updated head); then the costs are cleared for the next launch
+// and the queue heads are reset (this replaces the per-frame hipMemsetAsync of the heads).
+//
+// Footprint: a workgroup is sized like one workgroup of the persistent render kernel (4 waves, 16 KB of
+// LDS), so with overlapped frames it runs in the workgroup slots the render grid leaves free (option
+// "reserve", rt_api.cpp) while the other lane's launch holds the rest of the GPU.  The first version used
+// one 1024-thread workgroup with 64 KB of LDS per band: it could only start once the other lane's
+// launch began to drain, and averaged 172 us per frame instead of 10 us (profiles/r01_kernel_stats_final.csv).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -26,8 +32,10 @@
 namespace rtamd {
 namespace {
 
-constexpr int SCHED_THREADS = 1024;     // 16 waves
-constexpr int SCHED_CLASSES = 16;       // one class per wave in the scan
+constexpr int SCHED_THREADS = 256;      // 4 waves: the footprint of one render workgroup
+constexpr int SCHED_CLASSES = 16;
+constexpr int SCHED_WAVES = SCHED_THREADS / 64;
+constexpr int SCAN_PER_LANE = SCHED_THREADS / 64;                    // threads' counts summed per lane in the scan
 
 // class 0 = heaviest: half-octaves of the unit's mean traversal steps per pixel, floor(2 log2(c/64 + 1))
 // (a sky unit averages ~5 steps per pixel, a unit over the particle cluster ~100; classes saturate at ~180)
@@ -69,21 +77,24 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
         }
         __syncthreads();
         // exclusive scan of each class's item counts over the threads (thread order = screen order):
-        // wave w scans class w, each lane 16 consecutive threads' counts
+        // wave w scans classes [4w, 4w + 4), each lane SCAN_PER_LANE consecutive threads' counts
         const uint32_t w = t >> 6, lane = t & 63u;
-        uint32_t local[16], run = 0;
+        for (int cc = 0; cc < SCHED_CLASSES / SCHED_WAVES; cc++) {
+            const uint32_t c = w * (SCHED_CLASSES / SCHED_WAVES) + cc;
+            uint32_t local[SCAN_PER_LANE], run = 0;
 #pragma unroll
-        for (int k = 0; k < 16; k++) { local[k] = run; run += cnt[w][lane * 16u + k]; }
-        uint32_t incl = run;
+            for (int k = 0; k < SCAN_PER_LANE; k++) { local[k] = run; run += cnt[c][lane * SCAN_PER_LANE + k]; }
+            uint32_t incl = run;
 #pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off, 64);
-            if (lane >= (uint32_t)off) incl += y;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(incl, off, 64);
+                if (lane >= (uint32_t)off) incl += y;
+            }
+            const uint32_t excl = incl - run;
+#pragma unroll
+            for (int k = 0; k < SCAN_PER_LANE; k++) cnt[c][lane * SCAN_PER_LANE + k] = excl + local[k];
+            if (lane == 63u) total[c] = incl;
         }
-        const uint32_t excl = incl - run;
-#pragma unroll
-        for (int k = 0; k < 16; k++) cnt[w][lane * 16u + k] = excl + local[k];
-        if (lane == 63u) total[w] = incl;
         __syncthreads();
         if (t == 0) {
             uint32_t acc = 0;

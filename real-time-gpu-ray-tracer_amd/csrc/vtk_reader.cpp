@@ -29,6 +29,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
+#include <memory>
 #include <new>
 #include <string>
 #include <vector>
@@ -81,9 +83,24 @@ int type_size(const std::string &t) {
     return 0;
 }
 
+// a * b without wrap-around (counts read from the file are untrusted)
+bool mul_ok(size_t a, size_t b, size_t &r) {
+    if (a != 0 && b > SIZE_MAX / a) return false;
+    r = a * b;
+    return true;
+}
+
 // Reads n values of VTK type `t` as doubles (binary: a big-endian block; the next keyword is found by
-// skipping whitespace, as vtkDataReader does — some writers put no newline after a block).
+// skipping whitespace, as vtkDataReader does — some writers put no newline after a block).  n is bounded
+// by the bytes left in the file before anything is allocated: sz bytes per binary value, at least one
+// byte per ASCII token.
 bool read_values(Cursor &c, bool binary, const std::string &t, size_t n, std::vector<double> &out) {
+    const size_t left = c.d.size() - c.p;
+    if (!binary && n > left) return false;
+    if (binary) {
+        const int sz = type_size(t);
+        if (sz == 0 || n > left / (size_t)sz) return false;
+    }
     out.resize(n);
     if (!binary) {
         for (size_t i = 0; i < n; i++) {
@@ -96,7 +113,6 @@ bool read_values(Cursor &c, bool binary, const std::string &t, size_t n, std::ve
         return true;
     }
     const int sz = type_size(t);
-    if (sz == 0 || c.p + (size_t)sz * n > c.d.size()) return false;
     const uint8_t *b = c.d.data() + c.p;
     for (size_t i = 0; i < n; i++, b += sz) {
         const uint64_t u = be(b, sz);
@@ -151,6 +167,8 @@ struct rt_vtk_series {
 namespace {
 
 void take_cell_array(rt_vtk_file &f, const std::string &name, size_t comps, size_t tuples, const std::vector<double> &v) {
+    size_t need = 0;
+    if (comps == 0 || !mul_ok(comps, tuples, need) || v.size() < need) return;   // read_values read exactly `need`
     if (name == "id") {
         f.ids.resize(tuples);
         for (size_t i = 0; i < tuples; i++) f.ids[i] = v[i * comps];
@@ -257,7 +275,9 @@ rt_status parse_vtk(const std::vector<uint8_t> &data, rt_vtk_file &f) {
             const size_t n = std::strtoull(c.token().c_str(), nullptr, 10);
             const std::string t = c.token();
             c.end_of_line();
-            if (!read_values(c, binary, t, 3 * n, vals)) return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: truncated POINTS");
+            size_t n3 = 0;
+            if (!mul_ok(3, n, n3) || n > 0xFFFFFFFFull) return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: POINTS count out of range");
+            if (!read_values(c, binary, t, n3, vals)) return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: truncated POINTS");
             f.points.resize(n);
             for (size_t i = 0; i < n; i++) f.points[i] = {vals[3 * i], vals[3 * i + 1], vals[3 * i + 2]};
         } else if (kw == "TRIANGLE_STRIPS") {
@@ -269,7 +289,9 @@ rt_status parse_vtk(const std::vector<uint8_t> &data, rt_vtk_file &f) {
             f.strip_offsets.assign(1, 0);
             for (size_t s = 0; s < n; s++) {
                 if (k >= size) return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: strip list shorter than its cell count");
-                const size_t m = (size_t)vals[k++];
+                const double mv = vals[k++];
+                if (!(mv >= 0.0) || mv > (double)(size - k)) return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: strip runs past its list");
+                const size_t m = (size_t)mv;
                 if (k + m > size) return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: strip runs past its list");
                 for (size_t j = 0; j < m; j++) {
                     const double id = vals[k++];
@@ -297,7 +319,9 @@ rt_status parse_vtk(const std::vector<uint8_t> &data, rt_vtk_file &f) {
                 else c.p = save;
             }
             const size_t tuples = in_cell_data ? n_cell_tuples : n_point_tuples;
-            if (!read_values(c, binary, t, comps * tuples, vals)) return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: truncated " + kw + " " + name);
+            size_t nv = 0;
+            if (!mul_ok(comps, tuples, nv)) return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: " + kw + " " + name + " size out of range");
+            if (!read_values(c, binary, t, nv, vals)) return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: truncated " + kw + " " + name);
             if (in_cell_data) take_cell_array(f, name, comps, tuples, vals);
         } else if (kw == "FIELD") {
             c.token();                                                          // field name
@@ -309,7 +333,9 @@ rt_status parse_vtk(const std::vector<uint8_t> &data, rt_vtk_file &f) {
                 const size_t tuples = std::strtoull(c.token().c_str(), nullptr, 10);
                 const std::string t = c.token();
                 c.end_of_line();
-                if (!read_values(c, binary, t, comps * tuples, vals)) return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: truncated FIELD array " + name);
+                size_t nv = 0;
+                if (!mul_ok(comps, tuples, nv)) return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: FIELD array " + name + " size out of range");
+                if (!read_values(c, binary, t, nv, vals)) return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: truncated FIELD array " + name);
                 if (in_cell_data) take_cell_array(f, name, comps, tuples, vals);
             }
         } else {
@@ -432,17 +458,31 @@ struct JsonParser {
 
 extern "C" {
 
+// No C++ exception may cross the C ABI (std::terminate would end the caller's process): allocation
+// failures become RT_ERR_OUT_OF_MEMORY, anything else RT_ERR_INVALID_ARGUMENT.
+#define VTK_GUARD_BEGIN try {
+#define VTK_GUARD_END                                                                          \
+    }                                                                                          \
+    catch (const std::bad_alloc &) { return vfail(RT_ERR_OUT_OF_MEMORY, "vtk: host allocation failed"); } \
+    catch (const std::exception &e) { return vfail(RT_ERR_INVALID_ARGUMENT, std::string("vtk: ") + e.what()); } \
+    catch (...) { return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: malformed input"); }
+
 rt_status rt_vtk_read(const char *path, rt_vtk_file **out) {
     if (!path || !out) return vfail(RT_ERR_INVALID_ARGUMENT, "null argument");
     *out = nullptr;
+    rt_vtk_file *f = nullptr;
+    VTK_GUARD_BEGIN
     std::vector<uint8_t> data;
     if (!read_file(path, data)) return vfail(RT_ERR_INVALID_ARGUMENT, std::string("failed to open vtk file: ") + path);
-    auto *f = new (std::nothrow) rt_vtk_file();
-    if (!f) return vfail(RT_ERR_OUT_OF_MEMORY, "host allocation failed");
+    f = new rt_vtk_file();
     const rt_status st = parse_vtk(data, *f);
     if (st != RT_OK) { delete f; return st; }
     *out = f;
     return RT_OK;
+    }
+    catch (const std::bad_alloc &) { delete f; return vfail(RT_ERR_OUT_OF_MEMORY, "vtk: host allocation failed"); }
+    catch (const std::exception &e) { delete f; return vfail(RT_ERR_INVALID_ARGUMENT, std::string("vtk: ") + e.what()); }
+    catch (...) { delete f; return vfail(RT_ERR_INVALID_ARGUMENT, "vtk: malformed input"); }
 }
 
 void rt_vtk_free(rt_vtk_file *f) { delete f; }
@@ -500,6 +540,7 @@ rt_status rt_vtk_convert(const rt_vtk_file *f, uint32_t triangle_index_base, rt_
                          rt_instance_desc *instances) {
     if (!f || !triangles || !instances) return vfail(RT_ERR_INVALID_ARGUMENT, "null argument");
     const size_t cells = f->strip_offsets.size() - 1;
+    VTK_GUARD_BEGIN
     std::vector<rt_vtk_particle> parts(cells);
     const rt_status st = rt_vtk_particles(f, parts.data());
     if (st != RT_OK) return st;
@@ -533,11 +574,13 @@ rt_status rt_vtk_convert(const rt_vtk_file *f, uint32_t triangle_index_base, rt_
         I.xform.scale = rt_vec3{3.0f, 3.0f, 3.0f};
     }
     return RT_OK;
+    VTK_GUARD_END
 }
 
 rt_status rt_vtk_series_read(const char *path, rt_vtk_series **out) {
     if (!path || !out) return vfail(RT_ERR_INVALID_ARGUMENT, "null argument");
     *out = nullptr;
+    VTK_GUARD_BEGIN
     std::vector<uint8_t> data;
     if (!read_file(path, data)) return vfail(RT_ERR_INVALID_ARGUMENT, std::string("could not open the series file: ") + path);
     const std::string text(data.begin(), data.end());
@@ -546,8 +589,7 @@ rt_status rt_vtk_series_read(const char *path, rt_vtk_series **out) {
     if (!jp.ok || root.kind != Json::OBJ) return vfail(RT_ERR_INVALID_ARGUMENT, "JSON parsing error in series file");
     const Json *files = root.get("files");
     if (!files || files->kind != Json::ARR) return vfail(RT_ERR_INVALID_ARGUMENT, "failed to parse files array in series file");
-    auto *s = new (std::nothrow) rt_vtk_series();
-    if (!s) return vfail(RT_ERR_OUT_OF_MEMORY, "host allocation failed");
+    std::unique_ptr<rt_vtk_series> s(new rt_vtk_series());
     // names are relative to the series file's directory (Renderer.cu:440 strips the file name)
     std::string dir(path);
     const size_t slash = dir.find_last_of('/');
@@ -555,14 +597,14 @@ rt_status rt_vtk_series_read(const char *path, rt_vtk_series **out) {
     for (const Json &it : files->items) {
         const Json *name = it.get("name"), *time = it.get("time");
         if (!name || name->kind != Json::STR || !time || time->kind != Json::NUM) {
-            delete s;
             return vfail(RT_ERR_INVALID_ARGUMENT, "series entry without name / time");
         }
         s->paths.push_back(!name->str.empty() && name->str[0] == '/' ? name->str : dir + name->str);
         s->times.push_back((float)time->num);
     }
-    *out = s;
+    *out = s.release();
     return RT_OK;
+    VTK_GUARD_END
 }
 
 size_t rt_vtk_series_count(const rt_vtk_series *s) { return s ? s->paths.size() : 0; }

@@ -227,3 +227,26 @@ def test_large_single_blas_device_wide_path(gpu_lib):
     rgba, _, _ = r.render(0, exact=True)
     f, mx = frac_within(rgba, orgba)
     assert f >= 0.999, (f, mx)
+
+
+def test_rebuild_sah_then_lbvh_equals_fresh_lbvh(gpu_lib):
+    """A scene built with SAH (instance records staged in TLAS slot order) and then rebuilt with LBVH
+    must trace instance-ordered records again: frames and per-ray hits equal a fresh LBVH scene
+    (the LBVH frame path left the slot-order flag of its frame block set)."""
+    s = scenes.demo_with_particles(10)
+    rays = np.concatenate([np.tile([[0.0, 2.0, 10.0]], (4000, 1)),
+                           np.random.default_rng(5).normal(size=(4000, 3)) * [1, 0.5, 1] + [0, 0, -1]], 1)
+    rays[:, 3:] /= np.linalg.norm(rays[:, 3:], axis=1, keepdims=True)
+    fresh = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(200, 120, ray_trace_depth=2)
+    want = [fresh.render(f)[0] for f in range(5)]
+    want_hits = fresh.trace_rays(rays)
+    fresh.cleanup()
+    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(200, 120, ray_trace_depth=2)
+    for f in range(5):                       # every frame block gets staged in slot order
+        r.render(f)
+    r.build_acceleration_structure(0, mode="lbvh")
+    for f in range(5):
+        assert np.array_equal(r.render(f)[0], want[f]), f
+    got = r.trace_rays(rays)
+    for k in ("t", "instance", "pindex", "ptype", "point", "normal"):
+        assert np.array_equal(got[k], want_hits[k]), k

@@ -111,3 +111,24 @@ def test_ascii_file_with_field_arrays(lib, tmp_path):
     assert int(part["id"]) == 42 and part["velocity"].tolist() == [1.0, 2.0, 3.0]
     tris, inst = f.convert(0)
     assert tris["vertex"][1].tolist() == [[1, 0, 0], [1, 1, 0], [0, 1, 0]]   # odd triangle: 2nd/3rd swapped
+
+
+@pytest.mark.parametrize("body", [
+    # 3 * n wraps to 2 in 64-bit arithmetic
+    b"POINTS 6148914691236517206 float\n",
+    # comps * tuples wraps to 0: a wrapped size used to pass and then index far out of bounds
+    b"POINTS 3 float\n0 0 0 1 0 0 0 1 0\nTRIANGLE_STRIPS 1 4\n3 0 1 2\nCELL_DATA 4\n"
+    b"FIELD FieldData 1\nid 4611686018427387904 4 int\n1\n",
+    # a huge count that does not wrap must fail before allocating (no bad_alloc through the C ABI)
+    b"POINTS 3 float\n0 0 0 1 0 0 0 1 0\nTRIANGLE_STRIPS 1 4\n3 0 1 2\nCELL_DATA 1\n"
+    b"SCALARS id int 1000000000000000\n1\n",
+    # negative / oversized strip length
+    b"POINTS 3 float\n0 0 0 1 0 0 0 1 0\nTRIANGLE_STRIPS 1 4\n-5 0 1 2\n",
+])
+def test_hostile_counts_fail_cleanly(lib, tmp_path, body):
+    """Counts from the file are untrusted: products are checked, sizes are bounded by the bytes left in
+    the file before any allocation, and no C++ exception crosses the C ABI."""
+    p = tmp_path / "hostile.vtk"
+    p.write_bytes(b"# vtk DataFile Version 3.0\nx\nASCII\nDATASET POLYDATA\n" + body)
+    with pytest.raises(abi.RtError):
+        VtkFile(str(p))
