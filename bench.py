@@ -7,8 +7,9 @@
 A step is one frame of the reference's render loop (src/Global/Renderer.cu:264-317): the
 instance update callback (Main.cu updateInstance, native), the host TLAS rebuild + upload,
 and the trace kernel over the frame — for N > 1 each rank traces its interleaved 64x64
-screen tiles, the tile slabs are gathered to rank 0 over RCCL (torch.distributed "nccl") and
-assembled into the frame on rank 0.  Scene, BVHs and framebuffer stay in HBM; nothing is
+screen tiles, and the library gathers the tiles to rank 0 over RCCL and assembles the frame there,
+inside rt_render (rt_scene_attach_comm; torch.distributed only broadcasts the RCCL id and runs the
+barriers and the max-over-ranks timing).  Scene, BVHs and framebuffer stay in HBM; nothing is
 copied to the host inside the timed region.
 
 Rank 0 prints one JSON line (see DESIGN.md §4 for every field's definition).
@@ -58,6 +59,8 @@ def parse():
     p.add_argument("--opt", action="append", default=[], help="extra rt_scene_set_option key=value (A/B studies)")
     p.add_argument("--pre-opt", action="append", default=[], help="rt_scene_set_option key=value before the build")
     p.add_argument("--tile", type=int, default=64, help="N > 1 screen-tile edge in pixels (multiple of 8)")
+    p.add_argument("--attach-comm", action="store_true",
+                   help="N = 1: run the multi-GPU frame path anyway (a world-1 RCCL communicator: tiles + assemble)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     return p.parse_args()
@@ -191,61 +194,34 @@ def main():
     # "overlap": frame k runs on lanes[k % L]; each lane is a self-contained trace -> gather -> assemble chain
     lanes = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(L - 1)] if overlap else None
     shard = tuple(int(v) for v in args.shard.split("/")) if args.shard else None
-    if shard and n > 1:
+    if shard and (n > 1 or args.attach_comm):
         raise SystemExit("--shard is a one-GPU study")
 
     tiles = None
-    pending = []                 # N > 1: (gather work, gathered buffer) of the previous frame
-    if n > 1:
-        tiles = (TILE, TILE, rank, n)
-        slab_tiles = max(r.tiles_for_rank(TILE, TILE, k, n) for k in range(n))
-        slab_px = slab_tiles * TILE * TILE
-        # double-buffered slabs: frame k's gather (RCCL stream) overlaps frame k+1's trace
-        slabs = [torch.zeros(slab_px * 4, dtype=torch.uint8, device="cuda") for _ in range(max(2, L))]
-        gathered = [torch.zeros(n * slab_px * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
-                    for _ in range(max(2, L))]
-        frame_buf = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
-        frame_bufs = [frame_buf] + [torch.zeros_like(frame_buf) if overlap else frame_buf for _ in range(L - 1)] \
-            if rank == 0 else None
-    else:
-        if shard:
-            tiles = (TILE, TILE, shard[0], shard[1])
-        frame_buf = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda")
-        frame_bufs = [frame_buf] + [torch.zeros_like(frame_buf) if overlap else frame_buf for _ in range(L - 1)]
+    if n > 1 or args.attach_comm:
+        # the library's multi-GPU frame (rt_scene_attach_comm): each rank traces its interleaved tiles,
+        # the tiles are gathered to rank 0 over RCCL and assembled there, all on the frame's stream
+        cid = [Renderer.comm_unique_id() if rank == 0 else None]
+        if n > 1:
+            dist.broadcast_object_list(cid, src=0)
+        r.attach_comm(cid[0], rank, n, TILE, TILE)
+    elif shard:
+        tiles = (TILE, TILE, shard[0], shard[1])
+    frame_buf = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
+    frame_bufs = ([frame_buf] + [torch.zeros_like(frame_buf) if overlap else frame_buf for _ in range(L - 1)]
+                  if rank == 0 else [None] * L)
 
     def finish_gather():
-        """Wait (stream-ordered) for the previous frame's gather; rank 0 assembles it into the frame."""
-        if pending:
-            work, g = pending.pop()
-            work.wait()
-            if rank == 0:
-                r.assemble_tiles(g.data_ptr(), slab_tiles, TILE, TILE, n, frame_buf.data_ptr(), stream)
+        """(kept for the call sites: the gather is stream-ordered inside rt_render)"""
 
     def step(frame, sync=True, keep=False):
-        """One frame; sync=False pipelines it (host TLAS build of the next frame overlaps the GPU)."""
-        b = frame % L if overlap else frame % 2
-        if n == 1:
-            st = lanes[b].cuda_stream if overlap else stream
-            r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=frame_bufs[b % len(frame_bufs)].data_ptr(), stream=st,
-                     sync=sync, keep_counters=keep, tiles=tiles)
-            return
-        if overlap:
-            with torch.cuda.stream(lanes[b]):
-                r.render(frame, exact=args.exact, want_rgba=False, tiles=tiles, rgba8_device=slabs[b].data_ptr(),
-                         stream=lanes[b].cuda_stream, sync=sync, keep_counters=keep)
-                work = dist.gather(slabs[b], list(gathered[b].chunk(n)) if rank == 0 else None, dst=0, async_op=True)
-                work.wait()        # stream-ordered: this lane's next frame reuses slabs[b] after the gather
-                if rank == 0:
-                    r.assemble_tiles(gathered[b].data_ptr(), slab_tiles, TILE, TILE, n, frame_bufs[b].data_ptr(),
-                                     lanes[b].cuda_stream)
-            return
-        r.render(frame, exact=args.exact, want_rgba=False, tiles=tiles, rgba8_device=slabs[b].data_ptr(), stream=stream,
-                 sync=sync, keep_counters=keep)
-        work = dist.gather(slabs[b], list(gathered[b].chunk(n)) if rank == 0 else None, dst=0, async_op=True)
-        finish_gather()            # frame - 1: its slab is free again before frame + 1 is traced into it
-        pending.append((work, gathered[b]))
-        if sync:
-            finish_gather()
+        """One frame; sync=False pipelines it (host TLAS build of the next frame overlaps the GPU).
+        With "overlap", frame k runs on lanes[k % L] (its own trace -> gather -> assemble chain)."""
+        b = frame % L if overlap else 0
+        st = lanes[b].cuda_stream if overlap else stream
+        fb = frame_bufs[b]
+        r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=fb.data_ptr() if fb is not None else None,
+                 stream=st, sync=sync, keep_counters=keep, tiles=tiles)
 
     for f in range(args.warmup):
         step(f)
@@ -283,7 +259,8 @@ def main():
     lat = []
     for k in range(20):
         t1 = time.perf_counter()
-        step(args.warmup + args.steps + k, sync=True)
+        step(args.warmup + args.steps + k, sync=False)    # enqueue, then wait for the whole device
+        finish_gather()
         torch.cuda.synchronize()
         lat.append((time.perf_counter() - t1) * 1e3)
     _, serial_ms = r.collect()
@@ -293,7 +270,7 @@ def main():
     # untimed work-counting pass (same frame as the first timed step) for the roofline
     torch.cuda.synchronize()
     _, _, cst = r.render(args.warmup, exact=args.exact, want_rgba=False, count_work=True,
-                         rgba8_device=(slabs[0] if n > 1 else frame_buf).data_ptr(), tiles=tiles, stream=stream)
+                         rgba8_device=frame_buf.data_ptr() if frame_buf is not None else None, tiles=tiles, stream=stream)
     if n > 1:
         dist.barrier()
 
@@ -325,8 +302,11 @@ def main():
                 "width": cfg.width, "height": cfg.height, "spp": cfg.spp, "depth": cfg.depth,
                 "triangles": scene.triangle_count, "instances": len(scene.instances),
                 "blas_node_pairs": info["blas_node_pairs"],
-                "parallelism": (f"screen-tiles{n} ({TILE}x{TILE} interleaved, RCCL gather overlapping the next frame)"
-                                if n > 1 else (f"single-gpu, shard {args.shard} only" if shard else "single-gpu")),
+                "parallelism": (f"screen-tiles{n} ({TILE}x{TILE} interleaved; rt_scene_attach_comm: RCCL gather + "
+                                f"assemble inside rt_render, overlapped across {L} lanes)"
+                                if n > 1 else (f"single-gpu, shard {args.shard} only" if shard else
+                                               ("single-gpu through the world-1 comm path" if args.attach_comm
+                                                else "single-gpu"))),
                 "overlap_lanes": L,
                 "tile": TILE,
                 "threshold": args.threshold if args.threshold is not None else 32,

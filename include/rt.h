@@ -260,6 +260,34 @@ rt_status rt_assemble_tiles(rt_scene *scene, const void *gathered_device, uint32
 uint32_t rt_tiles_for_rank(const rt_scene *scene, uint32_t tile_w, uint32_t tile_h,
                            uint32_t tile_rank, uint32_t tile_count);
 
+/* --- multi-GPU frames: screen tiles + RCCL gather inside the library --------------
+ * One process (or thread) per GPU, each holding its own scene built from the same inputs (the
+ * reference is single-GPU: Renderer.cu:305-317 launches one kernel over the whole surface).  After
+ * rt_scene_attach_comm, every rt_render of the scene traces only this rank's screen tiles (tile t of
+ * the row-major tile grid belongs to rank t mod world), gathers the tiles to rank 0 over RCCL (grouped
+ * ncclSend / ncclRecv, xGMI) and assembles the frame there (csrc/assemble.hip), all enqueued on the
+ * call's stream.  Rank 0's rgba8 outputs receive the whole frame; other ranks' output arguments are
+ * ignored.  Every rank must make the same sequence of rt_render calls (with "overlap", the same lane
+ * sequence).  rgb32 outputs and rt_render_opts tile fields are rejected while attached; rt_stats count
+ * this rank's work.  The assembled frame is byte-identical for any world size: the RNG is keyed by the
+ * global padded pixel index. */
+typedef struct rt_comm_id { char internal[128]; } rt_comm_id;      /* an ncclUniqueId */
+
+/* Rank 0 creates the id (ncclGetUniqueId) and passes it to every rank out of band. */
+rt_status rt_comm_unique_id(rt_comm_id *id);
+/* Collective over the `world` ranks (same id, world, tile size); world == 1 is allowed.  librccl.so.1 is
+ * resolved at this call (the one already in the process, else ROCm's): single-GPU callers never need it. */
+rt_status rt_scene_attach_comm(rt_scene *scene, const rt_comm_id *id, int rank, int world,
+                               uint32_t tile_w, uint32_t tile_h);
+rt_status rt_scene_detach_comm(rt_scene *scene);
+
+/* Tile bookkeeping shared by the kernels and the host (no GPU needed): the largest number of tiles a
+ * rank owns (slabs are padded to it), and the frame pixel of slab pixels [first, first + n) of `rank`
+ * (xy[2i], xy[2i+1]; -1, -1 for pixels outside the frame). */
+uint32_t rt_slab_tiles(uint32_t width, uint32_t height, uint32_t tile_w, uint32_t tile_h, uint32_t tile_count);
+rt_status rt_tile_pixels(uint32_t width, uint32_t height, uint32_t tile_w, uint32_t tile_h, uint32_t tile_rank,
+                         uint32_t tile_count, uint64_t first, uint64_t n, int32_t *xy);
+
 /* Trace arbitrary world rays (origin xyz, direction xyz per ray) against the current TLAS
  * with t in [0.001, inf) and return the closest hit (TLAS::hit, src/AS/TLAS.cu:131-201). */
 rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_count,

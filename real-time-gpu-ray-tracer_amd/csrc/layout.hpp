@@ -40,6 +40,30 @@ __host__ __device__ inline uint32_t ref_leaf_start(uint32_t r) { return r & REF_
 __host__ __device__ inline uint32_t ref_leaf_count(uint32_t r) { return ((r >> 26) & 3u) + 1u; }
 __host__ __device__ inline uint32_t ref_leaf_type(uint32_t r) { return (r >> 28) & 3u; }
 
+// ---- screen-tile sharding (multi-GPU frames) ------------------------------------
+// Tiles of tw x th pixels cover the frame in row-major tile order; rank r of n owns tiles t = r, r + n,
+// r + 2n, ...  Its slab holds its tiles back to back, row-major inside a tile, padded to the largest
+// rank's tile count.  Slab pixel i of rank r -> frame pixel (x, y); false for a pixel outside the frame
+// (the right / bottom edge tiles, the padding of a short slab).  The assemble kernel, the host ABI
+// (rt_tile_pixels) and the CPU protocol tests share this one definition.
+__host__ __device__ inline uint32_t tiles_total(uint32_t W, uint32_t H, uint32_t tw, uint32_t th) {
+    return ((W + tw - 1) / tw) * ((H + th - 1) / th);
+}
+__host__ __device__ inline uint32_t slab_tile_count(uint32_t W, uint32_t H, uint32_t tw, uint32_t th, uint32_t count) {
+    return (tiles_total(W, H, tw, th) + count - 1) / count;      // rank 0 owns the most tiles
+}
+__host__ __device__ inline bool tile_pixel(uint32_t W, uint32_t H, uint32_t tw, uint32_t th, uint32_t rank, uint32_t count,
+                                           uint64_t i, uint32_t &x, uint32_t &y) {
+    const uint32_t tiles_x = (W + tw - 1) / tw;
+    const uint64_t tile_px = (uint64_t)tw * th;
+    const uint64_t t = rank + (i / tile_px) * count;
+    const uint32_t p = (uint32_t)(i % tile_px);
+    if (t >= tiles_total(W, H, tw, th)) return false;
+    x = (uint32_t)(t % tiles_x) * tw + p % tw;
+    y = (uint32_t)(t / tiles_x) * th + p / tw;
+    return x < W && y < H;
+}
+
 // ---- records -------------------------------------------------------------------------
 struct alignas(16) NodePair {       // 64 B
     float c0[6];                    // child 0 box {xmin,xmax,ymin,ymax,zmin,zmax}

@@ -20,6 +20,7 @@
 
 #include "../../include/rt.h"
 #include "bvh_build.hpp"
+#include "comm.hpp"
 #include "host_math.hpp"
 #include "layout.hpp"
 #include "lbvh.hpp"
@@ -35,7 +36,7 @@ hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, c
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
 hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t, uint32_t,
-                           void *, const void *, size_t, hipStream_t);
+                           void *, const void *, size_t, unsigned long long *, hipStream_t);
 hipError_t launch_frame_copy(void *, const void *, size_t, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean, bool wide);
 hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, uint32_t, hipStream_t);
@@ -94,6 +95,18 @@ struct DevBuf {
     T *p = nullptr;
     size_t n = 0;
     void release() { if (p) (void)hipFree(p); p = nullptr; n = 0; }
+};
+
+// rt_scene_attach_comm: this scene is rank `rank` of a `world`-rank frame.  One communicator
+// per overlap lane (split from the first), so the lanes' gathers on different streams never share one.
+struct CommState {
+    static constexpr int NLANE = 4;
+    int rank = 0, world = 1;
+    uint32_t tile_w = 64, tile_h = 64;
+    ncclComm_t comm[NLANE] = {};
+    size_t slab_bytes = 0;                 // one rank's slab (largest tile count), RGBA8
+    DevBuf<uint8_t> slab[NLANE];           // ranks > 0: this rank's traced tiles
+    DevBuf<uint8_t> gathered[NLANE];       // rank 0: world slabs; its own tiles are traced into slab 0
 };
 
 size_t align16(size_t x) { return (x + 15) & ~size_t(15); }
@@ -201,6 +214,11 @@ struct rt_scene {
     // or reading it never races with another lane's launch still in flight (rt_scene_collect sums the lanes)
     unsigned long long *counters = nullptr;       // HBM NLANE x CNT_NUM
     unsigned long long *counters_host = nullptr;  // pinned NLANE x CNT_NUM
+    // a frame without RT_RENDER_KEEP_COUNTERS starts a new epoch; a lane's block is cleared by the first launch
+    // of that lane in the epoch (no waiting on the other lanes), and rt_scene_collect sums only blocks of the
+    // current epoch
+    uint64_t cnt_epoch = 0;
+    uint64_t lane_epoch[NLANE] = {};
 
     // camera
     bool cam_ok = false;
@@ -225,12 +243,25 @@ struct rt_scene {
     hipEvent_t ev_render_done = nullptr;   // last trace launch finished (BLAS rebuilds wait on it)
     bool gpu_tlas() const { return build_mode == RT_BUILD_LBVH; }
 
+    CommState *comm = nullptr;             // multi-GPU frame (rt_scene_attach_comm)
+    void release_comm() {
+        if (!comm) return;
+        for (int q = 0; q < CommState::NLANE; q++) {
+            if (comm->comm[q]) (void)rccl().CommDestroy(comm->comm[q]);
+            comm->slab[q].release();
+            comm->gathered[q].release();
+        }
+        delete comm;
+        comm = nullptr;
+    }
+
     ~rt_scene() {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         for (int q = 0; q < NLANE; q++)          // launches still running on caller streams
             if (ev_lane_done[q]) (void)hipEventSynchronize(ev_lane_done[q]);
         if (ev_render_done) (void)hipEventSynchronize(ev_render_done);
+        release_comm();
         blas_pairs.release(); blas_quads.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
         quad_hot.release(); quad_cold.release(); materials.release(); out_rgba.release(); out_rgb.release();
         timeline.release(); costmap.release();
@@ -834,6 +865,70 @@ uint32_t rt_tiles_for_rank(const rt_scene *s, uint32_t tw, uint32_t th, uint32_t
     return tiles_for_rank(s->width, s->height, tw, th, rank, count);
 }
 
+uint32_t rt_slab_tiles(uint32_t w, uint32_t h, uint32_t tw, uint32_t th, uint32_t count) {
+    if (w == 0 || h == 0 || tw == 0 || th == 0 || count == 0) return 0;
+    return slab_tile_count(w, h, tw, th, count);
+}
+
+rt_status rt_tile_pixels(uint32_t w, uint32_t h, uint32_t tw, uint32_t th, uint32_t rank, uint32_t count, uint64_t first,
+                         uint64_t n, int32_t *xy) {
+    if ((n && !xy) || w == 0 || h == 0 || tw == 0 || th == 0 || count == 0 || rank >= count)
+        return fail(RT_ERR_INVALID_ARGUMENT, "bad tile geometry");
+    for (uint64_t i = 0; i < n; i++) {
+        uint32_t x = 0, y = 0;
+        const bool in = tile_pixel(w, h, tw, th, rank, count, first + i, x, y);
+        xy[2 * i] = in ? (int32_t)x : -1;
+        xy[2 * i + 1] = in ? (int32_t)y : -1;
+    }
+    return RT_OK;
+}
+
+rt_status rt_comm_unique_id(rt_comm_id *id) {
+    if (!id) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
+    static_assert(sizeof(rt_comm_id) == sizeof(ncclUniqueId), "rt_comm_id must be an ncclUniqueId");
+    const Rccl &R = rccl();
+    if (!R.ok) return fail(RT_ERR_UNSUPPORTED, R.error);
+    ncclUniqueId u;
+    const ncclResult_t e = R.GetUniqueId(&u);
+    if (e != ncclSuccess) return fail(RT_ERR_DEVICE, std::string("ncclGetUniqueId: ") + R.GetErrorString(e));
+    std::memcpy(id, &u, sizeof u);
+    return RT_OK;
+}
+
+rt_status rt_scene_attach_comm(rt_scene *s, const rt_comm_id *id, int rank, int world, uint32_t tw, uint32_t th) {
+    if (!s || !id) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
+    if (world < 1 || rank < 0 || rank >= world) return fail(RT_ERR_INVALID_ARGUMENT, "rank must be in [0, world)");
+    if (tw == 0 || th == 0 || tw % 8 || th % 8) return fail(RT_ERR_INVALID_ARGUMENT, "tiles must be multiples of 8");
+    const Rccl &R = rccl();
+    if (!R.ok) return fail(RT_ERR_UNSUPPORTED, R.error);
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(drain(s));
+    s->release_comm();
+    auto *cm = new (std::nothrow) CommState();
+    if (!cm) return fail(RT_ERR_OUT_OF_MEMORY, "host allocation failed");
+    cm->rank = rank; cm->world = world; cm->tile_w = tw; cm->tile_h = th;
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    ncclResult_t e = R.CommInitRank(&cm->comm[0], world, u, rank);
+    for (int q = 1; q < CommState::NLANE && e == ncclSuccess; q++) e = R.CommSplit(cm->comm[0], 0, rank, &cm->comm[q], nullptr);
+    s->comm = cm;
+    if (e != ncclSuccess) {
+        const std::string msg = std::string("RCCL communicator: ") + R.GetErrorString(e);
+        s->release_comm();
+        return fail(RT_ERR_DEVICE, msg);
+    }
+    return RT_OK;
+}
+
+rt_status rt_scene_detach_comm(rt_scene *s) {
+    if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
+    if (!s->comm) return RT_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(drain(s));
+    s->release_comm();
+    return RT_OK;
+}
+
 rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uint8_t *rgba_host, float *rgb_host,
                     rt_stats *stats) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -843,6 +938,13 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     rt_render_opts o{};
     if (opts) o = *opts;
     if (o.frame_seed == 0) o.frame_seed = 0x5EED;
+    CommState *cm = s->comm;
+    if (cm) {                                  // multi-GPU frame: the communicator owns the tiling
+        if (o.tile_count) return fail(RT_ERR_INVALID_ARGUMENT, "tile options are set by rt_scene_attach_comm");
+        if (o.rgb32_device || rgb_host) return fail(RT_ERR_UNSUPPORTED, "rgb32 outputs are not gathered across ranks");
+        o.tile_w = cm->tile_w; o.tile_h = cm->tile_h;
+        o.tile_rank = (uint32_t)cm->rank; o.tile_count = (uint32_t)cm->world;
+    }
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t stream = o.stream ? static_cast<hipStream_t>(o.stream) : s->stream;
     double update_ms = 0.0;
@@ -853,6 +955,11 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         update_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - u0).count();
     }
 
+    // Launches of one lane never overlap, whatever streams callers pass (queue heads, unit costs).
+    // Without "overlap" every launch is lane 0.  With it, frames alternate lanes: a launch waits only
+    // for the previous launch of its own lane (and, below, for its frame block), so the caller can run
+    // consecutive frames concurrently on two streams.
+    const int q = s->overlap ? (int)s->lane : 0;
     OutputGPU out{};
     out.nt_store = s->nt_store;
     const uint32_t W = s->width, H = s->height;
@@ -870,8 +977,37 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         out.units = mine * (o.tile_w / 8) * (o.tile_h / 8);
         npix = (size_t)mine * o.tile_w * o.tile_h;
     }
-    // outputs: caller device buffers, else scene-owned
-    if (o.rgba8_device) {
+    // outputs: caller device buffers, else scene-owned; a rank of a multi-GPU frame traces into its lane's slab
+    uint8_t *frame_out = nullptr;              // multi-GPU, rank 0: the assembled frame
+    if (cm) {
+        const size_t slab_bytes = (size_t)slab_tile_count(W, H, cm->tile_w, cm->tile_h, (uint32_t)cm->world) * cm->tile_w *
+                                  cm->tile_h * 4;
+        if (slab_bytes != cm->slab_bytes) {    // first frame, or the camera size changed: lanes may be in flight
+            HIP_TRY(drain(s));
+            for (int l = 0; l < CommState::NLANE; l++) { cm->slab[l].release(); cm->gathered[l].release(); }
+            cm->slab_bytes = slab_bytes;
+        }
+        DevBuf<uint8_t> &buf = cm->rank == 0 ? cm->gathered[q] : cm->slab[q];
+        const size_t need = cm->rank == 0 ? slab_bytes * (size_t)cm->world : slab_bytes;
+        if (!buf.p) {
+            HIP_TRY(hipMalloc(&buf.p, need));
+            HIP_TRY(hipMemset(buf.p, 0, need));
+            buf.n = need;
+        }
+        out.rgba = buf.p;                      // rank 0: slab 0 of the gather buffer
+        if (cm->rank == 0) {
+            if (o.rgba8_device) {
+                frame_out = static_cast<uint8_t *>(o.rgba8_device);
+            } else {
+                if (s->out_rgba.n < (size_t)W * H * 4) {
+                    s->out_rgba.release();
+                    HIP_TRY(hipMalloc(&s->out_rgba.p, (size_t)W * H * 4));
+                    s->out_rgba.n = (size_t)W * H * 4;
+                }
+                frame_out = s->out_rgba.p;
+            }
+        }
+    } else if (o.rgba8_device) {
         out.rgba = static_cast<uint8_t *>(o.rgba8_device);
     } else {
         if (s->out_rgba.n < npix * 4) {
@@ -927,14 +1063,13 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             s->costmap_pixels = npix;
         }
     }
-    // Launches of one lane never overlap, whatever streams callers pass (queue heads, unit costs).
-    // Without "overlap" every launch is lane 0.  With it, frames alternate lanes: a launch waits only
-    // for the previous launch of its own lane (and, below, for its frame block), so the caller can run
-    // consecutive frames concurrently on two streams.
-    const int q = s->overlap ? (int)s->lane : 0;
     s->lane = s->overlap ? (s->lane + 1) % s->lanes : 0u;
     s->last_lane = q;
     HIP_TRY(hipStreamWaitEvent(stream, s->overlap ? s->ev_lane_done[q] : s->ev_render_done, 0));
+    unsigned long long *lane_counters = s->counters + (size_t)q * CNT_NUM;   // only this lane's launches add here
+    if (!(o.flags & RT_RENDER_KEEP_COUNTERS)) s->cnt_epoch++;
+    bool zero_lane = s->lane_epoch[q] != s->cnt_epoch;                      // cleared before this launch
+    s->lane_epoch[q] = s->cnt_epoch;
     bool reset_queue = true;
     if (s->use_persistent && s->reorder && s->grab == 64u) {
         DevBuf<uint32_t> &unit_cost = s->unit_cost[q], &unit_order = s->unit_order[q];
@@ -955,7 +1090,9 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         const int pc = s->pending_copy;
         HIP_TRY(launch_schedule(unit_cost.p, unit_order.p, s->queue[q], rows, upr, out.queue_parts, do_order,
                                 s->split & 0xFFu, (s->split >> 8) & 0xFFu, pc >= 0 ? s->frame_dev[pc] : nullptr,
-                                pc >= 0 ? s->staging_dev[pc] : nullptr, pc >= 0 ? s->frame_block : 0, stream));
+                                pc >= 0 ? s->staging_dev[pc] : nullptr, pc >= 0 ? s->frame_block : 0,
+                                zero_lane ? lane_counters : nullptr, stream));
+        zero_lane = false;
         if (pc >= 0) HIP_TRY(hipEventRecord(s->ev_copied[pc], stream));
         s->pending_copy = -1;
         std::memcpy(s->sched_sig[q], sig, sizeof sig);
@@ -970,17 +1107,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         s->pending_copy = -1;
     }
     HIP_TRY(hipStreamWaitEvent(stream, s->ev_copied[s->active], 0));
-    unsigned long long *lane_counters = s->counters + (size_t)q * CNT_NUM;   // only this lane's launches add here
-    if (!(o.flags & RT_RENDER_KEEP_COUNTERS)) {
-        // every lane's block: the counters restart from this frame (other lanes' blocks are reset behind
-        // their own last launch, so no in-flight add is lost into a cleared block)
-        HIP_TRY(hipMemsetAsync(lane_counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
-        for (int l = 0; l < rt_scene::NLANE; l++) {
-            if (l == q || !s->overlap) continue;
-            HIP_TRY(hipStreamWaitEvent(stream, s->ev_lane_done[l], 0));
-            HIP_TRY(hipMemsetAsync(s->counters + (size_t)l * CNT_NUM, 0, CNT_NUM * sizeof(unsigned long long), stream));
-        }
-    }
+    if (zero_lane) HIP_TRY(hipMemsetAsync(lane_counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
     const uint32_t slot = s->ring_head;
     s->ring_head = (s->ring_head + 1) % rt_scene::RING;
     if (s->ring_pending < rt_scene::RING) s->ring_pending++;
@@ -999,6 +1126,27 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, lane_counters, stream)
                       : launch_render_fast(g, cam, out, count, lane_counters, stream));
     HIP_TRY(hipEventRecord(s->ring_stop[slot], stream));
+    if (cm) {
+        // gather the ranks' slabs to rank 0 (grouped point-to-point over xGMI: each rank's bytes take
+        // their own link into rank 0), then scatter them into the frame there
+        const Rccl &R = rccl();
+        const size_t sb = cm->slab_bytes;
+        if (cm->world > 1) {
+            ncclResult_t e = R.GroupStart();
+            if (cm->rank == 0) {
+                for (int r = 1; r < cm->world && e == ncclSuccess; r++)
+                    e = R.Recv(cm->gathered[q].p + (size_t)r * sb, sb, ncclUint8, r, cm->comm[q], stream);
+            } else if (e == ncclSuccess) {
+                e = R.Send(cm->slab[q].p, sb, ncclUint8, 0, cm->comm[q], stream);
+            }
+            const ncclResult_t e2 = R.GroupEnd();
+            if (e != ncclSuccess || e2 != ncclSuccess)
+                return fail(RT_ERR_DEVICE, std::string("RCCL tile gather: ") + R.GetErrorString(e != ncclSuccess ? e : e2));
+        }
+        if (cm->rank == 0)
+            HIP_TRY(launch_assemble(cm->gathered[q].p, (uint32_t)(sb / (4ull * cm->tile_w * cm->tile_h)), cm->tile_w,
+                                    cm->tile_h, (uint32_t)cm->world, W, H, frame_out, stream));
+    }
     HIP_TRY(hipEventRecord(s->ev_used[s->active], stream));
     HIP_TRY(hipEventRecord(s->ev_render_done, stream));
     HIP_TRY(hipEventRecord(s->ev_lane_done[q], stream));
@@ -1009,7 +1157,8 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     HIP_TRY(hipMemcpyAsync(s->counters_host, lane_counters, CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
     HIP_TRY(hipStreamSynchronize(stream));
     s->ring_pending = 0;
-    if (rgba_host) HIP_TRY(hipMemcpy(rgba_host, out.rgba, npix * 4, hipMemcpyDeviceToHost));
+    if (rgba_host && cm && cm->rank == 0) HIP_TRY(hipMemcpy(rgba_host, frame_out, (size_t)W * H * 4, hipMemcpyDeviceToHost));
+    else if (rgba_host && !cm) HIP_TRY(hipMemcpy(rgba_host, out.rgba, npix * 4, hipMemcpyDeviceToHost));
     if (rgb_host) HIP_TRY(hipMemcpy(rgb_host, out.rgb, npix * 3 * sizeof(float), hipMemcpyDeviceToHost));
     if (stats) {
         float kms = 0.0f;
@@ -1196,11 +1345,14 @@ rt_status rt_scene_collect(rt_scene *s, rt_stats *acc, float *kernel_ms, uint32_
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(drain(s));
     HIP_TRY(hipMemcpy(s->counters_host, s->counters, rt_scene::NLANE * CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    for (int l = 1; l < rt_scene::NLANE; l++)          // sum the lanes' blocks into lane 0's slot
-        for (uint32_t k = 0; k < CNT_NUM; k++) s->counters_host[k] += s->counters_host[(size_t)l * CNT_NUM + k];
-    if (acc) fill_stats(acc, s->counters_host);
-    // collected: the next KEEP_COUNTERS frames accumulate from zero
+    unsigned long long sum[CNT_NUM] = {};
+    for (int l = 0; l < rt_scene::NLANE; l++)          // lanes whose block belongs to the current epoch
+        if (s->lane_epoch[l] == s->cnt_epoch)
+            for (uint32_t k = 0; k < CNT_NUM; k++) sum[k] += s->counters_host[(size_t)l * CNT_NUM + k];
+    if (acc) fill_stats(acc, sum);
+    // collected: the next KEEP_COUNTERS frames accumulate from zero (every block is clear and current)
     HIP_TRY(hipMemset(s->counters, 0, rt_scene::NLANE * CNT_NUM * sizeof(unsigned long long)));
+    for (uint64_t &e : s->lane_epoch) e = s->cnt_epoch;
     const uint32_t n = s->ring_pending;
     uint32_t written = 0;
     for (uint32_t k = 0; k < n; k++) {

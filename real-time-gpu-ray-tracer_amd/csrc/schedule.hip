@@ -53,78 +53,101 @@ __device__ __forceinline__ uint32_t split_log2(uint32_t cls, uint32_t k_half, ui
     return k >= k_quarter ? 2u : (k >= k_half ? 1u : 0u);
 }
 
+constexpr uint32_t SCHED_LDS_UNITS = 32768;  // units per band whose cost classes are kept in LDS (1 B each)
+constexpr uint32_t SCHED_LOAD_BATCH = 8;          // cost loads issued back to back per thread
+
 __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__restrict__ cost, uint32_t *__restrict__ order,
                                                                  uint32_t *__restrict__ queue, uint32_t rows,
                                                                  uint32_t upr, uint32_t parts, uint32_t do_order,
                                                                  uint32_t k_half, uint32_t k_quarter, uint4 *copy_dst,
-                                                                 const uint4 *copy_src, uint32_t copy_n16) {
+                                                                 const uint4 *copy_src, uint32_t copy_n16,
+                                                                 unsigned long long *zero_counters) {
     __shared__ uint32_t cnt[SCHED_CLASSES][SCHED_THREADS];   // per-thread class counts -> exclusive offsets
+    __shared__ uint8_t cls_of[SCHED_LDS_UNITS];              // class of each unit of the band (pass 1 -> pass 2)
     __shared__ uint32_t total[SCHED_CLASSES];
     __shared__ uint32_t base[SCHED_CLASSES];
     const uint32_t part = blockIdx.x, t = threadIdx.x;
     if (part == 0 && t < QUEUE_MAX_PARTS) queue[t * QUEUE_STRIDE] = 0u;      // every head: `parts` may change
+    if (part == 0 && zero_counters && t < CNT_NUM) zero_counters[t] = 0ull;  // the lane's work counters
     // the frame's TLAS / instance block, read from pinned host staging (see launch_frame_copy)
     for (uint32_t i = part * SCHED_THREADS + t; i < copy_n16; i += parts * SCHED_THREADS) copy_dst[i] = copy_src[i];
     // the band's unit range, computed exactly as the render kernel computes it
     const uint32_t b0 = rows * part / parts * upr, b1 = rows * (part + 1) / parts * upr;
     const uint32_t n = b1 - b0, per = (n + SCHED_THREADS - 1) / SCHED_THREADS;
     const uint32_t lo = b0 + min(n, t * per), hi = b0 + min(n, (t + 1) * per);
-    if (do_order) {
-        for (int c = 0; c < SCHED_CLASSES; c++) cnt[c][t] = 0u;
-        for (uint32_t u = lo; u < hi; u++) {
-            const uint32_t c = cost_class(cost[u]);
+    if (!do_order) {
+        for (uint32_t u = lo; u < hi; u++) cost[u] = 0u;
+        return;
+    }
+    const bool lds_cls = n <= SCHED_LDS_UNITS;
+    for (int c = 0; c < SCHED_CLASSES; c++) cnt[c][t] = 0u;
+    // pass 1: classes and per-thread item counts; the costs are read in batches of independent loads
+    // (this kernel runs beside another lane's launch: each dependent round trip is ~1-2 us there) and
+    // cleared for the next launch
+    for (uint32_t u0 = lo; u0 < hi; u0 += SCHED_LOAD_BATCH) {
+        uint32_t cv[SCHED_LOAD_BATCH];
+#pragma unroll
+        for (uint32_t k = 0; k < SCHED_LOAD_BATCH; k++) cv[k] = u0 + k < hi ? cost[u0 + k] : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < SCHED_LOAD_BATCH; k++) {
+            if (u0 + k >= hi) break;
+            const uint32_t c = cost_class(cv[k]);
+            if (lds_cls) cls_of[u0 + k - b0] = (uint8_t)c;
             cnt[c][t] += 1u << split_log2(c, k_half, k_quarter);
-        }
-        __syncthreads();
-        // exclusive scan of each class's item counts over the threads (thread order = screen order):
-        // wave w scans classes [4w, 4w + 4), each lane SCAN_PER_LANE consecutive threads' counts
-        const uint32_t w = t >> 6, lane = t & 63u;
-        for (int cc = 0; cc < SCHED_CLASSES / SCHED_WAVES; cc++) {
-            const uint32_t c = w * (SCHED_CLASSES / SCHED_WAVES) + cc;
-            uint32_t local[SCAN_PER_LANE], run = 0;
-#pragma unroll
-            for (int k = 0; k < SCAN_PER_LANE; k++) { local[k] = run; run += cnt[c][lane * SCAN_PER_LANE + k]; }
-            uint32_t incl = run;
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const uint32_t y = __shfl_up(incl, off, 64);
-                if (lane >= (uint32_t)off) incl += y;
-            }
-            const uint32_t excl = incl - run;
-#pragma unroll
-            for (int k = 0; k < SCAN_PER_LANE; k++) cnt[c][lane * SCAN_PER_LANE + k] = excl + local[k];
-            if (lane == 63u) total[c] = incl;
-        }
-        __syncthreads();
-        if (t == 0) {
-            uint32_t acc = 0;
-            for (int c = 0; c < SCHED_CLASSES; c++) { base[c] = acc; acc += total[c]; }
-            queue[(QUEUE_MAX_PARTS + part) * QUEUE_STRIDE] = acc;   // items in the band (own line)
-        }
-        __syncthreads();
-        // items of the band: [4 b0, 4 b0 + items) — at most 4 per unit
-        uint32_t *items = order + 4u * b0;
-        for (uint32_t u = lo; u < hi; u++) {
-            const uint32_t c = cost_class(cost[u]), ls = split_log2(c, k_half, k_quarter);
-            const uint32_t at = base[c] + cnt[c][t];
-            for (uint32_t k = 0; k < (1u << ls); k++) items[at + k] = (u << 4) | (k << 2) | ls;
-            cnt[c][t] = at - base[c] + (1u << ls);
+            if (lds_cls) cost[u0 + k] = 0u;
         }
     }
-    for (uint32_t u = lo; u < hi; u++) cost[u] = 0u;
+    __syncthreads();
+    // exclusive scan of each class's item counts over the threads (thread order = screen order):
+    // wave w scans classes [4w, 4w + 4), each lane SCAN_PER_LANE consecutive threads' counts
+    const uint32_t w = t >> 6, lane = t & 63u;
+    for (int cc = 0; cc < SCHED_CLASSES / SCHED_WAVES; cc++) {
+        const uint32_t c = w * (SCHED_CLASSES / SCHED_WAVES) + cc;
+        uint32_t local[SCAN_PER_LANE], run = 0;
+#pragma unroll
+        for (int k = 0; k < SCAN_PER_LANE; k++) { local[k] = run; run += cnt[c][lane * SCAN_PER_LANE + k]; }
+        uint32_t incl = run;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, 64);
+            if (lane >= (uint32_t)off) incl += y;
+        }
+        const uint32_t excl = incl - run;
+#pragma unroll
+        for (int k = 0; k < SCAN_PER_LANE; k++) cnt[c][lane * SCAN_PER_LANE + k] = excl + local[k];
+        if (lane == 63u) total[c] = incl;
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t acc = 0;
+        for (int c = 0; c < SCHED_CLASSES; c++) { base[c] = acc; acc += total[c]; }
+        queue[(QUEUE_MAX_PARTS + part) * QUEUE_STRIDE] = acc;   // items in the band (own line)
+    }
+    __syncthreads();
+    // pass 2: items of the band: [4 b0, 4 b0 + items) — at most 4 per unit
+    uint32_t *items = order + 4u * b0;
+    for (uint32_t u = lo; u < hi; u++) {
+        const uint32_t c = lds_cls ? (uint32_t)cls_of[u - b0] : cost_class(cost[u]), ls = split_log2(c, k_half, k_quarter);
+        const uint32_t at = base[c] + cnt[c][t];
+        for (uint32_t k = 0; k < (1u << ls); k++) items[at + k] = (u << 4) | (k << 2) | ls;
+        cnt[c][t] = at - base[c] + (1u << ls);
+    }
+    if (!lds_cls)
+        for (uint32_t u = lo; u < hi; u++) cost[u] = 0u;
 }
 
 }  // namespace
 
 // rows x upr units per frame split into `parts` bands as in render_persistent_body; do_order = 0 only
 // clears the costs and the queue heads (first launch of a layout: no costs recorded yet).
+// zero_counters (optional): CNT_NUM device counters cleared before the launch that follows.
 hipError_t launch_schedule(uint32_t *cost, uint32_t *order, uint32_t *queue, uint32_t rows, uint32_t upr,
                            uint32_t parts, bool do_order, uint32_t k_half, uint32_t k_quarter, void *copy_dst,
-                           const void *copy_src, size_t copy_bytes, hipStream_t stream) {
+                           const void *copy_src, size_t copy_bytes, unsigned long long *zero_counters, hipStream_t stream) {
     if (parts == 0 || parts > QUEUE_MAX_PARTS || copy_bytes % 16) return hipErrorInvalidValue;
     hipLaunchKernelGGL(schedule_kernel, dim3(parts), dim3(SCHED_THREADS), 0, stream, cost, order, queue, rows, upr, parts,
                        do_order ? 1u : 0u, k_half, k_quarter, static_cast<uint4 *>(copy_dst),
-                       static_cast<const uint4 *>(copy_src), (uint32_t)(copy_bytes / 16));
+                       static_cast<const uint4 *>(copy_src), (uint32_t)(copy_bytes / 16), zero_counters);
     return hipGetLastError();
 }
 

@@ -127,6 +127,11 @@ class SceneInfo(C.Structure):
                 ("tlas_height", C.c_uint32), ("blas_height_max", C.c_uint32)]
 
 
+class CommId(C.Structure):
+    """rt_comm_id (= ncclUniqueId, 128 opaque bytes)."""
+    _fields_ = [("internal", C.c_char * 128)]
+
+
 class VtkInfo(C.Structure):
     _fields_ = [("point_count", C.c_uint64), ("particle_count", C.c_uint64),
                 ("strip_vertex_count", C.c_uint64), ("triangle_count", C.c_uint64)]
@@ -146,6 +151,7 @@ EXPORTED_SYMBOLS = (
     "rt_scene_collect", "rt_scene_debug_read", "rt_scene_update_triangles", "rt_scene_update_instances",
     "rt_vtk_read", "rt_vtk_free", "rt_vtk_get_info", "rt_vtk_particles", "rt_vtk_vertices", "rt_vtk_convert",
     "rt_vtk_series_read", "rt_vtk_series_count", "rt_vtk_series_entry", "rt_vtk_series_free",
+    "rt_comm_unique_id", "rt_scene_attach_comm", "rt_scene_detach_comm", "rt_slab_tiles", "rt_tile_pixels",
 )
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -208,6 +214,14 @@ def _declare(lib):
     lib.rt_vtk_series_free.restype = None
     for name in ("rt_vtk_read", "rt_vtk_get_info", "rt_vtk_particles", "rt_vtk_vertices", "rt_vtk_convert",
                  "rt_vtk_series_read", "rt_vtk_series_entry"):
+        getattr(lib, name).restype = C.c_int
+    lib.rt_comm_unique_id.argtypes = [P(CommId)]
+    lib.rt_scene_attach_comm.argtypes = [C.c_void_p, P(CommId), C.c_int, C.c_int, C.c_uint32, C.c_uint32]
+    lib.rt_scene_detach_comm.argtypes = [C.c_void_p]
+    lib.rt_slab_tiles.argtypes = [C.c_uint32] * 5
+    lib.rt_slab_tiles.restype = C.c_uint32
+    lib.rt_tile_pixels.argtypes = [C.c_uint32] * 6 + [C.c_uint64, C.c_uint64, C.c_void_p]
+    for name in ("rt_comm_unique_id", "rt_scene_attach_comm", "rt_scene_detach_comm", "rt_tile_pixels"):
         getattr(lib, name).restype = C.c_int
     lib.rt_demo_update.argtypes = [C.c_void_p, P(Xform), C.c_size_t, C.c_uint64]
     lib.rt_demo_update.restype = None

@@ -85,6 +85,9 @@ class Renderer:
         o.flags = (abi.RT_RENDER_EXACT if exact else 0) | (abi.RT_RENDER_COUNT_WORK if count_work else 0) | \
                   (abi.RT_RENDER_SKIP_UPDATE if skip_update else 0) | (0 if sync else abi.RT_RENDER_NO_SYNC) | \
                   (abi.RT_RENDER_KEEP_COUNTERS if keep_counters else 0)
+        comm = getattr(self, "comm", None)
+        if comm is not None and comm[0] != 0:
+            want_rgba = False                     # only rank 0 receives the assembled frame
         if tiles is not None:
             o.tile_w, o.tile_h, o.tile_rank, o.tile_count = tiles
             npix = self.tiles_for_rank(*tiles) * tiles[0] * tiles[1]
@@ -145,6 +148,28 @@ class Renderer:
     def assemble_tiles(self, gathered_device, slab_tiles, tile_w, tile_h, tile_count, frame_device, stream=None):
         abi.check(self.lib, self.lib.rt_assemble_tiles(self.h, gathered_device, slab_tiles, tile_w, tile_h,
                                                        tile_count, frame_device, stream))
+
+    # ---- multi-GPU frames (rt_scene_attach_comm) ---------------------------------------------
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        """Rank 0: a fresh RCCL unique id (128 bytes) to hand to every rank out of band."""
+        lib = abi.load_library()
+        cid = abi.CommId()
+        abi.check(lib, lib.rt_comm_unique_id(C.byref(cid)))
+        return bytes(bytearray(cid))
+
+    def attach_comm(self, comm_id: bytes, rank: int, world: int, tile_w: int = 64, tile_h: int = 64):
+        """Make this scene rank `rank` of a `world`-GPU frame: render() traces this rank's tiles, gathers
+        them to rank 0 over RCCL and assembles the frame there (collective over the ranks)."""
+        cid = abi.CommId.from_buffer_copy(bytes(comm_id))
+        abi.check(self.lib, self.lib.rt_scene_attach_comm(self.h, C.byref(cid), rank, world, tile_w, tile_h))
+        self.comm = (rank, world, tile_w, tile_h)
+        return self
+
+    def detach_comm(self):
+        abi.check(self.lib, self.lib.rt_scene_detach_comm(self.h))
+        self.comm = None
+        return self
 
     def trace_rays(self, rays, exact: bool = False):
         rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)

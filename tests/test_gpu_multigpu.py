@@ -1,0 +1,70 @@
+"""The multi-GPU frame inside the library (rt_scene_attach_comm) on one GPU.
+
+A world-1 communicator runs the whole multi-GPU code path of rt_render — the rank's tiles traced
+into the gather buffer, the (empty) RCCL group, the assemble kernel into rank 0's frame — so the
+frame must equal the single-launch frame byte for byte, with and without overlapped lanes.
+(World > 1 needs one GPU per rank: RCCL rejects two ranks on one device; the driver's 8-GPU bench
+runs it, and tests/test_multirank_cpu.py checks the gather protocol with the library's tile
+bookkeeping on CPU.)
+"""
+import numpy as np
+import pytest
+
+from rtamd import Renderer, abi, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def test_world1_comm_frames_equal_single_launch(gpu_lib):
+    import torch
+    s = scenes.demo_with_particles(10)
+    W, H = 400, 232
+    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(W, H, ray_trace_depth=2)
+    ref = [r.render(f)[0] for f in range(6)]
+    cid = Renderer.comm_unique_id()
+    assert len(cid) == 128
+    for tw, th in ((64, 64), (32, 16)):
+        r.attach_comm(cid if (tw, th) == (64, 64) else Renderer.comm_unique_id(), 0, 1, tw, th)
+        for f in range(3):
+            rgba, _, st = r.render(f)
+            assert np.array_equal(rgba, ref[f]), (tw, th, f)
+            assert st["pixels"] == W * H
+        # overlapped lanes on two caller streams, device outputs
+        r.set_option("overlap", 2)
+        lanes = [torch.cuda.Stream() for _ in range(2)]
+        bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(6)]
+        torch.cuda.synchronize()
+        for f in range(6):
+            r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=lanes[f % 2].cuda_stream,
+                     sync=False, keep_counters=True)
+        r.synchronize()
+        torch.cuda.synchronize()
+        for f in range(6):
+            assert np.array_equal(bufs[f].cpu().numpy().reshape(H, W, 4), ref[f]), (tw, th, f)
+        r.set_option("overlap", 0)
+        r.detach_comm()
+    assert np.array_equal(r.render(2)[0], ref[2])       # detached: whole-frame launches again
+
+
+def test_comm_rejects_tiles_and_rgb(gpu_lib):
+    s = scenes.demo_scene()
+    r = Renderer(s).build_acceleration_structure(0).configure_camera(64, 64)
+    r.attach_comm(Renderer.comm_unique_id(), 0, 1)
+    with pytest.raises(abi.RtError, match="tile"):
+        r.render(0, tiles=(64, 64, 0, 2))
+    with pytest.raises(abi.RtError, match="rgb32"):
+        r.render(0, want_rgb=True)
+    with pytest.raises(abi.RtError):
+        r.attach_comm(Renderer.comm_unique_id(), 1, 1)      # rank outside [0, world)
+
+
+def test_c4_through_the_comm_path(gpu_lib):
+    """C4's scene and settings through the library's multi-GPU path (world 1): the assembled frame
+    equals the single-launch frame."""
+    cfg = scenes.CONFIGS["C4"]
+    s = scenes.config_scene(scenes.CONFIGS["C3"])
+    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(
+        cfg.width, cfg.height, sample_count=cfg.spp, ray_trace_depth=cfg.depth)
+    full = r.render(0)[0]
+    r.attach_comm(Renderer.comm_unique_id(), 0, 1, 64, 64)
+    assert np.array_equal(r.render(0)[0], full)

@@ -28,16 +28,14 @@ def _free_port():
 
 
 def _render_slab(o, rank, count):
-    st = tiles.slab_tiles(W, H, TW, TH, count)
-    slab = np.zeros((st * TW * TH, 4), np.uint8)
-    for k, t in enumerate(tiles.rank_tiles(W, H, TW, TH, rank, count)):
+    """The rank's tiles traced by the oracle (the checker stands in for the GPU here), packed into the
+    padded slab with the library's slab -> frame mapping (rt_tile_pixels, the assemble kernel's)."""
+    canvas = np.zeros((H, W, 4), np.uint8)
+    for t in tiles.rank_tiles(W, H, TW, TH, rank, count):
         x0, y0 = tiles.tile_origin(t, W, TW, TH)
         w, h = min(TW, W - x0), min(TH, H - y0)
-        _, rgba, _ = o.render(region=(x0, y0, w, h), threads=2, want_rgb=False)
-        tile = np.zeros((TH, TW, 4), np.uint8)
-        tile[:h, :w] = rgba
-        slab[k * TW * TH:(k + 1) * TW * TH] = tile.reshape(-1, 4)
-    return slab
+        canvas[y0:y0 + h, x0:x0 + w] = o.render(region=(x0, y0, w, h), threads=2, want_rgb=False)[1]
+    return tiles.pack(lambda: canvas, W, H, TW, TH, rank, count)
 
 
 def _worker(rank, world, port, result_path):
@@ -162,10 +160,21 @@ def test_tile_gather_assemble_gloo(tmp_path, world):
 
 
 def test_tile_bookkeeping_covers_frame_once():
-    for count in (1, 2, 3, 8):
-        seen = np.zeros(tiles.tiles_xy(W, H, TW, TH), int).T.ravel()
-        for r in range(count):
-            for t in tiles.rank_tiles(W, H, TW, TH, r, count):
-                seen[t] += 1
-        assert (seen == 1).all()
-        assert sum(tiles.tiles_for_rank(W, H, TW, TH, r, count) for r in range(count)) == seen.size
+    """The library's slab -> frame mapping (rt_tile_pixels) puts every frame pixel in exactly one slab
+    pixel of exactly one rank, agrees with the row-major tile restatement, and rt_slab_tiles is the
+    largest rank's tile count."""
+    for w, h in ((W, H), (1920, 1080), (64, 64), (65, 7)):
+        for count in (1, 2, 3, 8):
+            seen = np.zeros((h, w), int)
+            st = tiles.slab_tiles(w, h, TW, TH, count)
+            assert st == max(tiles.tiles_for_rank(w, h, TW, TH, r, count) for r in range(count))
+            for r in range(count):
+                xy = tiles.slab_pixels(w, h, TW, TH, r, count)
+                assert xy.shape == (st * TW * TH, 2)
+                ok = xy[:, 0] >= 0
+                np.add.at(seen, (xy[ok, 1], xy[ok, 0]), 1)
+                for k, t in enumerate(tiles.rank_tiles(w, h, TW, TH, r, count)[:3]):
+                    x0, y0 = tiles.tile_origin(t, w, TW, TH)
+                    p = xy[k * TW * TH]
+                    assert tuple(p) == (x0, y0)
+            assert (seen == 1).all(), (w, h, count)
