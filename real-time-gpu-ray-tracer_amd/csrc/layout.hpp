@@ -190,9 +190,35 @@ struct OutputGPU {
     // largest cost (traversal rounds + 1) of unit u's pixels for the next launch's order
     const uint32_t *order;
     uint32_t *unit_cost;
+    // fused schedule (option "reorder"): the last workgroup of the launch to finish turns unit_cost into
+    // the next launch's claim order (written to `order_next`, the band item counts and reset heads into
+    // `queue`), copies the costs to cost_prev (debug) and clears them; null = no schedule
+    uint32_t *sched_done;           // arrival counter of the launch's workgroups
+    uint32_t *order_next;
+    uint32_t *cost_prev;
+    uint32_t split_half, split_quarter;
 };
 constexpr uint32_t QUEUE_STRIDE = 32;         // u32 words between partition heads (128 B lines)
 constexpr uint32_t QUEUE_MAX_PARTS = 8;
+// queue block of a lane: band heads (lines 0..7), band item counts (lines 8..15), arrival counter (line 16)
+constexpr uint32_t QUEUE_DONE_WORD = 2 * QUEUE_MAX_PARTS * QUEUE_STRIDE;
+constexpr uint32_t QUEUE_WORDS = QUEUE_DONE_WORD + QUEUE_STRIDE;
+constexpr uint32_t SCHED_CLASSES = 16;       // cost classes of the claim order (half-octaves of steps per pixel)
+
+// class 0 = heaviest: half-octaves of a unit's mean traversal steps per pixel, floor(2 log2(c/64 + 1))
+// (a sky unit averages ~5 steps per pixel, a unit over the particle cluster ~100; classes saturate at ~180);
+// in integers: 2 log2(x/64) = log2(x^2) - 12 with x = c + 64
+__host__ __device__ inline uint32_t cost_class(uint32_t c) {
+    const uint64_t x = (uint64_t)c + 64u;
+    const int k = (63 - __builtin_clzll(x * x)) - 12;
+    return (SCHED_CLASSES - 1) - (uint32_t)(k < 0 ? 0 : (k > (int)SCHED_CLASSES - 1 ? (int)SCHED_CLASSES - 1 : k));
+}
+// heavy units may be claimed in pieces so that several waves share them: 1/4 of a unit (16 pixels)
+// from class level k_quarter up, 1/2 from k_half up (levels k = 15 - class; > 15 = never)
+__host__ __device__ inline uint32_t split_log2(uint32_t cls, uint32_t k_half, uint32_t k_quarter) {
+    const uint32_t k = (SCHED_CLASSES - 1) - cls;
+    return k >= k_quarter ? 2u : (k >= k_half ? 1u : 0u);
+}
 constexpr uint32_t TIMELINE_WORDS = 16;
 constexpr uint32_t LEAN_STACK = 24;       // LDS stack entries of the lean traversal
 

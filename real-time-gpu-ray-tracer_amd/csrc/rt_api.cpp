@@ -35,9 +35,7 @@ hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, c
                                           uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
-hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t, uint32_t,
-                           void *, const void *, size_t, unsigned long long *, hipStream_t);
-hipError_t launch_frame_copy(void *, const void *, size_t, hipStream_t);
+hipError_t launch_frame_copy(void *, const void *, size_t, unsigned long long *, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean, bool wide);
 hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, uint32_t, hipStream_t);
 uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean, bool wide);
@@ -204,8 +202,9 @@ struct rt_scene {
     bool reorder = true;
     uint32_t split = 10u | 12u << 8;  // heavy-unit pieces: class level for halves | quarters << 8 (0xFF = never)
     DevBuf<uint32_t> unit_cost[NLANE], unit_order[NLANE];
-    uint32_t sched_sig[NLANE][7] = {};  // launch layout the recorded costs belong to
+    uint32_t sched_sig[NLANE][7] = {};  // layout of the lane's last launch: the order it built is for this layout
     bool sched_valid[NLANE] = {};
+    bool heads_zero[NLANE] = {};        // the lane's last launch reset its queue heads (fused schedule)
     DevBuf<uint32_t> costmap;
     size_t costmap_pixels = 0;
     DevBuf<unsigned long long> timeline;
@@ -378,7 +377,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         uint8_t *fd = s->frame_dev[b];
         HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_used[b], 0));
         // a blit kernel reading the pinned staging block, not an SDMA copy (see the host-built path below)
-        HIP_TRY(launch_frame_copy(fd, s->staging_dev[b], s->frame_block, s->stream));
+        HIP_TRY(launch_frame_copy(fd, s->staging_dev[b], s->frame_block, nullptr, s->stream));
         if (s->rebuild_blas || s->blas_dirty) {
             const rt_status bs = gpu_build_blas(s);
             if (bs != RT_OK) return bs;
@@ -693,6 +692,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
     for (bool &v : s->sched_valid) v = false;
+    for (bool &v : s->heads_zero) v = false;
     if (mode == RT_BUILD_LBVH) {
         if ((st = gpu_setup_blas(s, segs, slot_base)) != RT_OK) return st;
     } else {
@@ -793,8 +793,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     }
     for (int q = 0; q < rt_scene::NLANE; q++) {
         if (!s->queue[q]) {   // band heads, then (option "reorder") band item counts, one 128 B line each
-            HIP_TRY(hipMalloc(&s->queue[q], 2 * QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t)));
-            HIP_TRY(hipMemset(s->queue[q], 0, 2 * QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t)));
+            HIP_TRY(hipMalloc(&s->queue[q], QUEUE_WORDS * sizeof(uint32_t)));
+            HIP_TRY(hipMemset(s->queue[q], 0, QUEUE_WORDS * sizeof(uint32_t)));
         }
         if (!s->ev_lane_done[q]) HIP_TRY(hipEventCreateWithFlags(&s->ev_lane_done[q], hipEventDisableTiming));
     }
@@ -989,9 +989,8 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         }
         DevBuf<uint8_t> &buf = cm->rank == 0 ? cm->gathered[q] : cm->slab[q];
         const size_t need = cm->rank == 0 ? slab_bytes * (size_t)cm->world : slab_bytes;
-        if (!buf.p) {
+        if (!buf.p) {                          // slab padding is never assembled: no clearing needed
             HIP_TRY(hipMalloc(&buf.p, need));
-            HIP_TRY(hipMemset(buf.p, 0, need));
             buf.n = need;
         }
         out.rgba = buf.p;                      // rank 0: slab 0 of the gather buffer
@@ -1070,41 +1069,40 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     if (!(o.flags & RT_RENDER_KEEP_COUNTERS)) s->cnt_epoch++;
     bool zero_lane = s->lane_epoch[q] != s->cnt_epoch;                      // cleared before this launch
     s->lane_epoch[q] = s->cnt_epoch;
-    bool reset_queue = true;
-    if (s->use_persistent && s->reorder && s->grab == 64u) {
+    // the lane's queue heads are zero after a launch that built a schedule (its last workgroup resets them)
+    bool reset_queue = !s->heads_zero[q];
+    const bool fused_schedule = s->use_persistent && s->reorder && s->grab == 64u;
+    if (fused_schedule) {
         DevBuf<uint32_t> &unit_cost = s->unit_cost[q], &unit_order = s->unit_order[q];
-        if (unit_cost.n < out.units) {
+        if (unit_cost.n < 2 * (size_t)out.units) {        // [recorded costs | costs of the last launch (debug)]
             unit_cost.release();
             unit_order.release();
-            HIP_TRY(hipMalloc(&unit_cost.p, out.units * sizeof(uint32_t)));
-            unit_cost.n = out.units;
+            HIP_TRY(hipMalloc(&unit_cost.p, 2 * (size_t)out.units * sizeof(uint32_t)));
+            unit_cost.n = 2 * (size_t)out.units;
+            HIP_TRY(hipMemsetAsync(unit_cost.p, 0, unit_cost.n * sizeof(uint32_t), stream));
             HIP_TRY(hipMalloc(&unit_order.p, 4 * (size_t)out.units * sizeof(uint32_t)));   // <= 4 items per unit
             unit_order.n = 4 * (size_t)out.units;
             s->sched_valid[q] = false;
         }
         const uint32_t sig[7] = {out.units, out.units_x, out.tile_w, out.tile_h, out.tile_rank, out.tile_count,
                                  out.queue_parts};
+        // the order the lane's previous launch built is for the layout it had
         const bool do_order = s->sched_valid[q] && std::memcmp(sig, s->sched_sig[q], sizeof sig) == 0;
-        const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
-        const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
-        const int pc = s->pending_copy;
-        HIP_TRY(launch_schedule(unit_cost.p, unit_order.p, s->queue[q], rows, upr, out.queue_parts, do_order,
-                                s->split & 0xFFu, (s->split >> 8) & 0xFFu, pc >= 0 ? s->frame_dev[pc] : nullptr,
-                                pc >= 0 ? s->staging_dev[pc] : nullptr, pc >= 0 ? s->frame_block : 0,
-                                zero_lane ? lane_counters : nullptr, stream));
-        zero_lane = false;
-        if (pc >= 0) HIP_TRY(hipEventRecord(s->ev_copied[pc], stream));
-        s->pending_copy = -1;
         std::memcpy(s->sched_sig[q], sig, sizeof sig);
-        s->sched_valid[q] = true;
         out.order = do_order ? unit_order.p : nullptr;
         out.unit_cost = unit_cost.p;
-        reset_queue = false;
+        out.cost_prev = unit_cost.p + out.units;
+        out.order_next = unit_order.p;
+        out.sched_done = s->queue[q] + QUEUE_DONE_WORD;
+        out.split_half = s->split & 0xFFu;
+        out.split_quarter = (s->split >> 8) & 0xFFu;
     }
-    if (s->pending_copy >= 0) {                // no schedule launch carried the upload
-        HIP_TRY(launch_frame_copy(s->frame_dev[s->pending_copy], s->staging_dev[s->pending_copy], s->frame_block, stream));
+    if (s->pending_copy >= 0) {                // the frame block's upload (and the lane's counter reset)
+        HIP_TRY(launch_frame_copy(s->frame_dev[s->pending_copy], s->staging_dev[s->pending_copy], s->frame_block,
+                                  zero_lane ? lane_counters : nullptr, stream));
         HIP_TRY(hipEventRecord(s->ev_copied[s->pending_copy], stream));
         s->pending_copy = -1;
+        zero_lane = false;
     }
     HIP_TRY(hipStreamWaitEvent(stream, s->ev_copied[s->active], 0));
     if (zero_lane) HIP_TRY(hipMemsetAsync(lane_counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
@@ -1121,6 +1119,8 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
                                                        s->variant, false, reset_queue, stream)
                       : launch_render_persistent_fast(g, cam, out, count, lane_counters, s->queue[q], blocks, s->threshold,
                                                       s->variant, lean, reset_queue, stream));
+        s->heads_zero[q] = fused_schedule;
+        if (fused_schedule) s->sched_valid[q] = true;
     }
     else
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, lane_counters, stream)
@@ -1314,8 +1314,9 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
         return RT_OK;
     } else if (k == "unit_cost" || k == "unit_order") {
         const int q = s->last_lane;
-        src = k == "unit_cost" ? s->unit_cost[q].p : s->unit_order[q].p;
-        size = s->sched_valid[q] ? (size_t)s->sched_sig[q][0] * (k == "unit_cost" ? 1 : 4) * sizeof(uint32_t) : 0;
+        const size_t units = s->sched_sig[q][0];
+        src = k == "unit_cost" ? s->unit_cost[q].p + units : s->unit_order[q].p;
+        size = s->sched_valid[q] ? units * (k == "unit_cost" ? 1 : 4) * sizeof(uint32_t) : 0;
     } else {
         return fail(RT_ERR_INVALID_ARGUMENT, "unknown debug buffer " + k);
     }

@@ -15,7 +15,7 @@ run() {  # name timeout cmd...
 }
 STEPS=${STEPS:-smoke,tests,bench,prof}
 [[ $STEPS == *smoke* ]] && run smoke 400 python -c "import __graft_entry__ as g; g.smoke()"
-[[ $STEPS == *tests* ]] && run gpu_tests 900 python -u -m pytest tests -m gpu -v -rf --timeout 120 --timeout-method thread ${TEST_ARGS:-}
+[[ $STEPS == *tests* ]] && run gpu_tests 900 python -u -m pytest ${TEST_ARGS:-tests} -m gpu -v -rf --timeout 120 --timeout-method thread
 [[ $STEPS == *ab* ]] && run ab 600 python scripts/ab_kernels.py ${AB_ARGS:-grid:kernel=0 p8:kernel=1,threshold=8 p16:kernel=1,threshold=16 p24:kernel=1,threshold=24 p32:kernel=1,threshold=32 p48:kernel=1,threshold=48}
 [[ $STEPS == *timeline* ]] && run timeline 300 python scripts/timeline.py ${TL_ARGS:-}
 [[ $STEPS == *bench* ]] && run bench 600 python bench.py

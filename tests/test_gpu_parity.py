@@ -264,7 +264,7 @@ def test_pipelined_frames_collect(gpu_lib):
 
 
 def _sched_class(c):
-    """schedule.hip cost_class: 0 = heaviest (half-octaves of the mean traversal steps per pixel)."""
+    """layout.hpp cost_class: 0 = heaviest (half-octaves of the mean traversal steps per pixel)."""
     x = c.astype(np.uint64) + 64
     k = np.array([int(v * v).bit_length() - 1 - 12 for v in x.tolist()], np.int64)
     return 15 - np.clip(k, 0, 15)
@@ -272,8 +272,9 @@ def _sched_class(c):
 
 @pytest.mark.parametrize("exact", [False, True])
 def test_reorder_schedule_is_byte_identical(gpu_lib, exact):
-    """Option "reorder" (claims ordered heaviest-unit-first from the previous frame's unit costs,
-    csrc/schedule.hip) changes only which wave traces which pixel: every frame is byte-identical
+    """Option "reorder" (claims ordered heaviest-unit-first from the previous frame's unit costs, built by
+    the previous launch's last workgroup: build_schedule in csrc/trace_kernel.hip) changes only which
+    wave traces which pixel: every frame is byte-identical
     to the screen-order walk (whole frame and a tile shard), and each launch's order is a stable,
     class-sorted permutation of every XCD band's units."""
     s = scenes.demo_with_particles(12)
@@ -286,35 +287,33 @@ def test_reorder_schedule_is_byte_identical(gpu_lib, exact):
         ref[f] = r.render(f, exact=exact, want_rgb=True)
     tref = r.render(3, exact=exact, tiles=(64, 64, 1, 3), skip_update=True)[0]
     r.set_option("reorder", 1).set_option("split", 8 | 10 << 8)
-    cost_prev = None
     ux, rows = W // 8, H // 8
     for f in range(4):
         rgba, rgb, st = r.render(f, exact=exact, want_rgb=True)
         assert np.array_equal(rgba, ref[f][0]) and np.array_equal(rgb, ref[f][1]), f
         assert st["rays"] == ref[f][2]["rays"]
+        # the costs this launch recorded, and the order its last workgroup built from them for the next launch
         order = r.debug_read("unit_order").view(np.uint32)
         cost = r.debug_read("unit_cost").view(np.uint32)
         assert (cost > 0).all()                       # every unit's pixels reported
-        if cost_prev is not None:
-            cls = _sched_class(cost_prev)
-            split = np.where(15 - cls >= 10, 2, np.where(15 - cls >= 8, 1, 0))   # log2 pieces per unit (split 8 | 10 << 8)
-            for p in range(parts):
-                b0, b1 = rows * p // parts * ux, rows * (p + 1) // parts * ux
-                n_items = int((1 << split[b0:b1]).sum())
-                it = order[4 * b0:4 * b0 + n_items].astype(np.int64)
-                unit, piece, ls = it >> 4, (it >> 2) & 3, it & 3
-                assert np.array_equal(ls, split[unit]), p             # pieces follow the unit's class
-                first = piece == 0
-                units = unit[first]
-                assert np.array_equal(np.sort(units), np.arange(b0, b1)), p
-                # a unit's pieces are consecutive: item i + k is piece k of the same unit
-                starts = np.flatnonzero(first)
-                for k in range(1, 4):
-                    sel = starts[(1 << ls[starts]) > k]
-                    assert np.array_equal(unit[sel + k], unit[sel]) and (piece[sel + k] == k).all(), p
-                key = cls[units] * (1 << 32) + units   # class-major, screen order inside a class
-                assert (np.diff(key) > 0).all(), p
-        cost_prev = cost.copy()
+        cls = _sched_class(cost)
+        split = np.where(15 - cls >= 10, 2, np.where(15 - cls >= 8, 1, 0))   # log2 pieces per unit (split 8 | 10 << 8)
+        for p in range(parts):
+            b0, b1 = rows * p // parts * ux, rows * (p + 1) // parts * ux
+            n_items = int((1 << split[b0:b1]).sum())
+            it = order[4 * b0:4 * b0 + n_items].astype(np.int64)
+            unit, piece, ls = it >> 4, (it >> 2) & 3, it & 3
+            assert np.array_equal(ls, split[unit]), p             # pieces follow the unit's class
+            first = piece == 0
+            units = unit[first]
+            assert np.array_equal(np.sort(units), np.arange(b0, b1)), p
+            # a unit's pieces are consecutive: item i + k is piece k of the same unit
+            starts = np.flatnonzero(first)
+            for k in range(1, 4):
+                sel = starts[(1 << ls[starts]) > k]
+                assert np.array_equal(unit[sel + k], unit[sel]) and (piece[sel + k] == k).all(), p
+            key = cls[units] * (1 << 32) + units   # class-major, screen order inside a class
+            assert (np.diff(key) > 0).all(), p
     for _ in range(2):                                # tile shard: first launch of a layout, then ordered
         assert np.array_equal(r.render(3, exact=exact, tiles=(64, 64, 1, 3), skip_update=True)[0], tref)
 
