@@ -36,6 +36,7 @@ hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, c
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
 hipError_t launch_frame_copy(void *, const void *, size_t, unsigned long long *, hipStream_t);
+hipError_t launch_zero_agent(uint32_t *, size_t, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean, bool wide);
 hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, uint32_t, hipStream_t);
 uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean, bool wide);
@@ -1079,7 +1080,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             unit_order.release();
             HIP_TRY(hipMalloc(&unit_cost.p, 2 * (size_t)out.units * sizeof(uint32_t)));
             unit_cost.n = 2 * (size_t)out.units;
-            HIP_TRY(hipMemsetAsync(unit_cost.p, 0, unit_cost.n * sizeof(uint32_t), stream));
+            HIP_TRY(launch_zero_agent(unit_cost.p, unit_cost.n, stream));
             HIP_TRY(hipMalloc(&unit_order.p, 4 * (size_t)out.units * sizeof(uint32_t)));   // <= 4 items per unit
             unit_order.n = 4 * (size_t)out.units;
             s->sched_valid[q] = false;

@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "layout.hpp"
 
 namespace rtamd {
@@ -29,6 +31,21 @@ hipError_t launch_frame_copy(void *dst, const void *src, size_t bytes, unsigned 
     const uint32_t blocks = n16 / 256u + 1u < 64u ? n16 / 256u + 1u : 64u;
     hipLaunchKernelGGL(frame_copy_kernel, dim3(blocks), dim3(256), 0, stream, static_cast<uint4 *>(dst),
                        static_cast<const uint4 *>(src), n16, zero_counters);
+    return hipGetLastError();
+}
+
+// Zero n u32 with write-through (sc1) stores: the unit costs are only ever touched by memory-side atomics
+// and write-through stores, so no XCD's L2 holds a copy the render kernel's last workgroup could read
+// stale (build_schedule in trace_kernel.hip).
+__global__ __launch_bounds__(256) void zero_agent_kernel(uint32_t *__restrict__ p, uint32_t n) {
+    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u)
+        __hip_atomic_store(p + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+hipError_t launch_zero_agent(uint32_t *p, size_t n, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    const uint32_t blocks = (uint32_t)std::min<size_t>((n + 255) / 256, 1024);
+    hipLaunchKernelGGL(zero_agent_kernel, dim3(blocks), dim3(256), 0, stream, p, (uint32_t)n);
     return hipGetLastError();
 }
 
