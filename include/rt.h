@@ -301,8 +301,7 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 4 / 5 waves per SIMD
  *   "queue_parts": persistent kernel work-queue bands (1..8, default 8; a wave starts on band XCC_ID % parts)
  *   "reorder"   : 1 (default) = each launch claims its band's 8x8 units heaviest-first, ordered by the
- *                 traversal work the previous launch of the same layout and lane recorded per unit (built by
- *                 that launch's last workgroup, build_schedule in trace_kernel.hip);
+ *                 traversal work the previous launch of the same layout and lane recorded per unit (schedule.hip);
  *                 0 = screen order.  Images are identical either way (the RNG is keyed by pixel).
  *   "split"     : with "reorder", heavy units are claimed in pieces shared by several waves: halves from
  *                 cost level k_half, quarters from k_quarter (value k_half | k_quarter << 8, levels 0..15 =
@@ -335,9 +334,9 @@ rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
  *               cycles spent refilling, descending, testing leaves and shading, descent-loop
  *               iterations, refill-loop iterations, 2 reserved;
  *   "costmap" : 1 u32 per output pixel: traversal steps (interior steps + leaf phases) of its path;
- *   "unit_cost", "unit_order": option "reorder" — per 8x8 unit, the work the last launch recorded, and
- *               the claim order that launch's last workgroup built from it for the lane's next launch
- *               (band b's items start at 4 x its first unit: unit << 4 | piece << 2 | log2 pieces);
+ *   "unit_cost", "unit_order": option "reorder" — per 8x8 unit, the work the lane's last launch recorded
+ *               (after the next launch's schedule: the costs that schedule read), and the claim order the
+ *               last launch used (band b's items start at 4 x its first unit: unit << 4 | piece << 2 | log2 pieces);
  *   "leaf_prims": 1 u32 per leaf-ordered triangle slot: the caller's triangle index stored there (each
  *               BLAS owns the contiguous slots of its primitives, in leaf order).
  * Copies min(capacity, size) bytes to dst and stores the buffer's full size in *bytes. */

@@ -190,19 +190,11 @@ struct OutputGPU {
     // largest cost (traversal rounds + 1) of unit u's pixels for the next launch's order
     const uint32_t *order;
     uint32_t *unit_cost;
-    // fused schedule (option "reorder"): the last workgroup of the launch to finish turns unit_cost into
-    // the next launch's claim order (written to `order_next`, the band item counts and reset heads into
-    // `queue`), copies the costs to cost_prev (debug) and clears them; null = no schedule
-    uint32_t *sched_done;           // arrival counter of the launch's workgroups
-    uint32_t *order_next;
-    uint32_t *cost_prev;
-    uint32_t split_half, split_quarter;
 };
 constexpr uint32_t QUEUE_STRIDE = 32;         // u32 words between partition heads (128 B lines)
 constexpr uint32_t QUEUE_MAX_PARTS = 8;
-// queue block of a lane: band heads (lines 0..7), band item counts (lines 8..15), arrival counter (line 16)
-constexpr uint32_t QUEUE_DONE_WORD = 2 * QUEUE_MAX_PARTS * QUEUE_STRIDE;
-constexpr uint32_t QUEUE_WORDS = QUEUE_DONE_WORD + QUEUE_STRIDE;
+// queue block of a lane: band heads (lines 0..7), band item counts (lines 8..15)
+constexpr uint32_t QUEUE_WORDS = 2 * QUEUE_MAX_PARTS * QUEUE_STRIDE;
 constexpr uint32_t SCHED_CLASSES = 16;       // cost classes of the claim order (half-octaves of steps per pixel)
 
 // class 0 = heaviest: half-octaves of a unit's mean traversal steps per pixel, floor(2 log2(c/64 + 1))

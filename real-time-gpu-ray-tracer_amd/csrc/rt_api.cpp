@@ -36,7 +36,8 @@ hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, c
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
 hipError_t launch_frame_copy(void *, const void *, size_t, unsigned long long *, hipStream_t);
-hipError_t launch_zero_agent(uint32_t *, size_t, hipStream_t);
+hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t,
+                           uint32_t, void *, const void *, size_t, unsigned long long *, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean, bool wide);
 hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, uint32_t, hipStream_t);
 uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean, bool wide);
@@ -203,9 +204,8 @@ struct rt_scene {
     bool reorder = true;
     uint32_t split = 10u | 12u << 8;  // heavy-unit pieces: class level for halves | quarters << 8 (0xFF = never)
     DevBuf<uint32_t> unit_cost[NLANE], unit_order[NLANE];
-    uint32_t sched_sig[NLANE][7] = {};  // layout of the lane's last launch: the order it built is for this layout
+    uint32_t sched_sig[NLANE][7] = {};  // launch layout the recorded costs belong to
     bool sched_valid[NLANE] = {};
-    bool heads_zero[NLANE] = {};        // the lane's last launch reset its queue heads (fused schedule)
     DevBuf<uint32_t> costmap;
     size_t costmap_pixels = 0;
     DevBuf<unsigned long long> timeline;
@@ -693,7 +693,6 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
     for (bool &v : s->sched_valid) v = false;
-    for (bool &v : s->heads_zero) v = false;
     if (mode == RT_BUILD_LBVH) {
         if ((st = gpu_setup_blas(s, segs, slot_base)) != RT_OK) return st;
     } else {
@@ -1070,33 +1069,38 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     if (!(o.flags & RT_RENDER_KEEP_COUNTERS)) s->cnt_epoch++;
     bool zero_lane = s->lane_epoch[q] != s->cnt_epoch;                      // cleared before this launch
     s->lane_epoch[q] = s->cnt_epoch;
-    // the lane's queue heads are zero after a launch that built a schedule (its last workgroup resets them)
-    bool reset_queue = !s->heads_zero[q];
-    const bool fused_schedule = s->use_persistent && s->reorder && s->grab == 64u;
-    if (fused_schedule) {
+    bool reset_queue = true;
+    if (s->use_persistent && s->reorder && s->grab == 64u) {
         DevBuf<uint32_t> &unit_cost = s->unit_cost[q], &unit_order = s->unit_order[q];
         if (unit_cost.n < 2 * (size_t)out.units) {        // [recorded costs | costs of the last launch (debug)]
             unit_cost.release();
             unit_order.release();
             HIP_TRY(hipMalloc(&unit_cost.p, 2 * (size_t)out.units * sizeof(uint32_t)));
             unit_cost.n = 2 * (size_t)out.units;
-            HIP_TRY(launch_zero_agent(unit_cost.p, unit_cost.n, stream));
+            HIP_TRY(hipMemsetAsync(unit_cost.p, 0, unit_cost.n * sizeof(uint32_t), stream));
             HIP_TRY(hipMalloc(&unit_order.p, 4 * (size_t)out.units * sizeof(uint32_t)));   // <= 4 items per unit
             unit_order.n = 4 * (size_t)out.units;
             s->sched_valid[q] = false;
         }
         const uint32_t sig[7] = {out.units, out.units_x, out.tile_w, out.tile_h, out.tile_rank, out.tile_count,
                                  out.queue_parts};
-        // the order the lane's previous launch built is for the layout it had
+        // the costs the lane's previous launch recorded are for the layout it had
         const bool do_order = s->sched_valid[q] && std::memcmp(sig, s->sched_sig[q], sizeof sig) == 0;
+        const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
+        const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
+        const int pc = s->pending_copy;
+        HIP_TRY(launch_schedule(unit_cost.p, unit_cost.p + out.units, unit_order.p, s->queue[q], rows, upr, out.queue_parts,
+                                do_order, s->split & 0xFFu, (s->split >> 8) & 0xFFu, pc >= 0 ? s->frame_dev[pc] : nullptr,
+                                pc >= 0 ? s->staging_dev[pc] : nullptr, pc >= 0 ? s->frame_block : 0,
+                                zero_lane ? lane_counters : nullptr, stream));
+        zero_lane = false;
+        if (pc >= 0) HIP_TRY(hipEventRecord(s->ev_copied[pc], stream));
+        s->pending_copy = -1;
         std::memcpy(s->sched_sig[q], sig, sizeof sig);
+        s->sched_valid[q] = true;
         out.order = do_order ? unit_order.p : nullptr;
         out.unit_cost = unit_cost.p;
-        out.cost_prev = unit_cost.p + out.units;
-        out.order_next = unit_order.p;
-        out.sched_done = s->queue[q] + QUEUE_DONE_WORD;
-        out.split_half = s->split & 0xFFu;
-        out.split_quarter = (s->split >> 8) & 0xFFu;
+        reset_queue = false;
     }
     if (s->pending_copy >= 0) {                // the frame block's upload (and the lane's counter reset)
         HIP_TRY(launch_frame_copy(s->frame_dev[s->pending_copy], s->staging_dev[s->pending_copy], s->frame_block,
@@ -1120,8 +1124,6 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
                                                        s->variant, false, reset_queue, stream)
                       : launch_render_persistent_fast(g, cam, out, count, lane_counters, s->queue[q], blocks, s->threshold,
                                                       s->variant, lean, reset_queue, stream));
-        s->heads_zero[q] = fused_schedule;
-        if (fused_schedule) s->sched_valid[q] = true;
     }
     else
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, lane_counters, stream)

@@ -1,23 +1,172 @@
-// schedule.hip — per-frame upload of the TLAS / instance block, by a kernel.
+// schedule.hip — claim order of the persistent render kernel's work queue (option "reorder"), and the
+// per-frame upload of the TLAS / instance block.
 //
-// The block (TLAS nodes, slots, instance records: ~35 KB for C2) is built on the host into pinned
-// staging memory and read by this kernel over PCIe.  hipMemcpyAsync of the same bytes is handed to an
-// SDMA engine and, between two traces on one stream, cost ~35 us of idle GPU per frame (rocprofv3 trace,
-// round 1).  The kernel uses 8 VGPRs, so with overlapped lanes it fits beside a full persistent render
-// grid (3 waves x 168 VGPRs per SIMD) instead of waiting for a drained workgroup slot.  It also clears
-// the lane's work counters when the next launch starts a new counting epoch.
+// The persistent launch (trace_kernel.hip) ends when its last wave does.  A wave claims one 8x8 unit at
+// a time and its lanes refill from that unit, so a unit holds a wave for as long as its 64 paths take,
+// and that is very uneven: a sky unit averages ~5 traversal steps per pixel, a unit over the particle
+// cluster ~100.  Claimed in screen order, the heavy units that sit late in a band start late and the GPU
+// waits for them (C2: the queue ran dry at ~270 us, the last wave ended at ~520 us).  Animated frames
+// change little from one frame to the next, so each launch records the traversal work of every unit
+// (unit_cost, one atomicAdd per unit and shade step) and this kernel orders the lane's next launch's
+// claims heaviest-first (longest-processing-time-first list scheduling).  The image does not depend on
+// the order: every pixel's RNG stream is keyed by its global pixel index.
 //
-// (The claim-order schedule that used to run here is built by the render kernel's last workgroup:
-// build_schedule in trace_kernel.hip.)
+// One 256-thread workgroup per band: the band's costs are read coalesced (8 B per lane, several loads in
+// flight) into 4-bit class codes in LDS and cleared for the next launch, then a stable counting sort over
+// 16 cost classes (class order = heaviest first; equal classes keep screen order, so neighbouring units
+// of one class are still claimed together).  A heavy unit becomes 2 or 4 claim items (32 / 16 pixels) so
+// that its paths spread over several waves.  The band's items go to order[4 b0 ...) as
+// (unit << 4 | piece << 2 | log2 pieces), the item count to the band's count word (a line of its own,
+// away from the atomically updated head), and the queue heads are reset.  The kernel also uploads the
+// frame's TLAS / instance block from pinned staging and clears the lane's work counters.
+//
+// Footprint (measured, profiles/r02_*): with overlapped lanes this kernel runs while the other lane's
+// persistent grid holds the GPU, in the workgroup slots the grid leaves free (option "reserve": one per
+// XCD).  Round 1's version (one 1024-thread workgroup, 64 KB of LDS per band) could only start once the
+// other launch drained and averaged 172 us per frame; a 256-thread version with 49 KB of LDS still
+// waited (84 us: a drained render workgroup leaves 32 KB holes of LDS); building the order in the render
+// launch's last workgroup instead added ~90 us to every launch (one CU doing the whole frame's sort).
+// So: 4 waves and <= 16.2 KB of LDS — half the LDS footprint of one render workgroup.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-
-#include <algorithm>
 
 #include "layout.hpp"
 
 namespace rtamd {
+namespace {
 
+constexpr uint32_t SCHED_THREADS = 256;
+constexpr uint32_t SCHED_NIB_UNITS = 16384;    // band units whose class nibbles fit in 8 KB of LDS
+constexpr uint32_t SCHED_LOADS = 4;            // 8-byte cost loads in flight per thread
+
+__global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__restrict__ cost, uint32_t *__restrict__ cost_prev,
+                                                                 uint32_t *__restrict__ order, uint32_t *__restrict__ queue,
+                                                                 uint32_t rows, uint32_t upr, uint32_t parts, uint32_t do_order,
+                                                                 uint32_t kh, uint32_t kq, uint4 *copy_dst,
+                                                                 const uint4 *copy_src, uint32_t copy_n16,
+                                                                 unsigned long long *zero_counters) {
+    __shared__ uint16_t cnt[SCHED_CLASSES * SCHED_THREADS];   // per-thread class item counts -> offsets (8 KB)
+    __shared__ uint8_t nib[SCHED_NIB_UNITS / 2];               // class codes, 2 per byte (8 KB)
+    __shared__ uint32_t total[SCHED_CLASSES], base[SCHED_CLASSES];
+    const uint32_t part = blockIdx.x, t = threadIdx.x;
+    if (part == 0 && t < QUEUE_MAX_PARTS) queue[t * QUEUE_STRIDE] = 0u;      // every head: `parts` may change
+    if (part == 0 && zero_counters && t < CNT_NUM) zero_counters[t] = 0ull;  // the lane's work counters
+    // the frame's TLAS / instance block, read from pinned host staging (see launch_frame_copy)
+    for (uint32_t i = part * SCHED_THREADS + t; i < copy_n16; i += parts * SCHED_THREADS) copy_dst[i] = copy_src[i];
+    // the band's unit range, computed exactly as the render kernel's refill computes it
+    const uint32_t b0 = rows * part / parts * upr, b1 = rows * (part + 1) / parts * upr;
+    const uint32_t n = b1 - b0;
+    if (!do_order) {
+        for (uint32_t u = b0 + t; u < b1; u += SCHED_THREADS) { cost_prev[u] = cost[u]; cost[u] = 0u; }
+        return;
+    }
+    // bands of < 16384 units (any frame up to 4K with 8 bands) sort from LDS class codes with 16-bit
+    // offsets
+    const uint32_t gbase = b0 & ~1u;
+    const bool in_lds = b1 - gbase <= SCHED_NIB_UNITS && 4u * n < 65536u;
+    if (in_lds) {
+        // pass A: pairs of costs, coalesced 8-byte loads -> class codes; costs kept (debug) and cleared
+        const uint32_t npair = (b1 - gbase + 1) / 2;
+        for (uint32_t i0 = t; i0 < npair; i0 += SCHED_THREADS * SCHED_LOADS) {
+            uint2 v[SCHED_LOADS];
+#pragma unroll
+            for (uint32_t k = 0; k < SCHED_LOADS; k++) {
+                const uint32_t i = i0 + k * SCHED_THREADS;
+                v[k] = i < npair ? reinterpret_cast<const uint2 *>(cost + gbase)[i] : make_uint2(0u, 0u);
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < SCHED_LOADS; k++) {
+                const uint32_t i = i0 + k * SCHED_THREADS;
+                if (i >= npair) break;
+                uint32_t code = 0;
+#pragma unroll
+                for (uint32_t h = 0; h < 2; h++) {
+                    const uint32_t u = gbase + 2 * i + h;
+                    if (u < b0 || u >= b1) continue;       // the neighbour band's unit: not ours to clear
+                    const uint32_t c = h ? v[k].y : v[k].x;
+                    code |= cost_class(c) << (4 * h);
+                    cost_prev[u] = c;
+                    cost[u] = 0u;
+                }
+                nib[i] = (uint8_t)code;
+            }
+        }
+    }
+    __syncthreads();
+    if (!in_lds) {
+        // a band of >= 16384 units (beyond 4K with 8 bands): screen order, one item per unit
+        for (uint32_t u = b0 + t; u < b1; u += SCHED_THREADS) {
+            cost_prev[u] = cost[u];
+            cost[u] = 0u;
+            order[4u * b0 + (u - b0)] = u << 4;
+        }
+        if (t == 0) queue[(QUEUE_MAX_PARTS + part) * QUEUE_STRIDE] = n;
+        return;
+    }
+    const uint32_t per = (n + SCHED_THREADS - 1) / SCHED_THREADS;
+    const uint32_t lo = b0 + min(n, t * per), hi = b0 + min(n, (t + 1) * per);
+    const auto cls = [&](uint32_t u) { return (uint32_t)(nib[(u - gbase) >> 1] >> (4 * ((u - gbase) & 1u))) & 15u; };
+    for (uint32_t c = 0; c < SCHED_CLASSES; c++) cnt[c * SCHED_THREADS + t] = 0;
+    for (uint32_t u = lo; u < hi; u++) {
+        const uint32_t c = cls(u);
+        cnt[c * SCHED_THREADS + t] += (uint16_t)(1u << split_log2(c, kh, kq));
+    }
+    __syncthreads();
+    // exclusive scan of each class's item counts over the threads (thread order = screen order):
+    // wave w scans classes [4w, 4w + 4), each lane 4 consecutive threads' counts (< 65536 items per band)
+    const uint32_t w = t >> 6, lane = t & 63u;
+    for (uint32_t cc = 0; cc < SCHED_CLASSES / 4; cc++) {
+        const uint32_t c = w * (SCHED_CLASSES / 4) + cc;
+        uint32_t local[4], run = 0;
+#pragma unroll
+        for (int k = 0; k < 4; k++) { local[k] = run; run += cnt[c * SCHED_THREADS + lane * 4 + k]; }
+        uint32_t incl = run;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off, 64);
+            if (lane >= (uint32_t)off) incl += y;
+        }
+        const uint32_t excl = incl - run;
+        if (lane == 63u) total[c] = incl;
+#pragma unroll
+        for (int k = 0; k < 4; k++) cnt[c * SCHED_THREADS + lane * 4 + k] = (uint16_t)(excl + local[k]);
+    }
+    __syncthreads();
+    if (t == 0) {
+        uint32_t acc = 0;
+        for (uint32_t c = 0; c < SCHED_CLASSES; c++) { base[c] = acc; acc += total[c]; }
+        queue[(QUEUE_MAX_PARTS + part) * QUEUE_STRIDE] = acc;   // items in the band (own line)
+    }
+    __syncthreads();
+    // pass 2: the band's items [4 b0, 4 b0 + items) — at most 4 per unit
+    uint32_t *items = order + 4u * b0;
+    for (uint32_t u = lo; u < hi; u++) {
+        const uint32_t c = cls(u), ls = split_log2(c, kh, kq);
+        const uint32_t at = base[c] + cnt[c * SCHED_THREADS + t];
+        cnt[c * SCHED_THREADS + t] = (uint16_t)(at - base[c] + (1u << ls));
+        for (uint32_t k = 0; k < (1u << ls); k++) items[at + k] = (u << 4) | (k << 2) | ls;
+    }
+}
+
+}  // namespace
+
+// rows x upr units per frame split into `parts` bands as in render_persistent_body; do_order = 0 only
+// clears the costs and the queue heads (first launch of a layout: no costs recorded yet).
+// zero_counters (optional): CNT_NUM device counters cleared before the launch that follows.
+hipError_t launch_schedule(uint32_t *cost, uint32_t *cost_prev, uint32_t *order, uint32_t *queue, uint32_t rows, uint32_t upr,
+                           uint32_t parts, bool do_order, uint32_t k_half, uint32_t k_quarter, void *copy_dst,
+                           const void *copy_src, size_t copy_bytes, unsigned long long *zero_counters, hipStream_t stream) {
+    if (parts == 0 || parts > QUEUE_MAX_PARTS || copy_bytes % 16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(schedule_kernel, dim3(parts), dim3(SCHED_THREADS), 0, stream, cost, cost_prev, order, queue, rows, upr,
+                       parts, do_order ? 1u : 0u, k_half, k_quarter, static_cast<uint4 *>(copy_dst),
+                       static_cast<const uint4 *>(copy_src), (uint32_t)(copy_bytes / 16), zero_counters);
+    return hipGetLastError();
+}
+
+// Per-frame upload of the TLAS / instance block by a kernel reading the pinned staging buffer over PCIe,
+// when no schedule kernel carries it.  hipMemcpyAsync of the same ~35 KB is handed to an SDMA engine and,
+// between two traces on one stream, cost ~35 us of idle GPU per frame (rocprofv3 trace, round 1).  8 VGPRs:
+// it fits beside a full persistent grid.
 __global__ __launch_bounds__(256) void frame_copy_kernel(uint4 *__restrict__ dst, const uint4 *__restrict__ src, uint32_t n16,
                                                          unsigned long long *zero_counters) {
     if (zero_counters && blockIdx.x == 0 && threadIdx.x < CNT_NUM) zero_counters[threadIdx.x] = 0ull;
@@ -31,21 +180,6 @@ hipError_t launch_frame_copy(void *dst, const void *src, size_t bytes, unsigned 
     const uint32_t blocks = n16 / 256u + 1u < 64u ? n16 / 256u + 1u : 64u;
     hipLaunchKernelGGL(frame_copy_kernel, dim3(blocks), dim3(256), 0, stream, static_cast<uint4 *>(dst),
                        static_cast<const uint4 *>(src), n16, zero_counters);
-    return hipGetLastError();
-}
-
-// Zero n u32 with write-through (sc1) stores: the unit costs are only ever touched by memory-side atomics
-// and write-through stores, so no XCD's L2 holds a copy the render kernel's last workgroup could read
-// stale (build_schedule in trace_kernel.hip).
-__global__ __launch_bounds__(256) void zero_agent_kernel(uint32_t *__restrict__ p, uint32_t n) {
-    for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u)
-        __hip_atomic_store(p + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-hipError_t launch_zero_agent(uint32_t *p, size_t n, hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    if (n > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    const uint32_t blocks = (uint32_t)std::min<size_t>((n + 255) / 256, 1024);
-    hipLaunchKernelGGL(zero_agent_kernel, dim3(blocks), dim3(256), 0, stream, p, (uint32_t)n);
     return hipGetLastError();
 }
 

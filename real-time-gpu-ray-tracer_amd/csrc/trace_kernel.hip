@@ -1077,161 +1077,6 @@ __device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t
     }
 }
 
-// ---- claim order of the next launch (option "reorder"), built by this launch's last workgroup ----------
-// The persistent launch ends when its last wave does.  A wave claims one 8x8 unit at a time and its lanes
-// refill from that unit, so a unit holds a wave for as long as its 64 paths take, and that is very uneven:
-// a sky unit averages ~5 traversal steps per pixel, a unit over the particle cluster ~100.  Claimed in
-// screen order, the heavy units that sit late in a band start late and the GPU waits for them (C2: the
-// queue ran dry at ~270 us, the last wave ended at ~520 us).  Animated frames change little from one frame
-// to the next, so each launch records the traversal work of every unit (unit_cost_add) and the claims of
-// the lane's next launch go heaviest-first (longest-processing-time-first list scheduling).  The image
-// does not depend on the order: every pixel's RNG stream is keyed by its global pixel index.
-//
-// Per band: a stable counting sort of the band's units over 16 cost classes (class order = heaviest
-// first; equal classes keep screen order, so neighbouring units of one class are still claimed together).
-// A heavy unit becomes 2 or 4 claim items (32 / 16 pixels) so that its paths spread over several waves.
-// The band's items go to order[4 b0 ...) as (unit << 4 | piece << 2 | log2 pieces), the item count to the
-// band's count word (a line of its own, away from the atomically updated head); the costs are copied to
-// cost_prev and cleared, and the heads and the arrival counter are reset.
-//
-// Round 1 ran this as a separate kernel between two launches.  With overlapped lanes it had to wait for
-// a free workgroup slot while the other lane's persistent grid held the GPU (172 us per frame at 1024
-// threads / 64 KB of LDS, 23-84 us at 256 threads, profiles/r02_*), and the next launch waited behind
-// it.  Here the last workgroup to finish does it in its own slot: no extra kernel, no slot to wait for.
-// Visibility: the costs are only ever written by agent-scope atomics and write-through (sc1) stores, which
-// execute at the memory side and leave no copy in any XCD's L2; every workgroup drains its atomics
-// (s_waitcnt vmcnt(0)) before its arrival add, and the last workgroup reads the costs with sc1 loads
-// (L1 bypassed; no L2 holds the lines), so it sees every XCD's adds.
-// Cost: the costs are read coalesced, 8 B per lane, several loads in flight, into 4-bit class codes in
-// LDS (32768 units per pass), then each band is sorted from LDS.
-constexpr uint32_t SCHED_NIB_UNITS = 32768;   // units whose class nibbles fit in the 16 KB after the counts
-constexpr uint32_t SCHED_LOADS = 4;           // 8-byte cost loads in flight per thread
-
-__device__ __forceinline__ uint64_t load_agent64(const uint32_t *p) {
-    return __hip_atomic_load(reinterpret_cast<const uint64_t *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t load_agent(const uint32_t *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void store_agent(uint32_t *p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// scratch: >= 8192 u32 of LDS no wave of the block uses any more; small: 2 * SCHED_CLASSES u32 of LDS
-__device__ void build_schedule(const OutputGPU &out, uint32_t *queue, uint32_t *scratch, uint32_t *small) {
-    const uint32_t t = threadIdx.x;
-    uint32_t *cnt = scratch;                                                      // [SCHED_CLASSES][BLOCK]
-    uint8_t *nib = reinterpret_cast<uint8_t *>(scratch + SCHED_CLASSES * BLOCK);  // 2 class codes per byte
-    uint32_t *total = small, *base = small + SCHED_CLASSES;
-    uint32_t *cost = out.unit_cost;
-    const uint32_t parts = out.queue_parts;
-    const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
-    const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
-    const uint32_t kh = out.split_half, kq = out.split_quarter;
-    // band p = units [bstart(p), bstart(p + 1)), computed exactly as the refill computes it
-    const auto bstart = [&](uint32_t p) { return rows * p / parts * upr; };
-    for (uint32_t part = 0; part < parts;) {
-        // a group of consecutive bands whose class codes fit in LDS (all 8 bands at 1080p)
-        const uint32_t g0 = bstart(part), gbase = g0 & ~1u;
-        uint32_t pe = part + 1;
-        while (pe < parts && bstart(pe + 1) - gbase <= SCHED_NIB_UNITS) pe++;
-        const uint32_t g1 = bstart(pe);
-        const bool in_lds = g1 - gbase <= SCHED_NIB_UNITS;
-        if (in_lds) {
-            // pass A: pairs of costs, coalesced 8-byte loads -> class codes, costs kept for the debug read
-            // and cleared (write-through) for the next launch
-            const uint32_t npair = (g1 - gbase + 1) / 2;
-            for (uint32_t i0 = t; i0 < npair; i0 += BLOCK * SCHED_LOADS) {
-                uint64_t v[SCHED_LOADS];
-#pragma unroll
-                for (uint32_t k = 0; k < SCHED_LOADS; k++) {
-                    const uint32_t i = i0 + k * BLOCK;
-                    v[k] = i < npair ? load_agent64(cost + gbase + 2 * i) : 0ull;
-                }
-#pragma unroll
-                for (uint32_t k = 0; k < SCHED_LOADS; k++) {
-                    const uint32_t i = i0 + k * BLOCK;
-                    if (i >= npair) break;
-                    uint32_t code = 0;
-#pragma unroll
-                    for (uint32_t h = 0; h < 2; h++) {
-                        const uint32_t u = gbase + 2 * i + h;
-                        if (u < g0 || u >= g1) continue;
-                        const uint32_t c = (uint32_t)(v[k] >> (32 * h));
-                        code |= cost_class(c) << (4 * h);
-                        out.cost_prev[u] = c;
-                        store_agent(cost + u, 0u);
-                    }
-                    nib[i] = (uint8_t)code;
-                }
-            }
-            __syncthreads();
-        }
-        for (uint32_t p = part; p < pe; p++) {
-            const uint32_t b0 = bstart(p), b1 = bstart(p + 1);
-            const uint32_t n = b1 - b0, per = (n + BLOCK - 1) / BLOCK;
-            const uint32_t lo = b0 + min(n, t * per), hi = b0 + min(n, (t + 1) * per);
-            // class of unit u: from LDS, or (a band larger than the LDS pass) from its cost
-            const auto cls = [&](uint32_t u, bool first) {
-                if (in_lds) return (uint32_t)(nib[(u - gbase) >> 1] >> (4 * ((u - gbase) & 1u))) & 15u;
-                uint32_t c;
-                if (first) {                   // pass 1 reads the cost once, keeps it, clears it
-                    c = load_agent(cost + u);
-                    out.cost_prev[u] = c;
-                    store_agent(cost + u, 0u);
-                } else {
-                    c = out.cost_prev[u];      // this thread's own store
-                }
-                return cost_class(c);
-            };
-            for (uint32_t c = 0; c < SCHED_CLASSES; c++) cnt[c * BLOCK + t] = 0u;
-            for (uint32_t u = lo; u < hi; u++) {
-                const uint32_t c = cls(u, true);
-                cnt[c * BLOCK + t] += 1u << split_log2(c, kh, kq);
-            }
-            __syncthreads();
-            // exclusive scan of each class's item counts over the threads (thread order = screen order):
-            // wave w scans classes [4w, 4w + 4), each lane 4 consecutive threads' counts
-            const uint32_t w = t >> 6, lane = t & 63u;
-            for (uint32_t cc = 0; cc < SCHED_CLASSES / 4; cc++) {
-                const uint32_t c = w * (SCHED_CLASSES / 4) + cc;
-                uint32_t local[4], run = 0;
-#pragma unroll
-                for (int k = 0; k < 4; k++) { local[k] = run; run += cnt[c * BLOCK + lane * 4 + k]; }
-                uint32_t incl = run;
-#pragma unroll
-                for (int off = 1; off < 64; off <<= 1) {
-                    const uint32_t y = __shfl_up(incl, off, 64);
-                    if (lane >= (uint32_t)off) incl += y;
-                }
-                const uint32_t excl = incl - run;
-#pragma unroll
-                for (int k = 0; k < 4; k++) cnt[c * BLOCK + lane * 4 + k] = excl + local[k];
-                if (lane == 63u) total[c] = incl;
-            }
-            __syncthreads();
-            if (t == 0) {
-                uint32_t acc = 0;
-                for (uint32_t c = 0; c < SCHED_CLASSES; c++) { base[c] = acc; acc += total[c]; }
-                store_agent(queue + (QUEUE_MAX_PARTS + p) * QUEUE_STRIDE, acc);     // items in the band (own line)
-            }
-            __syncthreads();
-            // pass 2: the band's items [4 b0, 4 b0 + items) — at most 4 per unit
-            uint32_t *items = out.order_next + 4u * b0;
-            for (uint32_t u = lo; u < hi; u++) {
-                const uint32_t c = cls(u, false), ls = split_log2(c, kh, kq);
-                const uint32_t at = base[c] + cnt[c * BLOCK + t];
-                for (uint32_t k = 0; k < (1u << ls); k++) items[at + k] = (u << 4) | (k << 2) | ls;
-                cnt[c * BLOCK + t] = at - base[c] + (1u << ls);
-            }
-            __syncthreads();                 // the next band reuses cnt
-        }
-        part = pe;
-    }
-    if (t < QUEUE_MAX_PARTS) store_agent(queue + t * QUEUE_STRIDE, 0u);          // every head: `parts` may change
-    if (t == 0) store_agent(queue + QUEUE_DONE_WORD, 0u);
-}
-
 template <bool COUNT, bool LEAN, bool WIDE>
 __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out,
                                                        uint32_t *queue, uint32_t threshold,
@@ -1461,19 +1306,6 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             w[12] = pc.iters;
             w[13] = pc.refill_iters;
         }
-    }
-    if (out.sched_done) {
-        // arrival: every wave's unit-cost atomics have left (vmcnt), then one add per workgroup; the
-        // workgroup whose add comes last builds the next launch's claim order
-        __shared__ uint32_t sched_small[2 * SCHED_CLASSES + 1];
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0)
-            sched_small[2 * SCHED_CLASSES] =
-                __hip_atomic_fetch_add(out.sched_done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
-        __syncthreads();
-        if (sched_small[2 * SCHED_CLASSES])
-            build_schedule(out, queue, reinterpret_cast<uint32_t *>(&lds_stack[0][0]), sched_small);
     }
 }
 
