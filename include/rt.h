@@ -337,6 +337,9 @@ rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
  *   "unit_cost", "unit_order": option "reorder" — per 8x8 unit, the work the lane's last launch recorded
  *               (after the next launch's schedule: the costs that schedule read), and the claim order the
  *               last launch used (band b's items start at 4 x its first unit: unit << 4 | piece << 2 | log2 pieces);
+ *   "instances": RT_BUILD_LBVH: 45 floats per instance, the records the GPU computed for the current frame
+ *               (instances.hip): inverse, forward and inverse-transpose rows 1-3 (12 each), transformed box
+ *               {xmin,xmax,ymin,ymax,zmin,zmax}, transformed centroid;
  *   "leaf_prims": 1 u32 per leaf-ordered triangle slot: the caller's triangle index stored there (each
  *               BLAS owns the contiguous slots of its primitives, in leaf order).
  * Copies min(capacity, size) bytes to dst and stores the buffer's full size in *bytes. */

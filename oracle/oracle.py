@@ -66,6 +66,7 @@ def lib():
         L.oracle_instance_matrices.argtypes = [P(abi.Xform), C.c_void_p]
         L.oracle_instance_matrices.restype = None
         L.oracle_camera_export.argtypes = [C.c_void_p, C.c_void_p]
+        L.oracle_instance_state.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
         L.oracle_demo_update.argtypes = [C.c_void_p, P(abi.Xform), C.c_size_t, C.c_uint64]
         L.oracle_demo_update.restype = None
         _lib = L
@@ -135,6 +136,14 @@ class OracleScene:
         cnt = Counters()
         assert lib().oracle_trace(self.h, rays.ctypes.data, n, hits, int(brute_force), C.byref(cnt)) == 0
         return hits_to_numpy(hits, n), cnt.as_dict()
+
+    def instance_state(self):
+        """(n_inst, 45) float32: inverse / forward / inverse-transpose rows 1-3, transformed box, centroid."""
+        n = len(self._scene.instances)
+        out = np.zeros((n, 45), np.float32)
+        for i in range(n):
+            assert lib().oracle_instance_state(self.h, i, out[i].ctypes.data) == 0
+        return out
 
     def blas_count(self):
         return lib().oracle_blas_count(self.h)

@@ -576,6 +576,20 @@ void oracle_instance_matrices(const rt_xform *x, float *out48) {
             for (int j = 0; j < 4; j++) out48[k * 16 + i * 4 + j] = ms[k]->d[i + 1][j + 1];
 }
 
+/* Instance i after the last update (Instance.cu:4-17): rows 1-3 of the inverse, forward and inverse-
+ * transpose matrices (12 floats each), the transformed box {xmin,xmax,...} (6) and centroid (3). */
+int oracle_instance_state(const oracle_scene *s, uint32_t i, float *out45) {
+    if (!s || i >= s->n_inst) return 1;
+    const Inst *in = &s->inst[i];
+    const Mat *ms[3] = {&in->inv, &in->fwd, &in->nrm};
+    for (int k = 0; k < 3; k++)
+        for (int r = 0; r < 3; r++)
+            for (int c = 0; c < 4; c++) out45[k * 12 + r * 4 + c] = ms[k]->d[r + 1][c + 1];
+    for (int a = 0; a < 3; a++) { out45[36 + 2 * a] = in->tbox.r[a].min; out45[37 + 2 * a] = in->tbox.r[a].max; }
+    out45[42] = in->tcentroid.x; out45[43] = in->tcentroid.y; out45[44] = in->tcentroid.z;
+    return 0;
+}
+
 static Box prim_box(const oracle_scene *s, uint32_t type, uint32_t idx) {
     if (type == RT_PRIM_SPHERE) return sphere_box(&s->sph[idx]);
     if (type == RT_PRIM_PARALLELOGRAM) return quad_box(&s->quad[idx]);

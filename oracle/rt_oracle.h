@@ -81,6 +81,7 @@ float oracle_rng_uniform(uint64_t *state);
 /* Instance matrices after Instance::updateTransformArguments (Instance.cu:4-17):
  * out = 16 floats forward (row-major 4x4) + 16 inverse + 16 normal (inverse^T). */
 void oracle_instance_matrices(const rt_xform *x, float *out48);
+int oracle_instance_state(const oracle_scene *s, uint32_t i, float *out45);
 
 /* Camera after calculateCameraProperties: pixelOrigin, dx, dy, center, U, V (18 floats),
  * then recip_sqrt, sqrt_sample_count. */

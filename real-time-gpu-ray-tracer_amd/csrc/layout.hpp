@@ -120,6 +120,21 @@ struct alignas(16) InstCold {       // 96 B: hit finalisation (Instance.cu:41-45
     float nrm[12];                  // rows 1..3 of normalTransformMatrix
 };
 
+// GPU instance update (instances.hip, GPU-built frames): per-instance inputs kept resident in HBM, and the
+// delta record the host uploads for an instance whose transform or local box changed.
+struct alignas(16) InstParams {     // 96 B
+    float shift[3], cos[3], sin[3], scale[3];   // Instance::updateTransformArguments arguments (cos / sin: host libm)
+    float box[6];                   // local box {xmin,xmax,ymin,ymax,zmin,zmax} (volume-expanded, as the host holds it)
+    float centroid[3];              // local centroid
+    float pad[3];
+};
+static_assert(sizeof(InstParams) == 96, "InstParams must be 96 B");
+struct alignas(16) InstDelta {      // 112 B
+    uint32_t index, pad0, pad1, pad2;
+    InstParams p;
+};
+static_assert(sizeof(InstDelta) == 112, "InstDelta must be 112 B");
+
 constexpr uint32_t MAT_METAL_BIT = 1u << 31;
 
 struct alignas(16) TreeRoot {       // 32 B: root of one tree (GPU-built trees keep it in HBM)

@@ -40,6 +40,8 @@ hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint3
                            uint32_t, void *, const void *, size_t, unsigned long long *, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean, bool wide);
 hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, uint32_t, hipStream_t);
+hipError_t launch_instance_update(const InstDelta *, uint32_t, InstParams *, uint32_t, InstHot *, InstCold *, float *, float4 *,
+                                  hipStream_t);
 uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean, bool wide);
 }  // namespace rtamd
 
@@ -153,7 +155,11 @@ struct rt_scene {
     //   [tlas root | tlas pairs | tlas slots | inst hot | inst cold | tlas item boxes | tlas item centroids]
     // (the root and the item arrays are used by GPU-built TLASes only)
     size_t frame_block = 0, off_root = 0, off_pairs = 0, off_slots = 0, off_hot = 0, off_cold = 0, off_tbox = 0,
-           off_tcent = 0, off_root_wide = 0, off_quads = 0;
+           off_tcent = 0, off_root_wide = 0, off_quads = 0, off_delta = 0;
+    // GPU-built frames: per-instance parameters resident in HBM (instances.hip); the host stages a delta
+    // (InstDelta at off_delta) only for instances whose transform or local box changed
+    DevBuf<InstParams> inst_params;
+    std::vector<uint8_t> inst_dirty;
     // frame blocks cycle through NLANE buffers, so "overlap" lanes never wait on each other's block
     static constexpr int NLANE = 4;
     uint8_t *staging[NLANE] = {};                 // pinned host
@@ -268,7 +274,7 @@ struct rt_scene {
         for (int q = 0; q < NLANE; q++) { unit_cost[q].release(); unit_order[q].release(); }
         delete blas_builder; delete tlas_builder;
         raw_tris.release(); raw_sph.release(); raw_quad.release(); blas_roots.release(); inst_blas.release();
-        gpu_counts.release();
+        gpu_counts.release(); inst_params.release();
         if (ev_render_done) (void)hipEventDestroy(ev_render_done);
         for (int b = 0; b < NLANE; b++) {
             if (staging[b]) (void)hipHostFree(staging[b]);
@@ -293,9 +299,23 @@ struct rt_scene {
 namespace {
 
 // Instance::updateTransformArguments (src/AS/Instance.cu:4-17)
+hm::V3 cos3(const rt_xform &x) {
+    hm::V3 c, s;
+    hm::rotate_cos_sin(x.rotate_deg.x, c.x, s.x);
+    hm::rotate_cos_sin(x.rotate_deg.y, c.y, s.y);
+    hm::rotate_cos_sin(x.rotate_deg.z, c.z, s.z);
+    return c;
+}
+hm::V3 sin3(const rt_xform &x) {
+    hm::V3 c, s;
+    hm::rotate_cos_sin(x.rotate_deg.x, c.x, s.x);
+    hm::rotate_cos_sin(x.rotate_deg.y, c.y, s.y);
+    hm::rotate_cos_sin(x.rotate_deg.z, c.z, s.z);
+    return s;
+}
 void instance_update(InstState &in, const rt_xform &x) {
     in.x = x;
-    in.fwd = hm::shift_matrix(hm::of(x.shift)) * hm::rotate_matrix(hm::of(x.rotate_deg)) * hm::scale_matrix(hm::of(x.scale));
+    in.fwd = hm::instance_matrix(hm::of(x.shift), cos3(x), sin3(x), hm::of(x.scale));
     in.inv = hm::inverse(in.fwd);
     in.nrm = hm::transpose(in.inv);
     in.tbox = hm::transform_box(in.box, in.fwd);
@@ -355,30 +375,48 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         for (size_t i = 0; i < xs.size(); i++) xs[i] = s->inst[i].x;
         s->update(s->update_user, xs.data(), xs.size(), frame);
         // matrices are a pure function of (local box, xform): only instances whose xform changed are
-        // recomputed (the demo animates 5 of C2's 73 instances)
+        // recomputed (the demo animates 5 of C2's 73 instances) — on the GPU for GPU-built frames
         for (size_t i = 0; i < xs.size(); i++)
-            if (std::memcmp(&xs[i], &s->inst[i].x, sizeof(rt_xform)) != 0) instance_update(s->inst[i], xs[i]);
+            if (std::memcmp(&xs[i], &s->inst[i].x, sizeof(rt_xform)) != 0) {
+                if (s->gpu_tlas()) { s->inst[i].x = xs[i]; s->inst_dirty[i] = 1; }
+                else instance_update(s->inst[i], xs[i]);
+            }
     }
     uint8_t *st = s->staging[b];
     InstHot *hot = reinterpret_cast<InstHot *>(st + s->off_hot);
     InstCold *cold = reinterpret_cast<InstCold *>(st + s->off_cold);
     if (s->gpu_tlas()) {
         s->block_by_slot[b] = false;                  // GPU-built TLASes keep instance order
-        float *tbox = reinterpret_cast<float *>(st + s->off_tbox);
-        float *tcent = reinterpret_cast<float *>(st + s->off_tcent);
+        // only the changed instances cross PCIe: (index, shift, cos / sin of the angles, scale, local box)
+        InstDelta *dl = reinterpret_cast<InstDelta *>(st + s->off_delta);
+        uint32_t nd = 0;
         for (size_t i = 0; i < s->inst.size(); i++) {
+            if (!s->inst_dirty[i]) continue;
+            s->inst_dirty[i] = 0;
             const InstState &in = s->inst[i];
-            store_rows(hot[i].inv, in.inv);
-            store_rows(cold[i].fwd, in.fwd);
-            store_rows(cold[i].nrm, in.nrm);
-            in.tbox.store(tbox + 6 * i);
-            tcent[4 * i] = in.tcentroid.x; tcent[4 * i + 1] = in.tcentroid.y; tcent[4 * i + 2] = in.tcentroid.z;
-            tcent[4 * i + 3] = 0.0f;
+            InstDelta &d = dl[nd++];
+            std::memset(&d, 0, sizeof d);
+            d.index = (uint32_t)i;
+            const hm::V3 c = cos3(in.x), sn = sin3(in.x);
+            for (int a = 0; a < 3; a++) {
+                d.p.shift[a] = hm::of(in.x.shift)[a];
+                d.p.cos[a] = c[a];
+                d.p.sin[a] = sn[a];
+                d.p.scale[a] = hm::of(in.x.scale)[a];
+                d.p.centroid[a] = in.centroid[a];
+            }
+            in.box.store(d.p.box);
         }
         uint8_t *fd = s->frame_dev[b];
         HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_used[b], 0));
         // a blit kernel reading the pinned staging block, not an SDMA copy (see the host-built path below)
-        HIP_TRY(launch_frame_copy(fd, s->staging_dev[b], s->frame_block, nullptr, s->stream));
+        if (nd) HIP_TRY(launch_frame_copy(fd + s->off_delta, s->staging_dev[b] + s->off_delta, nd * sizeof(InstDelta), nullptr,
+                                          s->stream));
+        // Instance::updateTransformArguments for every instance, on the GPU (instances.hip)
+        HIP_TRY(launch_instance_update(reinterpret_cast<const InstDelta *>(fd + s->off_delta), nd, s->inst_params.p,
+                                       (uint32_t)s->inst.size(), reinterpret_cast<InstHot *>(fd + s->off_hot),
+                                       reinterpret_cast<InstCold *>(fd + s->off_cold), reinterpret_cast<float *>(fd + s->off_tbox),
+                                       reinterpret_cast<float4 *>(fd + s->off_tcent), s->stream));
         if (s->rebuild_blas || s->blas_dirty) {
             const rt_status bs = gpu_build_blas(s);
             if (bs != RT_OK) return bs;
@@ -552,6 +590,12 @@ uint32_t tiles_for_rank(uint32_t w, uint32_t h, uint32_t tw, uint32_t th, uint32
 }
 
 }  // namespace
+
+template <typename T>
+static hipError_t read_back(std::vector<T> &v, const T *src, size_t n) {
+    v.resize(n);
+    return n ? hipMemcpy(v.data(), src, n * sizeof(T), hipMemcpyDeviceToHost) : hipSuccess;
+}
 
 static void fill_stats(rt_stats *st, const unsigned long long *c);
 
@@ -767,8 +811,11 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     s->off_tcent = align16(s->off_tbox + n * 6 * sizeof(float));
     s->off_root_wide = 32;                                         // second half of the root's 64 B
     s->off_quads = (s->off_tcent + n * 4 * sizeof(float) + 127) & ~size_t(127);
-    s->frame_block = s->off_quads + n * sizeof(NodeQuad);           // <= n - 1 quads
+    s->off_delta = align16(s->off_quads + n * sizeof(NodeQuad));   // <= n - 1 quads
+    s->frame_block = s->off_delta + (mode == RT_BUILD_LBVH ? n * sizeof(InstDelta) : 0);
     if (mode == RT_BUILD_LBVH) {
+        if ((st = alloc_buf(s->inst_params, n)) != RT_OK) return st;
+        s->inst_dirty.assign(n, 1);                                 // frame 0 uploads every instance
         delete s->tlas_builder;
         s->tlas_builder = new LbvhBuilder();
         const std::vector<LbvhSeg> tseg{LbvhSeg{0u, (uint32_t)n, 0u, 0u, 0u, 0u, LBVH_TLAS_LEAF_CAP, 0u}};
@@ -1302,6 +1349,35 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
     } else if (k == "costmap") {
         src = s->costmap.p;
         size = s->costmap_pixels * sizeof(uint32_t);
+    } else if (k == "instances") {
+        // GPU-built frames: the instance records the GPU computed for the current frame, in instance order,
+        // 45 floats each: inverse, forward, inverse-transpose rows 1-3 (12 each), transformed box, centroid
+        if (!s->built || !s->gpu_tlas()) return fail(RT_ERR_UNSUPPORTED, "instance records are computed on the GPU for RT_BUILD_LBVH only");
+        HIP_TRY(hipSetDevice(s->device));
+        HIP_TRY(drain(s));
+        const size_t n = s->inst.size();
+        *bytes = n * 45 * sizeof(float);
+        if (capacity) {
+            const uint8_t *fd = s->frame_dev[s->active];
+            std::vector<InstHot> hot;
+            std::vector<InstCold> cold;
+            std::vector<float> tbox, tcent;
+            HIP_TRY(read_back(hot, reinterpret_cast<const InstHot *>(fd + s->off_hot), n));
+            HIP_TRY(read_back(cold, reinterpret_cast<const InstCold *>(fd + s->off_cold), n));
+            HIP_TRY(read_back(tbox, reinterpret_cast<const float *>(fd + s->off_tbox), 6 * n));
+            HIP_TRY(read_back(tcent, reinterpret_cast<const float *>(fd + s->off_tcent), 4 * n));
+            std::vector<float> outv(n * 45);
+            for (size_t i = 0; i < n; i++) {
+                float *o = outv.data() + 45 * i;
+                std::memcpy(o, hot[i].inv, 12 * sizeof(float));
+                std::memcpy(o + 12, cold[i].fwd, 12 * sizeof(float));
+                std::memcpy(o + 24, cold[i].nrm, 12 * sizeof(float));
+                std::memcpy(o + 36, tbox.data() + 6 * i, 6 * sizeof(float));
+                std::memcpy(o + 42, tcent.data() + 4 * i, 3 * sizeof(float));
+            }
+            std::memcpy(dst, outv.data(), std::min(capacity, *bytes));
+        }
+        return RT_OK;
     } else if (k == "leaf_prims") {
         // caller triangle index of every leaf-ordered triangle slot (TriCold::orig_index): BLAS b owns
         // the slots [slot_base, slot_base + count) of its primitives, in leaf order
@@ -1401,6 +1477,7 @@ rt_status rt_scene_update_triangles(rt_scene *s, size_t first, size_t count, con
         in.centroid = in.pcount == 1 ? prim_centroid(s, in.ptype, in.pindex)
                                      : hm::v3((float)(c[0] / in.pcount), (float)(c[1] / in.pcount), (float)(c[2] / in.pcount));
         instance_update(in, in.x);
+        if (s->gpu_tlas()) s->inst_dirty[i] = 1;     // the GPU copy of its local box
     }
     s->blas_dirty = true;
     return RT_OK;
@@ -1426,6 +1503,7 @@ rt_status rt_scene_update_instances(rt_scene *s, size_t first, size_t count, con
             in.centroid = hm::of(d[k].local_centroid);
         }
         instance_update(in, d[k].xform);
+        if (s->gpu_tlas()) s->inst_dirty[i] = 1;
     }
     return RT_OK;
 }
@@ -1512,11 +1590,6 @@ static Tree tree_from_pairs(const TreeRoot &root, const std::vector<NodePair> &p
     return t;
 }
 
-template <typename T>
-static hipError_t read_back(std::vector<T> &v, const T *src, size_t n) {
-    v.resize(n);
-    return n ? hipMemcpy(v.data(), src, n * sizeof(T), hipMemcpyDeviceToHost) : hipSuccess;
-}
 
 extern "C" {
 

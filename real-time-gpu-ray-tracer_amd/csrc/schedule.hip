@@ -38,6 +38,7 @@ namespace {
 constexpr uint32_t SCHED_THREADS = 256;
 constexpr uint32_t SCHED_NIB_UNITS = 16384;    // band units whose class nibbles fit in 8 KB of LDS
 constexpr uint32_t SCHED_LOADS = 4;            // 8-byte cost loads in flight per thread
+constexpr uint32_t COPY_AHEAD = 2;             // 16-byte frame-block pieces loaded before the cost loads
 
 __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__restrict__ cost, uint32_t *__restrict__ cost_prev,
                                                                  uint32_t *__restrict__ order, uint32_t *__restrict__ queue,
@@ -51,12 +52,29 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
     const uint32_t part = blockIdx.x, t = threadIdx.x;
     if (part == 0 && t < QUEUE_MAX_PARTS) queue[t * QUEUE_STRIDE] = 0u;      // every head: `parts` may change
     if (part == 0 && zero_counters && t < CNT_NUM) zero_counters[t] = 0ull;  // the lane's work counters
-    // the frame's TLAS / instance block, read from pinned host staging (see launch_frame_copy)
-    for (uint32_t i = part * SCHED_THREADS + t; i < copy_n16; i += parts * SCHED_THREADS) copy_dst[i] = copy_src[i];
+    // the frame's TLAS / instance block, read from pinned host staging (see launch_frame_copy): the first
+    // COPY_AHEAD pieces per thread are loaded now and stored after the first cost loads have been issued,
+    // so the PCIe read and the cost reads overlap (vector loads return in order: one wait covers both)
+    const uint32_t cstride = parts * SCHED_THREADS;
+    uint4 ahead[COPY_AHEAD];
+#pragma unroll
+    for (uint32_t k = 0; k < COPY_AHEAD; k++) {
+        const uint32_t i = part * SCHED_THREADS + t + k * cstride;
+        ahead[k] = i < copy_n16 ? copy_src[i] : make_uint4(0u, 0u, 0u, 0u);
+    }
+    const auto finish_copy = [&]() {
+#pragma unroll
+        for (uint32_t k = 0; k < COPY_AHEAD; k++) {
+            const uint32_t i = part * SCHED_THREADS + t + k * cstride;
+            if (i < copy_n16) copy_dst[i] = ahead[k];
+        }
+        for (uint32_t i = part * SCHED_THREADS + t + COPY_AHEAD * cstride; i < copy_n16; i += cstride) copy_dst[i] = copy_src[i];
+    };
     // the band's unit range, computed exactly as the render kernel's refill computes it
     const uint32_t b0 = rows * part / parts * upr, b1 = rows * (part + 1) / parts * upr;
     const uint32_t n = b1 - b0;
     if (!do_order) {
+        finish_copy();
         for (uint32_t u = b0 + t; u < b1; u += SCHED_THREADS) { cost_prev[u] = cost[u]; cost[u] = 0u; }
         return;
     }
@@ -64,6 +82,7 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
     // offsets
     const uint32_t gbase = b0 & ~1u;
     const bool in_lds = b1 - gbase <= SCHED_NIB_UNITS && 4u * n < 65536u;
+    bool copied = false;
     if (in_lds) {
         // pass A: pairs of costs, coalesced 8-byte loads -> class codes; costs kept (debug) and cleared
         const uint32_t npair = (b1 - gbase + 1) / 2;
@@ -74,6 +93,7 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
                 const uint32_t i = i0 + k * SCHED_THREADS;
                 v[k] = i < npair ? reinterpret_cast<const uint2 *>(cost + gbase)[i] : make_uint2(0u, 0u);
             }
+            if (!copied) { finish_copy(); copied = true; }
 #pragma unroll
             for (uint32_t k = 0; k < SCHED_LOADS; k++) {
                 const uint32_t i = i0 + k * SCHED_THREADS;
@@ -92,6 +112,7 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
             }
         }
     }
+    if (!copied) finish_copy();
     __syncthreads();
     if (!in_lds) {
         // a band of >= 16384 units (beyond 4K with 8 bands): screen order, one item per unit
