@@ -340,6 +340,8 @@ rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
  *   "instances": RT_BUILD_LBVH: 45 floats per instance, the records the GPU computed for the current frame
  *               (instances.hip): inverse, forward and inverse-transpose rows 1-3 (12 each), transformed box
  *               {xmin,xmax,ymin,ymax,zmin,zmax}, transformed centroid;
+ *   "blas_pairs", "blas_quads", "blas_roots": RT_BUILD_LBVH: the GPU-built forest as NodePair / NodeQuad /
+ *               TreeRoot records (csrc/layout.hpp; quad q is the 4-wide node rooted at pair q);
  *   "leaf_prims": 1 u32 per leaf-ordered triangle slot: the caller's triangle index stored there (each
  *               BLAS owns the contiguous slots of its primitives, in leaf order).
  * Copies min(capacity, size) bytes to dst and stores the buffer's full size in *bytes. */

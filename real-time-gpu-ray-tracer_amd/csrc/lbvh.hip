@@ -500,6 +500,89 @@ __global__ void gather_items_kernel(const LbvhSeg *segs, const unsigned long lon
     slots[S.slot_base + (p - S.item_base)] = vals[p];
 }
 
+// ---- 4-wide collapse of a built forest (the quad form the FAST persistent kernel traverses) -------
+// Restates flatten_tree_wide (bvh_build.hpp) on the GPU: a quad starts from an interior node's two
+// children and twice replaces its largest-half-area interior child (first on ties) by that child's two
+// children, so a ray descends half as many dependent levels; leaves and boxes are the binary tree's.  Quad
+// q is the quad rooted at node pair q (pair indices are unique across the forest, so the interior refs the
+// pairs hold are also the quads' refs, and a tree's quad root ref equals its pair root ref).  One
+// workgroup per tree walks it level by level: a frontier of quad roots in LDS (global scratch, this tree's
+// pair range, for trees of more than LDS_FRONT pairs).
+constexpr uint32_t LDS_FRONT = 1024;
+
+__device__ __forceinline__ float half_area(const float *b) {
+    const float dx = b[1] - b[0], dy = b[3] - b[2], dz = b[5] - b[4];
+    return dx * dy + dy * dz + dz * dx;
+}
+
+__global__ __launch_bounds__(BLOCK) void collapse_wide_kernel(const LbvhSeg *segs, const TreeRoot *roots, const NodePair *pairs,
+                                                              NodeQuad *quads, uint32_t *scratch, uint32_t scratch_half,
+                                                              TreeRoot *roots_wide) {
+    __shared__ uint32_t lds_front[2][LDS_FRONT];
+    __shared__ uint32_t n_cur, n_next;
+    const uint32_t s = blockIdx.x, t = threadIdx.x;
+    const TreeRoot R = roots[s];
+    if (roots_wide && t == 0) roots_wide[s] = R;              // quad root ref == pair root ref
+    if ((R.ref & REF_LEAF) || R.ref == NONE) return;          // a leaf (or empty) tree has no quads
+    const uint32_t root = R.ref & REF_INDEX_MASK;
+    const bool blas = (R.ref & REF_BLAS) != 0;
+    const uint32_t max_pairs = segs[s].count > 1 ? segs[s].count - 1 : 1;
+    uint32_t *front[2];
+    if (max_pairs <= LDS_FRONT) { front[0] = lds_front[0]; front[1] = lds_front[1]; }
+    else {          // this tree's own pair range [root, root + its pairs): a frontier never holds more
+        front[0] = scratch + root;
+        front[1] = scratch + scratch_half + root;
+    }
+    if (t == 0) { front[0][0] = root; n_cur = 1; n_next = 0; }
+    __syncthreads();
+    uint32_t cur = 0;
+    while (n_cur > 0) {
+        const uint32_t nc_level = n_cur;
+        for (uint32_t i = t; i < nc_level; i += BLOCK) {
+            const uint32_t q = front[cur][i];
+            float box[4][6];
+            uint32_t ref[4];
+            const NodePair P = pairs[q];
+#pragma unroll
+            for (int k = 0; k < 6; k++) { box[0][k] = P.c0[k]; box[1][k] = P.c1[k]; }
+            ref[0] = P.ref0; ref[1] = P.ref1;
+            uint32_t nc = 2;
+            while (nc < 4) {
+                int best = -1;
+                float area = -1.0f;
+                for (uint32_t k = 0; k < nc; k++)
+                    if (!(ref[k] & REF_LEAF) && half_area(box[k]) > area) { area = half_area(box[k]); best = (int)k; }
+                if (best < 0) break;
+                const NodePair C = pairs[ref[best] & REF_INDEX_MASK];
+                for (int k = 0; k < 6; k++) { box[best][k] = C.c0[k]; box[nc][k] = C.c1[k]; }
+                ref[best] = C.ref0;
+                ref[nc] = C.ref1;
+                nc++;
+            }
+            NodeQuad Q;
+            for (uint32_t k = 0; k < 4; k++) {
+                const bool used = k < nc;
+                const float inf = __builtin_huge_valf();           // empty slot: rejected by every slab test
+                Q.lo_x[k] = used ? box[k][0] : inf; Q.hi_x[k] = used ? box[k][1] : inf;
+                Q.lo_y[k] = used ? box[k][2] : inf; Q.hi_y[k] = used ? box[k][3] : inf;
+                Q.lo_z[k] = used ? box[k][4] : inf; Q.hi_z[k] = used ? box[k][5] : inf;
+                Q.ref[k] = used ? ref[k] : REF_EMPTY;
+                Q.pad[k] = 0;
+                if (used && !(ref[k] & REF_LEAF)) front[cur ^ 1][atomicAdd(&n_next, 1u)] = ref[k] & REF_INDEX_MASK;
+            }
+            float4 *dst = reinterpret_cast<float4 *>(quads + q);
+            const float4 *src = reinterpret_cast<const float4 *>(&Q);
+#pragma unroll
+            for (int k = 0; k < 8; k++) dst[k] = src[k];
+            (void)blas;
+        }
+        __syncthreads();
+        if (t == 0) { n_cur = n_next; n_next = 0; }
+        cur ^= 1;
+        __syncthreads();
+    }
+}
+
 }  // namespace lbvh
 
 // ---- host --------------------------------------------------------------------------------------
@@ -524,7 +607,7 @@ static void dfree(T *&p) {
 void LbvhBuilder::release() {
     dfree(segs_); dfree(seg_of_); dfree(own_box_); dfree(own_cent_); dfree(bounds_);
     dfree(k0_); dfree(k1_); dfree(v0_); dfree(v1_); dfree(child_); dfree(parent_); dfree(parent_leaf_);
-    dfree(range_); dfree(flag_); dfree(height_); dfree(nbox_); dfree(kept_); dfree(pidx_);
+    dfree(range_); dfree(flag_); dfree(height_); dfree(nbox_); dfree(kept_); dfree(pidx_); dfree(front_);
     if (tmp_) (void)hipFree(tmp_);
     tmp_ = nullptr; tmp_bytes_ = 0;
     box_ = nullptr; cent_ = nullptr;
@@ -623,6 +706,14 @@ hipError_t LbvhBuilder::gather_blas(const RawPrimsGPU &raw, const PrimOutGPU &ou
     return hipGetLastError();
 }
 
+hipError_t LbvhBuilder::collapse_wide(const NodePair *pairs, const TreeRoot *roots, NodeQuad *quads, TreeRoot *roots_wide,
+                                      hipStream_t stream) {
+    if (max_count_ - 1 > LDS_FRONT && !front_) LB_TRY(dalloc(front_, 2 * (size_t)max_pairs()));
+    hipLaunchKernelGGL(collapse_wide_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, roots, pairs, quads, front_,
+                       max_pairs(), roots_wide);
+    return hipGetLastError();
+}
+
 hipError_t LbvhBuilder::gather_items(uint32_t *slots, hipStream_t stream) {
     hipLaunchKernelGGL(gather_items_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, n_items_,
                        slots);
@@ -642,7 +733,7 @@ __global__ void patch_roots_kernel(InstHot *hot, const uint32_t *inst_blas, cons
 #pragma unroll
     for (int k = 0; k < 6; k++) hot[i].root_box[k] = R.box[k];
     hot[i].root_ref = R.ref;
-    hot[i].root_ref_wide = R.ref;       // GPU-built trees have no quad form ("wide" needs host trees)
+    hot[i].root_ref_wide = R.ref;       // the quad root of a GPU-built tree has the pair root's ref (collapse_wide_kernel)
 }
 }  // namespace lbvh
 

@@ -79,6 +79,10 @@ public:
 
     // After build(): leaf-ordered BLAS primitive records.
     hipError_t gather_blas(const RawPrimsGPU &raw, const PrimOutGPU &out, hipStream_t stream);
+    // After build(): the 4-wide form of every tree (quads[q] = the quad rooted at node pair q, capacity
+    // max_pairs()); roots_wide (may be null) receives each tree's root for the quad traversal.
+    hipError_t collapse_wide(const NodePair *pairs, const TreeRoot *roots, NodeQuad *quads, TreeRoot *roots_wide,
+                             hipStream_t stream);
     // After build(): item index per leaf slot (TLAS: instance index per slot).
     hipError_t gather_items(uint32_t *slots, hipStream_t stream);
 
@@ -101,6 +105,7 @@ private:
     uint32_t *height_ = nullptr;          // per interior node
     float *nbox_ = nullptr;               // 6 per interior node
     uint32_t *kept_ = nullptr, *pidx_ = nullptr;
+    uint32_t *front_ = nullptr;           // collapse_wide frontier of trees too large for LDS
     void *tmp_ = nullptr;
     size_t tmp_bytes_ = 0;
 };

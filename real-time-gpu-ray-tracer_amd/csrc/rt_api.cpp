@@ -428,6 +428,10 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
                                            reinterpret_cast<const float4 *>(fd + s->off_tcent)));
         HIP_TRY(s->tlas_builder->build(reinterpret_cast<NodePair *>(fd + s->off_pairs), reinterpret_cast<TreeRoot *>(fd + s->off_root),
                                        s->gpu_counts.p + 1, s->stream));
+        HIP_TRY(s->tlas_builder->collapse_wide(reinterpret_cast<const NodePair *>(fd + s->off_pairs),
+                                               reinterpret_cast<const TreeRoot *>(fd + s->off_root),
+                                               reinterpret_cast<NodeQuad *>(fd + s->off_quads),
+                                               reinterpret_cast<TreeRoot *>(fd + s->off_root_wide), s->stream));
         HIP_TRY(s->tlas_builder->gather_items(reinterpret_cast<uint32_t *>(fd + s->off_slots), s->stream));
         HIP_TRY(hipEventRecord(s->ev_copied[b], s->stream));
         s->active = b;
@@ -490,7 +494,7 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.tlas_root_wide = reinterpret_cast<const TreeRoot *>(s->frame_dev[b] + s->off_root_wide);
     g.tlas_quads = reinterpret_cast<const NodeQuad *>(s->frame_dev[b] + s->off_quads);
     g.blas_quads = s->blas_quads.p;
-    g.wide = s->wide && !s->gpu_tlas() && s->blas_quads.p != nullptr ? 1u : 0u;
+    g.wide = s->wide && s->blas_quads.p != nullptr ? 1u : 0u;   // GPU-built trees: quads from collapse_wide
     g.tlas_slots = reinterpret_cast<const uint32_t *>(s->frame_dev[b] + s->off_slots);
     g.inst_hot = reinterpret_cast<const InstHot *>(s->frame_dev[b] + s->off_hot);
     g.inst_cold = reinterpret_cast<const InstCold *>(s->frame_dev[b] + s->off_cold);
@@ -532,6 +536,7 @@ rt_status gpu_build_blas(rt_scene *s) {
     const PrimOutGPU out{s->tri_hot.p, s->tri_cold.p, s->sph_hot.p, s->sph_cold.p, s->quad_hot.p, s->quad_cold.p};
     HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
     HIP_TRY(s->blas_builder->build(s->blas_pairs.p, s->blas_roots.p, s->gpu_counts.p, s->stream));
+    HIP_TRY(s->blas_builder->collapse_wide(s->blas_pairs.p, s->blas_roots.p, s->blas_quads.p, nullptr, s->stream));
     HIP_TRY(s->blas_builder->gather_blas(raw, out, s->stream));
     s->blas_dirty = false;
     s->blas_builds++;
@@ -563,6 +568,7 @@ rt_status gpu_setup_blas(rt_scene *s, const std::vector<LbvhSeg> &segs, const ui
     s->blas_builder = new LbvhBuilder();
     HIP_TRY(s->blas_builder->init(segs, s->stream));
     if ((st = alloc_buf(s->blas_pairs, s->blas_builder->max_pairs())) != RT_OK) return st;
+    if ((st = alloc_buf(s->blas_quads, s->blas_builder->max_pairs())) != RT_OK) return st;   // quad q = rooted at pair q
     if ((st = alloc_buf(s->blas_roots, segs.size())) != RT_OK) return st;
     if ((st = alloc_buf(s->gpu_counts, 2)) != RT_OK) return st;
     std::vector<uint32_t> ib(s->inst.size());
@@ -1377,6 +1383,17 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
             }
             std::memcpy(dst, outv.data(), std::min(capacity, *bytes));
         }
+        return RT_OK;
+    } else if (k == "blas_pairs" || k == "blas_quads" || k == "blas_roots") {
+        // RT_BUILD_LBVH: the forest as built on the GPU (NodePair / NodeQuad / TreeRoot records, layout.hpp)
+        if (!s->built || !s->gpu_tlas()) return fail(RT_ERR_UNSUPPORTED, "raw BLAS records are exported for RT_BUILD_LBVH only");
+        HIP_TRY(hipSetDevice(s->device));
+        HIP_TRY(drain(s));
+        const void *from = k == "blas_pairs" ? (const void *)s->blas_pairs.p
+                                             : (k == "blas_quads" ? (const void *)s->blas_quads.p : (const void *)s->blas_roots.p);
+        *bytes = k == "blas_roots" ? s->blas.size() * sizeof(TreeRoot)
+                                   : s->blas_pair_count * (k == "blas_pairs" ? sizeof(NodePair) : sizeof(NodeQuad));
+        if (capacity && *bytes) HIP_TRY(hipMemcpy(dst, from, std::min(capacity, *bytes), hipMemcpyDeviceToHost));
         return RT_OK;
     } else if (k == "leaf_prims") {
         // caller triangle index of every leaf-ordered triangle slot (TriCold::orig_index): BLAS b owns

@@ -250,3 +250,81 @@ def test_rebuild_sah_then_lbvh_equals_fresh_lbvh(gpu_lib):
     got = r.trace_rays(rays)
     for k in ("t", "instance", "pindex", "ptype", "point", "normal"):
         assert np.array_equal(got[k], want_hits[k]), k
+
+
+PAIR_DT = np.dtype([("c0", np.float32, 6), ("c1", np.float32, 6), ("ref0", np.uint32), ("ref1", np.uint32),
+                    ("pad", np.uint32, 2)])
+QUAD_DT = np.dtype([("lo_x", np.float32, 4), ("hi_x", np.float32, 4), ("lo_y", np.float32, 4), ("hi_y", np.float32, 4),
+                    ("lo_z", np.float32, 4), ("hi_z", np.float32, 4), ("ref", np.uint32, 4), ("pad", np.uint32, 4)])
+ROOT_DT = np.dtype([("box", np.float32, 6), ("ref", np.uint32), ("height", np.uint32)])
+REF_LEAF, REF_INDEX = 1 << 31, (1 << 30) - 1
+
+
+def _half_area(b):
+    f = np.float32
+    dx, dy, dz = f(b[1]) - f(b[0]), f(b[3]) - f(b[2]), f(b[5]) - f(b[4])
+    return f(f(dx * dy) + f(dy * dz)) + f(dz * dx)
+
+
+def _expected_quads(pairs, root_ref):
+    """csrc/bvh_build.hpp flatten_tree_wide restated on the GPU's own node pairs: quad q rooted at pair q
+    holds q's two children, twice expanding the largest-half-area interior child (first on ties)."""
+    out, todo = {}, ([root_ref & REF_INDEX] if not root_ref & REF_LEAF else [])
+    while todo:
+        q = todo.pop()
+        p = pairs[q]
+        box, ref = [p["c0"].copy(), p["c1"].copy()], [int(p["ref0"]), int(p["ref1"])]
+        while len(ref) < 4:
+            cand = [(k, _half_area(box[k])) for k in range(len(ref)) if not ref[k] & REF_LEAF]
+            if not cand:
+                break
+            best = max(cand, key=lambda kv: (kv[1], -kv[0]))[0]     # largest area, first on ties
+            c = pairs[ref[best] & REF_INDEX]
+            box[best], ref[best] = c["c0"].copy(), int(c["ref0"])
+            box.append(c["c1"].copy())
+            ref.append(int(c["ref1"]))
+        out[q] = (box, ref)
+        todo += [r & REF_INDEX for r in ref if not r & REF_LEAF]
+    return out
+
+
+@pytest.mark.parametrize("mode", ["particles", "large"])
+def test_gpu_quad_collapse_equals_restatement(gpu_lib, mode):
+    """RT_BUILD_LBVH trees get the 4-wide form on the GPU (collapse_wide_kernel, lbvh.hip): every quad equals
+    the host collapse rule applied to the GPU's binary tree (bit for bit, slot order included), and the quad
+    traversal renders the binary traversal's frame within the FAST tolerance with the same ray count."""
+    if mode == "particles":
+        s = scenes.demo_with_particles(12)
+    else:   # one BLAS of 65k triangles: its frontier lives in global scratch, not LDS
+        tris, inst = scenes.synth_particles(64, 1024, seed=3)
+        s = scenes.demo_scene()
+        s.triangles = np.concatenate([tris, s.triangles])
+        for d in s.instances:
+            if d["type"] == 2:
+                d["index"] += tris.shape[0]
+        s.instances.append(dict(type=2, index=0, count=tris.shape[0], shift=(0.0, 4.0, 0.0), rotate=(90.0, 0.0, 0.0),
+                                scale=(3.0, 3.0, 3.0)))
+    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(240, 136, ray_trace_depth=2)
+    pairs = r.debug_read("blas_pairs").view(PAIR_DT)
+    quads = r.debug_read("blas_quads").view(QUAD_DT)
+    roots = r.debug_read("blas_roots").view(ROOT_DT)
+    n_quads = 0
+    for b in range(len(roots)):
+        for q, (box, ref) in _expected_quads(pairs, int(roots[b]["ref"])).items():
+            g = quads[q]
+            n = len(ref)
+            assert list(g["ref"][:n]) == ref and (g["ref"][n:] == 0xFFFFFFFF).all(), (b, q)
+            for k in range(n):
+                got = [g["lo_x"][k], g["hi_x"][k], g["lo_y"][k], g["hi_y"][k], g["lo_z"][k], g["hi_z"][k]]
+                assert np.array_equal(np.asarray(got, np.float32), box[k]), (b, q, k)
+            assert np.isinf(g["lo_x"][n:]).all()
+            n_quads += 1
+    assert n_quads > 0
+    out = {}
+    for wide in (0, 1):
+        r.set_option("wide", wide)
+        out[wide] = r.render(3, count_work=True)
+    f, mx = frac_within(out[0][0], out[1][0])
+    assert f >= 0.999, (f, mx)
+    assert abs(out[0][2]["rays"] - out[1][2]["rays"]) <= 0.001 * out[0][2]["rays"]
+    assert out[1][2]["aabb_tests"] != out[0][2]["aabb_tests"]          # the quad form really ran
