@@ -53,7 +53,7 @@ def parse():
     p.add_argument("--threshold", type=int, default=None, help="refill threshold (default: the library's tuned value)")
     p.add_argument("--overlap", type=int, default=None,
                    help="L >= 2: consecutive frames cycle L streams / library lanes so frame k+1 fills the CUs "
-                        "frame k's tail leaves idle; 0 or 1: frames are serialised (default 2 at N=1, 3 at N>1)")
+                        "frame k's tail leaves idle; 0 or 1: frames are serialised (default 3)")
     p.add_argument("--shard", default=None, help="R/N: trace only rank R's tiles of an N-rank split on this one GPU "
                                                  "(per-rank cost study; no gather)")
     p.add_argument("--opt", action="append", default=[], help="extra rt_scene_set_option key=value (A/B studies)")
@@ -184,8 +184,8 @@ def main():
     for kv in args.opt:
         k, v = kv.split("=")
         r.set_option(k, int(v, 0))
-    # measured: 2 lanes best at N=1, 3 lanes for a rank's 1/N share
-    L = max(1, args.overlap if args.overlap is not None else (3 if n > 1 else 2))
+    # measured (profiles/r02_sweep_lanes.jsonl): 3 lanes best at N=1 and for a rank's 1/N share
+    L = max(1, args.overlap if args.overlap is not None else 3)
     overlap = L > 1
     if overlap:
         r.set_option("overlap", L)

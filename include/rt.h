@@ -318,8 +318,8 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "blas_leaf" : RT_BUILD_SAH: primitives per BLAS leaf (1..4, default 4; set before rt_scene_build)
  *   "inst_by_slot": 1 = host-built TLAS: stage the per-frame instance records in TLAS leaf-slot order
  *                 (default 1; 0 = instance order, for A/B — results are identical)
- *   "reserve"   : with "overlap", the persistent grid leaves this many workgroup slots free (default 8, one
- *                 per XCD) so the next lane's schedule / upload / GPU TLAS kernels start beside the running launch
+ *   "reserve"   : with "overlap", the persistent grid leaves this many workgroup slots free (default 16, two
+ *                 per XCD) so the next lanes' schedule / upload / GPU TLAS kernels start beside the running launch
  *   "overlap"   : L = consecutive rt_render calls cycle through L (2..4) internal lanes (work-queue
  *                 heads, unit costs, schedule); a launch waits only for the previous launch of its own
  *                 lane and for its frame block, so a caller that cycles L streams runs frame

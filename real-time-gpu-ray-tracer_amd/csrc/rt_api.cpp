@@ -187,10 +187,11 @@ struct rt_scene {
     bool inst_by_slot = true;       // option "inst_by_slot": host-built TLAS stages instance records in slot order
     bool block_by_slot[NLANE] = {};  // per frame block: staged in slot order
     uint32_t lanes = 1;
-    // option "reserve": with overlapped lanes the persistent grid leaves this many workgroup slots free (one
-    // per XCD at 8), so the next lane's schedule / upload kernels and GPU TLAS builds run beside a launch
-    // that holds the rest of the GPU instead of waiting for its drain
-    uint32_t reserve = 8;
+    // option "reserve": with overlapped lanes the persistent grid leaves this many workgroup slots free (two
+    // per XCD at 16), so the next lanes' schedule / upload kernels and GPU TLAS builds run beside a launch
+    // that holds the rest of the GPU instead of waiting for its drain (C2, 3 lanes: 16 -> 0.260-0.261,
+    // 8 -> 0.261-0.265, 0 -> 0.268-0.272 ms/frame; profiles/r02_sweep_lanes.jsonl)
+    uint32_t reserve = 16;
     uint32_t lane = 0;              // lane of the next rt_render (overlap)
     int last_lane = 0;              // lane of the last rt_render
     hipEvent_t ev_lane_done[NLANE] = {};   // last trace launch of each lane finished
