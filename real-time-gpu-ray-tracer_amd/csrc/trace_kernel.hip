@@ -45,6 +45,9 @@ constexpr float TMIN = 0.001f;          // Kernel.cu:66
 constexpr int BLOCK = 256;              // 4 waves; each wave owns one 8x8 pixel unit
 constexpr int LDS_DEPTH = 16;           // per-lane stack entries kept in LDS
 constexpr int SPILL_DEPTH = 48;         // overflow entries in scratch (max depth 64 = reference)
+#ifndef TRI_AHEAD
+#define TRI_AHEAD 2                     // triangle records of a leaf requested before the first test
+#endif
 
 struct f3 { float x, y, z; };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
@@ -598,23 +601,50 @@ __device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEn
         else pop_next(T, spill);
     } else {
         const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf), type = ref_leaf_type(leaf);
-        for (uint32_t k = 0; k < count; k++) {
-            const uint32_t slot = start + k;
-            float t = 0.0f, u = 0.0f, v = 0.0f;
-            bool h;
-            if (type == RT_PRIM_TRIANGLE) {
-                if (COUNT) cnt.tri++;
-                h = tri_test(sc.tri_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
-            } else if (type == RT_PRIM_SPHERE) {
-                if (COUNT) cnt.sq++;
-                h = sphere_test(sc.sph_hot[slot], T.lr, TMIN, T.tmax, t);
-            } else {
-                if (COUNT) { cnt.sq++; cnt.quad++; }
-                h = quad_test(sc.quad_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
+        if (type == RT_PRIM_TRIANGLE) {
+            // every triangle record of the leaf is requested before the first test: one memory round
+            // trip per leaf instead of one per triangle (tests still run in leaf order, BLAS.cu:153-176)
+            for (uint32_t k0 = 0; k0 < count; k0 += TRI_AHEAD) {
+                TriHot H[TRI_AHEAD];           // 3 x 12 B loads per triangle (the pad words stay unread)
+#pragma unroll
+                for (uint32_t k = 0; k < TRI_AHEAD; k++)
+                    if (k0 + k < count) {
+                        const float *src = sc.tri_hot[start + k0 + k].v0;
+                        const float3 a = *reinterpret_cast<const float3 *>(src);
+                        const float3 b = *reinterpret_cast<const float3 *>(src + 4);
+                        const float3 c = *reinterpret_cast<const float3 *>(src + 8);
+                        H[k].v0[0] = a.x; H[k].v0[1] = a.y; H[k].v0[2] = a.z;
+                        H[k].e1[0] = b.x; H[k].e1[1] = b.y; H[k].e1[2] = b.z;
+                        H[k].e2[0] = c.x; H[k].e2[1] = c.y; H[k].e2[2] = c.z;
+                    }
+#pragma unroll
+                for (uint32_t k = 0; k < TRI_AHEAD; k++) {
+                    if (k0 + k >= count) break;
+                    float t = 0.0f, u = 0.0f, v = 0.0f;
+                    if (COUNT) cnt.tri++;
+                    if (tri_test(H[k], T.lr, TMIN, T.tmax, t, u, v)) {
+                        T.found = true; T.tmax = t;
+                        T.hit.t = t; T.hit.inst = T.cur_inst; T.hit.ptype = type; T.hit.slot = start + k0 + k;
+                        T.hit.u = u; T.hit.v = v;
+                    }
+                }
             }
-            if (h) {
-                T.found = true; T.tmax = t;
-                T.hit.t = t; T.hit.inst = T.cur_inst; T.hit.ptype = type; T.hit.slot = slot; T.hit.u = u; T.hit.v = v;
+        } else {
+            for (uint32_t k = 0; k < count; k++) {
+                const uint32_t slot = start + k;
+                float t = 0.0f, u = 0.0f, v = 0.0f;
+                bool h;
+                if (type == RT_PRIM_SPHERE) {
+                    if (COUNT) cnt.sq++;
+                    h = sphere_test(sc.sph_hot[slot], T.lr, TMIN, T.tmax, t);
+                } else {
+                    if (COUNT) { cnt.sq++; cnt.quad++; }
+                    h = quad_test(sc.quad_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
+                }
+                if (h) {
+                    T.found = true; T.tmax = t;
+                    T.hit.t = t; T.hit.inst = T.cur_inst; T.hit.ptype = type; T.hit.slot = slot; T.hit.u = u; T.hit.v = v;
+                }
             }
         }
         if (T.cur != REF_NONE && !(T.curT < T.tmax)) pop_next(T, spill);   // re-test the successor
