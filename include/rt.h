@@ -201,6 +201,8 @@ typedef struct rt_stats {
     double kernel_ms;          /* device time of the trace kernel (HIP events)             */
     double frame_ms;           /* host wall time of the call                               */
     double update_ms;          /* host time of instance update + TLAS rebuild + upload     */
+    double update_wait_ms;     /* part of update_ms blocked on the GPU (a staging buffer still
+                                  read by an earlier frame's copy); the rest is host compute */
 } rt_stats;
 
 /* Closest-hit record for rt_trace_rays (per-ray parity tests). */
@@ -303,9 +305,11 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "reorder"   : 1 (default) = each launch claims its band's 8x8 units heaviest-first, ordered by the
  *                 traversal work the previous launch of the same layout and lane recorded per unit (schedule.hip);
  *                 0 = screen order.  Images are identical either way (the RNG is keyed by pixel).
+ *   "reorder_period": with "reorder", K = a lane records unit costs on one launch in K and rebuilds its
+ *                 claim order on the next; the other launches reuse the order (default 8; 1 = every launch)
  *   "split"     : with "reorder", heavy units are claimed in pieces shared by several waves: halves from
  *                 cost level k_half, quarters from k_quarter (value k_half | k_quarter << 8, levels 0..15 =
- *                 half-octaves of a unit's mean traversal steps per pixel; 0xFF = never; default 10 | 12 << 8)
+ *                 half-octaves of a unit's mean traversal steps per pixel; 0xFF = never; default 12 | 12 << 8)
  *   "lean"      : 1 = FAST persistent kernel uses the LDS-only-stack traversal (default 0) when the
  *                 TLAS height + deepest BLAS height + 2 <= 24
  *   "nt_store"  : 1 = non-temporal RGBA8 stores
@@ -316,6 +320,9 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal steps (debug)
  *   "tlas_leaf" : RT_BUILD_SAH: instances per leaf of the per-frame TLAS (1..4, default 1)
  *   "blas_leaf" : RT_BUILD_SAH: primitives per BLAS leaf (1..4, default 4; set before rt_scene_build)
+ *   "gpu_tlas"  : RT_BUILD_SAH: 1 = keep the host-built SAH BLASes but compute the instance records and
+ *                 build the TLAS on the GPU every frame, as RT_BUILD_LBVH does (only changed instances
+ *                 cross PCIe; no host TLAS build per frame).  Set before rt_scene_build (default 0)
  *   "inst_by_slot": 1 = host-built TLAS: stage the per-frame instance records in TLAS leaf-slot order
  *                 (default 1; 0 = instance order, for A/B — results are identical)
  *   "reserve"   : with "overlap", the persistent grid leaves this many workgroup slots free (default 16, two
@@ -337,7 +344,7 @@ rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
  *   "unit_cost", "unit_order": option "reorder" — per 8x8 unit, the work the lane's last launch recorded
  *               (after the next launch's schedule: the costs that schedule read), and the claim order the
  *               last launch used (band b's items start at 4 x its first unit: unit << 4 | piece << 2 | log2 pieces);
- *   "instances": RT_BUILD_LBVH: 45 floats per instance, the records the GPU computed for the current frame
+ *   "instances": RT_BUILD_LBVH or "gpu_tlas": 45 floats per instance, the records the GPU computed for the current frame
  *               (instances.hip): inverse, forward and inverse-transpose rows 1-3 (12 each), transformed box
  *               {xmin,xmax,ymin,ymax,zmin,zmax}, transformed centroid;
  *   "blas_pairs", "blas_quads", "blas_roots": RT_BUILD_LBVH: the GPU-built forest as NodePair / NodeQuad /

@@ -95,8 +95,11 @@ inline float half_area(const hm::Box &b) {
     return dx * dy + dy * dz + dz * dx;
 }
 
-inline Tree build_sah_tree(std::vector<BuildItem> items, uint32_t leaf_cap, float c_trav = 1.0f, float c_isect = 1.0f,
-                           uint32_t sweep_max = 4096) {
+// Reference form: every node re-sorts its items along each axis (O(n log^2 n)); build_sah_tree below
+// produces the same tree from lists presorted once.  Kept for lists above sweep_max (binned planes) and as
+// the equivalence check's reference (tests/cpp/sah_presort_check.cpp).
+inline Tree build_sah_tree_nodewise(std::vector<BuildItem> items, uint32_t leaf_cap, float c_trav = 1.0f,
+                                    float c_isect = 1.0f, uint32_t sweep_max = 4096) {
     Tree t;
     const uint32_t n = (uint32_t)items.size();
     t.nodes.resize(n ? 2 * (size_t)n - 1 : 0);
@@ -212,6 +215,115 @@ inline Tree build_sah_tree(std::vector<BuildItem> items, uint32_t leaf_cap, floa
         node.index = left;
         stack.push_back({task.start + mid, cnt - mid, left + 1});
         stack.push_back({task.start, mid, left});
+    }
+    t.nodes.resize(node_count);
+    return t;
+}
+
+// The exact-sweep SAH build (n <= sweep_max) from three centroid-sorted index lists sorted once and
+// split stably at every node, O(n log n): the per-frame SAH TLAS over C3's 258 instances took 0.29 ms
+// with per-node sorting, which bounded a C4 rank's frame rate (scripts/host_overhead.py).  The tree is
+// identical to build_sah_tree_nodewise's: the same (centroid, index) orders, the same cost arithmetic
+// over the same boxes (min / max merges do not depend on merge order), the same tie rules, the same
+// item order inside leaves and under "all centroids equal" splits, and the same DFS numbering.
+inline Tree build_sah_tree(std::vector<BuildItem> items, uint32_t leaf_cap, float c_trav = 1.0f, float c_isect = 1.0f,
+                           uint32_t sweep_max = 4096) {
+    const uint32_t n = (uint32_t)items.size();
+    if (n > sweep_max) return build_sah_tree_nodewise(std::move(items), leaf_cap, c_trav, c_isect, sweep_max);
+    Tree t;
+    t.nodes.resize(n ? 2 * (size_t)n - 1 : 0);
+    t.refs.reserve(n);
+    if (n == 0) return t;
+    // ord[a]: item ids sorted by (centroid[a], index) inside every pending node's range; cur: the node's
+    // incoming order (its parent's split order), which the nodewise builder leaves in place when no axis
+    // of the node has centroid extent
+    std::vector<uint32_t> ord[3], cur(n), tmp(n);
+    std::vector<uint8_t> left_side(n);
+    for (int a = 0; a < 3; a++) {
+        ord[a].resize(n);
+        for (uint32_t i = 0; i < n; i++) ord[a][i] = i;
+        std::sort(ord[a].begin(), ord[a].end(), [&](uint32_t x, uint32_t y) {
+            const float fa = items[x].centroid[a], fb = items[y].centroid[a];
+            return fa < fb || (!(fb < fa) && items[x].index < items[y].index);
+        });
+    }
+    for (uint32_t i = 0; i < n; i++) cur[i] = i;
+    struct Task { uint32_t start, count, node; };
+    std::vector<Task> stack;
+    stack.push_back({0, n, 0});
+    uint32_t node_count = 1;
+    std::vector<float> right_area(n + 1);
+    while (!stack.empty()) {
+        const Task task = stack.back();
+        stack.pop_back();
+        TreeNode &node = t.nodes[task.node];
+        const uint32_t s0 = task.start, cnt = task.count;
+        const uint32_t *o0 = ord[0].data() + s0;
+        hm::Box bb = items[o0[0]].box;
+        hm::Box cb{{{items[o0[0]].centroid.x, items[o0[0]].centroid.x},
+                    {items[o0[0]].centroid.y, items[o0[0]].centroid.y},
+                    {items[o0[0]].centroid.z, items[o0[0]].centroid.z}}};
+        for (uint32_t i = 1; i < cnt; i++) {
+            const BuildItem &it = items[o0[i]];
+            bb = hm::Box::merge(bb, it.box);
+            for (int a = 0; a < 3; a++) {
+                cb.r[a].min = std::min(cb.r[a].min, it.centroid[a]);
+                cb.r[a].max = std::max(cb.r[a].max, it.centroid[a]);
+            }
+        }
+        node.box = bb;
+        const float parent_area = std::max(half_area(bb), 1e-30f);
+        float best_cost = INFINITY;
+        int best_axis = -1, last_axis = -1;
+        uint32_t best_mid = 0;
+        if (cnt > 1) {
+            for (int axis = 0; axis < 3; axis++) {
+                if (!(cb.r[axis].max > cb.r[axis].min)) continue;
+                last_axis = axis;
+                const uint32_t *o = ord[axis].data() + s0;
+                hm::Box acc = items[o[cnt - 1]].box;
+                right_area[cnt - 1] = half_area(acc);
+                for (int64_t i = (int64_t)cnt - 2; i >= 1; i--) {
+                    acc = hm::Box::merge(acc, items[o[i]].box);
+                    right_area[i] = half_area(acc);
+                }
+                acc = items[o[0]].box;
+                for (uint32_t i = 1; i < cnt; i++) {
+                    const float c = c_trav + (half_area(acc) * i + right_area[i] * (cnt - i)) * c_isect / parent_area;
+                    if (c < best_cost) { best_cost = c; best_axis = axis; best_mid = i; }
+                    acc = hm::Box::merge(acc, items[o[i]].box);
+                }
+            }
+        }
+        const float leaf_cost = c_isect * cnt;
+        if (cnt <= leaf_cap && (best_axis < 0 || leaf_cost <= best_cost)) {
+            // the nodewise builder's item order here: its last axis sort, else the incoming order
+            const uint32_t *o = last_axis >= 0 ? ord[last_axis].data() + s0 : cur.data() + s0;
+            node.count = cnt;
+            node.index = (uint32_t)t.refs.size();
+            for (uint32_t i = 0; i < cnt; i++) t.refs.push_back(items[o[i]].index);
+            continue;
+        }
+        // the split order: the best axis's; without a split plane (all centroids equal) the order in
+        // place, cut in half
+        const uint32_t mid = best_axis >= 0 ? best_mid : cnt / 2;
+        const int split_axis = best_axis >= 0 ? best_axis : last_axis;
+        uint32_t *split = split_axis >= 0 ? ord[split_axis].data() + s0 : cur.data() + s0;
+        for (uint32_t i = 0; i < cnt; i++) left_side[split[i]] = i < mid ? 1 : 0;
+        if (split_axis >= 0) std::copy(split, split + cnt, cur.begin() + s0);  // children's incoming order
+        for (int a = 0; a < 3; a++) {                 // stable split of the other sorted lists
+            if (a == split_axis) continue;
+            uint32_t *o = ord[a].data() + s0;
+            uint32_t l = 0, r = mid;
+            for (uint32_t i = 0; i < cnt; i++) tmp[left_side[o[i]] ? l++ : r++] = o[i];
+            std::copy(tmp.begin(), tmp.begin() + cnt, o);
+        }
+        const uint32_t left = node_count++, right = node_count++;
+        (void)right;
+        node.count = 0;
+        node.index = left;
+        stack.push_back({s0 + mid, cnt - mid, left + 1});
+        stack.push_back({s0, mid, left});
     }
     t.nodes.resize(node_count);
     return t;

@@ -168,6 +168,7 @@ struct SceneGPU {
                                     // is the record index; tlas_slots maps it back to the instance id)
     uint32_t instance_count;
     uint32_t rough_count;           // material slot of metal m = rough_count + m
+    uint32_t material_count;        // slots in `materials` (roughs + metals)
 };
 
 struct CameraGPU {                  // Camera (RendererImpl.cuh:32-61), precomputed on host
@@ -185,6 +186,21 @@ struct CameraGPU {                  // Camera (RendererImpl.cuh:32-61), precompu
     uint64_t frame_seed;
 };
 
+// n / d by multiply-shift, exact for every n < 2^27 (round-up method: with l = ceil(log2 d),
+// s = 27 + l and m = ceil(2^s / d), the error m d - 2^s < d <= 2^l keeps n (m d - 2^s) < 2^s).
+// Work-item indices stay below 2^27 (rt_render checks units * 64); m < 2^28 + 1 fits 32 bits.
+constexpr uint32_t FASTDIV_BITS = 27;
+struct FastDiv {
+    uint32_t d, m, s;
+    __host__ __device__ uint32_t div(uint32_t n) const { return (uint32_t)(((uint64_t)n * m) >> s); }
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+    uint32_t l = 0;
+    while (l < 31 && (1u << l) < d) l++;
+    const uint32_t s = FASTDIV_BITS + l;
+    return FastDiv{d, (uint32_t)(((1ull << s) + d - 1) / d), s};
+}
+
 struct OutputGPU {
     uint8_t *rgba;                  // uchar4 per pixel
     float *rgb;                     // optional
@@ -192,6 +208,8 @@ struct OutputGPU {
     uint32_t units_x;               // frame layout: units per row
     // tile layout (tile_count > 0)
     uint32_t tile_w, tile_h, tile_rank, tile_count, tiles_x;
+    // the work-item -> pixel map's divisors: units_x (frame), units per tile, units per tile row, tiles_x
+    FastDiv div_units_x, div_upt, div_upr, div_tiles_x;
     // persistent kernel: work queue split into `queue_parts` bands of units (one per XCD), each with
     // its own head counter QUEUE_STRIDE words apart; optional per-wave timeline (debug)
     uint32_t queue_parts;

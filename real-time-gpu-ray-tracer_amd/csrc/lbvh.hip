@@ -726,22 +726,26 @@ namespace rtamd {
 namespace lbvh {
 // Per-frame: copy each instance's BLAS root {box, ref} into its hot record (the host staging block
 // carries the matrices; the roots of GPU-built BLASes live only in HBM).
-__global__ void patch_roots_kernel(InstHot *hot, const uint32_t *inst_blas, const TreeRoot *roots, uint32_t n) {
+// wide_refs: null for GPU-built BLASes (the quad root of a GPU-built tree has the pair root's ref,
+// collapse_wide_kernel); host-built BLASes under the GPU TLAS pass their quad roots
+__global__ void patch_roots_kernel(InstHot *hot, const uint32_t *inst_blas, const TreeRoot *roots, const uint32_t *wide_refs,
+                                   uint32_t n) {
     const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
     if (i >= n) return;
-    const TreeRoot R = roots[inst_blas[i]];
+    const uint32_t b = inst_blas[i];
+    const TreeRoot R = roots[b];
 #pragma unroll
     for (int k = 0; k < 6; k++) hot[i].root_box[k] = R.box[k];
     hot[i].root_ref = R.ref;
-    hot[i].root_ref_wide = R.ref;       // the quad root of a GPU-built tree has the pair root's ref (collapse_wide_kernel)
+    hot[i].root_ref_wide = wide_refs ? wide_refs[b] : R.ref;
 }
 }  // namespace lbvh
 
-hipError_t launch_patch_inst_roots(InstHot *hot, const uint32_t *inst_blas, const TreeRoot *roots, uint32_t n,
-                                   hipStream_t stream) {
+hipError_t launch_patch_inst_roots(InstHot *hot, const uint32_t *inst_blas, const TreeRoot *roots, const uint32_t *wide_refs,
+                                   uint32_t n, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(lbvh::patch_roots_kernel, dim3(lbvh::blocks_for(n)), dim3(lbvh::BLOCK), 0, stream, hot, inst_blas,
-                       roots, n);
+                       roots, wide_refs, n);
     return hipGetLastError();
 }
 }  // namespace rtamd

@@ -35,11 +35,11 @@ hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, c
                                           uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
-hipError_t launch_frame_copy(void *, const void *, size_t, unsigned long long *, hipStream_t);
+hipError_t launch_frame_copy(void *, const void *, size_t, unsigned long long *, uint32_t *, hipStream_t);
 hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t,
                            uint32_t, void *, const void *, size_t, unsigned long long *, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean, bool wide);
-hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, uint32_t, hipStream_t);
+hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t launch_instance_update(const InstDelta *, uint32_t, InstParams *, uint32_t, InstHot *, InstCold *, float *, float4 *,
                                   hipStream_t);
 uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean, bool wide);
@@ -198,6 +198,7 @@ struct rt_scene {
     uint32_t cus = 0;
     uint32_t threshold = 32;          // measured with "reorder" + "wide" + 2 overlap lanes: 32-48 beat 16
     uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4, 5)
+    double update_wait_ms = 0.0;    // last frame_update: time blocked on ev_copied (GPU progress)
     bool use_persistent = true;
     uint32_t queue_parts = 8;       // one band per XCD (measured with "reorder": 8 beat 4, 2 and 1 on C2)
     uint32_t nt_store = 0;
@@ -209,9 +210,16 @@ struct rt_scene {
     bool costmap_on = false;
     // option "reorder" (schedule.hip): longest-first claim order from the previous launch's unit costs
     bool reorder = true;
-    uint32_t split = 10u | 12u << 8;  // heavy-unit pieces: class level for halves | quarters << 8 (0xFF = never)
+    // heavy-unit pieces: class level for halves | quarters << 8 (0xFF = never); measured (C2 / C3 / C4
+    // shares, profiles/r02_sweep_period*.jsonl): quarters from level 12 and no halves
+    uint32_t split = 12u | 12u << 8;
     DevBuf<uint32_t> unit_cost[NLANE], unit_order[NLANE];
     uint32_t sched_sig[NLANE][7] = {};  // launch layout the recorded costs belong to
+    // option "reorder_period" K: a lane records unit costs on one launch in K and rebuilds its order on
+    // the next; the launches between reuse the order (the heaviest regions move little between frames)
+    uint32_t reorder_period = 8;        // measured: 8 (C2 0.242 ms/step) beats 1 (0.265) with 3 lanes
+    uint32_t sched_phase[NLANE] = {};
+    bool order_ok[NLANE] = {};
     bool sched_valid[NLANE] = {};
     DevBuf<uint32_t> costmap;
     size_t costmap_pixels = 0;
@@ -248,7 +256,10 @@ struct rt_scene {
     bool blas_dirty = false;            // rt_scene_update_triangles since the last BLAS build
     uint64_t blas_builds = 0;
     hipEvent_t ev_render_done = nullptr;   // last trace launch finished (BLAS rebuilds wait on it)
-    bool gpu_tlas() const { return build_mode == RT_BUILD_LBVH; }
+    bool gpu_tlas_sah = false;          // option "gpu_tlas" (set before the build): RT_BUILD_SAH BLASes, per-frame TLAS on the GPU
+    DevBuf<uint32_t> blas_wide_refs;    // host-built BLASes under a GPU TLAS: quad root ref per BLAS
+    // instance records + TLAS built by kernels each frame: RT_BUILD_LBVH, or RT_BUILD_SAH with "gpu_tlas"
+    bool gpu_tlas() const { return build_mode == RT_BUILD_LBVH || (gpu_tlas_sah && build_mode == RT_BUILD_SAH); }
 
     CommState *comm = nullptr;             // multi-GPU frame (rt_scene_attach_comm)
     void release_comm() {
@@ -275,6 +286,7 @@ struct rt_scene {
         for (int q = 0; q < NLANE; q++) { unit_cost[q].release(); unit_order[q].release(); }
         delete blas_builder; delete tlas_builder;
         raw_tris.release(); raw_sph.release(); raw_quad.release(); blas_roots.release(); inst_blas.release();
+        blas_wide_refs.release();
         gpu_counts.release(); inst_params.release();
         if (ev_render_done) (void)hipEventDestroy(ev_render_done);
         for (int b = 0; b < NLANE; b++) {
@@ -370,7 +382,9 @@ hipError_t drain(rt_scene *s) {
 // defer (rt_render): the copy itself is left to the next launch on `upload` (pending_copy).
 rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool defer = false) {
     const int b = s->active < 0 ? 0 : (s->active + 1) % rt_scene::NLANE;
+    const auto w0 = std::chrono::steady_clock::now();
     HIP_TRY(hipEventSynchronize(s->ev_copied[b]));     // staging[b] no longer read by a pending copy
+    s->update_wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     if (s->update) {                                  // Renderer.cu:269
         std::vector<rt_xform> xs(s->inst.size());
         for (size_t i = 0; i < xs.size(); i++) xs[i] = s->inst[i].x;
@@ -411,19 +425,20 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         uint8_t *fd = s->frame_dev[b];
         HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_used[b], 0));
         // a blit kernel reading the pinned staging block, not an SDMA copy (see the host-built path below)
-        if (nd) HIP_TRY(launch_frame_copy(fd + s->off_delta, s->staging_dev[b] + s->off_delta, nd * sizeof(InstDelta), nullptr,
+        if (nd) HIP_TRY(launch_frame_copy(fd + s->off_delta, s->staging_dev[b] + s->off_delta, nd * sizeof(InstDelta), nullptr, nullptr,
                                           s->stream));
         // Instance::updateTransformArguments for every instance, on the GPU (instances.hip)
         HIP_TRY(launch_instance_update(reinterpret_cast<const InstDelta *>(fd + s->off_delta), nd, s->inst_params.p,
                                        (uint32_t)s->inst.size(), reinterpret_cast<InstHot *>(fd + s->off_hot),
                                        reinterpret_cast<InstCold *>(fd + s->off_cold), reinterpret_cast<float *>(fd + s->off_tbox),
                                        reinterpret_cast<float4 *>(fd + s->off_tcent), s->stream));
-        if (s->rebuild_blas || s->blas_dirty) {
+        if (s->blas_builder && (s->rebuild_blas || s->blas_dirty)) {    // GPU-built BLASes only
             const rt_status bs = gpu_build_blas(s);
             if (bs != RT_OK) return bs;
         }
         const uint32_t n = (uint32_t)s->inst.size();
-        HIP_TRY(launch_patch_inst_roots(reinterpret_cast<InstHot *>(fd + s->off_hot), s->inst_blas.p, s->blas_roots.p, n,
+        HIP_TRY(launch_patch_inst_roots(reinterpret_cast<InstHot *>(fd + s->off_hot), s->inst_blas.p, s->blas_roots.p,
+                                        s->blas_wide_refs.p, n,
                                         s->stream));
         HIP_TRY(s->tlas_builder->set_items(reinterpret_cast<const float *>(fd + s->off_tbox),
                                            reinterpret_cast<const float4 *>(fd + s->off_tcent)));
@@ -506,6 +521,7 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.materials = s->materials.p;
     g.instance_count = (uint32_t)s->inst.size();
     g.rough_count = (uint32_t)s->roughs.size();
+    g.material_count = (uint32_t)(s->materials.n / 4);
     return g;
 }
 
@@ -819,8 +835,24 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     s->off_root_wide = 32;                                         // second half of the root's 64 B
     s->off_quads = (s->off_tcent + n * 4 * sizeof(float) + 127) & ~size_t(127);
     s->off_delta = align16(s->off_quads + n * sizeof(NodeQuad));   // <= n - 1 quads
-    s->frame_block = s->off_delta + (mode == RT_BUILD_LBVH ? n * sizeof(InstDelta) : 0);
-    if (mode == RT_BUILD_LBVH) {
+    s->frame_block = s->off_delta + (s->gpu_tlas() ? n * sizeof(InstDelta) : 0);
+    if (s->gpu_tlas() && mode == RT_BUILD_SAH) {
+        // host-built BLASes under the GPU TLAS: their roots (box, pair ref, quad ref) and the instance map
+        std::vector<TreeRoot> roots(s->blas.size());
+        std::vector<uint32_t> wide_refs(s->blas.size()), ib(n);
+        for (size_t b = 0; b < s->blas.size(); b++) {
+            std::memcpy(roots[b].box, s->blas[b].flat.root_box, sizeof roots[b].box);
+            roots[b].ref = s->blas[b].flat.root_ref;
+            roots[b].height = s->blas[b].flat.height;
+            wide_refs[b] = s->blas[b].wide.root_ref;
+        }
+        for (size_t i = 0; i < n; i++) ib[i] = s->inst[i].blas;
+        if ((st = upload(s->blas_roots, roots)) != RT_OK) return st;
+        if ((st = upload(s->blas_wide_refs, wide_refs)) != RT_OK) return st;
+        if ((st = upload(s->inst_blas, ib)) != RT_OK) return st;
+        if ((st = alloc_buf(s->gpu_counts, 2)) != RT_OK) return st;
+    }
+    if (s->gpu_tlas()) {
         if ((st = alloc_buf(s->inst_params, n)) != RT_OK) return st;
         s->inst_dirty.assign(n, 1);                                 // frame 0 uploads every instance
         delete s->tlas_builder;
@@ -1030,7 +1062,16 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         out.tiles_x = (W + o.tile_w - 1) / o.tile_w;
         out.units = mine * (o.tile_w / 8) * (o.tile_h / 8);
         npix = (size_t)mine * o.tile_w * o.tile_h;
+        const uint32_t upr = o.tile_w / 8;
+        out.div_upr = make_fastdiv(upr);
+        out.div_upt = make_fastdiv(upr * (o.tile_h / 8));
+        out.div_tiles_x = make_fastdiv(out.tiles_x);
+        if ((uint64_t)out.tiles_x * ((H + o.tile_h - 1) / o.tile_h) >= (1ull << FASTDIV_BITS))
+            return fail(RT_ERR_INVALID_ARGUMENT, "too many tiles");
     }
+    if ((uint64_t)out.units * 64u >= (1ull << FASTDIV_BITS))       // work items index pixels of whole units
+        return fail(RT_ERR_INVALID_ARGUMENT, "frame too large: more than 2^27 pixels per launch");
+    out.div_units_x = make_fastdiv(out.units_x ? out.units_x : 1u);
     // outputs: caller device buffers, else scene-owned; a rank of a multi-GPU frame traces into its lane's slab
     uint8_t *frame_out = nullptr;              // multi-GPU, rank 0: the assembled frame
     if (cm) {
@@ -1139,29 +1180,47 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         const uint32_t sig[7] = {out.units, out.units_x, out.tile_w, out.tile_h, out.tile_rank, out.tile_count,
                                  out.queue_parts};
         // the costs the lane's previous launch recorded are for the layout it had
-        const bool do_order = s->sched_valid[q] && std::memcmp(sig, s->sched_sig[q], sizeof sig) == 0;
-        const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
-        const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
-        const int pc = s->pending_copy;
-        HIP_TRY(launch_schedule(unit_cost.p, unit_cost.p + out.units, unit_order.p, s->queue[q], rows, upr, out.queue_parts,
-                                do_order, s->split & 0xFFu, (s->split >> 8) & 0xFFu, pc >= 0 ? s->frame_dev[pc] : nullptr,
-                                pc >= 0 ? s->staging_dev[pc] : nullptr, pc >= 0 ? s->frame_block : 0,
-                                zero_lane ? lane_counters : nullptr, stream));
-        zero_lane = false;
-        if (pc >= 0) HIP_TRY(hipEventRecord(s->ev_copied[pc], stream));
-        s->pending_copy = -1;
+        const bool layout_ok = s->sched_valid[q] && std::memcmp(sig, s->sched_sig[q], sizeof sig) == 0;
+        const uint32_t K = s->reorder_period;
+        uint32_t &ph = s->sched_phase[q];
+        // phase 0 records costs, phase 1 orders from them; K = 1: both on every launch.  A new layout
+        // starts over: the schedule kernel clears the costs and this launch records in screen order.
+        bool run_sched, track;
+        if (!layout_ok) {
+            run_sched = true; track = true; s->order_ok[q] = false; ph = K == 1 ? 0u : 1u;
+        } else if (K == 1) {
+            run_sched = true; track = true;
+        } else {
+            run_sched = ph == 1; track = ph == 0; ph = (ph + 1) % K;
+        }
+        const bool do_order = layout_ok && run_sched;
+        if (run_sched) {
+            const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
+            const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
+            const int pc = s->pending_copy;
+            HIP_TRY(launch_schedule(unit_cost.p, unit_cost.p + out.units, unit_order.p, s->queue[q], rows, upr, out.queue_parts,
+                                    do_order, s->split & 0xFFu, (s->split >> 8) & 0xFFu, pc >= 0 ? s->frame_dev[pc] : nullptr,
+                                    pc >= 0 ? s->staging_dev[pc] : nullptr, pc >= 0 ? s->frame_block : 0,
+                                    zero_lane ? lane_counters : nullptr, stream));
+            zero_lane = false;
+            if (pc >= 0) HIP_TRY(hipEventRecord(s->ev_copied[pc], stream));
+            s->pending_copy = -1;
+            if (do_order) s->order_ok[q] = true;
+            reset_queue = false;
+        }
         std::memcpy(s->sched_sig[q], sig, sizeof sig);
         s->sched_valid[q] = true;
-        out.order = do_order ? unit_order.p : nullptr;
-        out.unit_cost = unit_cost.p;
-        reset_queue = false;
+        out.order = s->order_ok[q] ? unit_order.p : nullptr;
+        out.unit_cost = track ? unit_cost.p : nullptr;
     }
-    if (s->pending_copy >= 0) {                // the frame block's upload (and the lane's counter reset)
+    if (s->pending_copy >= 0) {                // the frame block's upload (and the lane's counter / queue reset)
         HIP_TRY(launch_frame_copy(s->frame_dev[s->pending_copy], s->staging_dev[s->pending_copy], s->frame_block,
-                                  zero_lane ? lane_counters : nullptr, stream));
+                                  zero_lane ? lane_counters : nullptr, reset_queue && s->use_persistent ? s->queue[q] : nullptr,
+                                  stream));
         HIP_TRY(hipEventRecord(s->ev_copied[s->pending_copy], stream));
         s->pending_copy = -1;
         zero_lane = false;
+        reset_queue = false;
     }
     HIP_TRY(hipStreamWaitEvent(stream, s->ev_copied[s->active], 0));
     if (zero_lane) HIP_TRY(hipMemsetAsync(lane_counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
@@ -1208,7 +1267,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     HIP_TRY(hipEventRecord(s->ev_render_done, stream));
     HIP_TRY(hipEventRecord(s->ev_lane_done[q], stream));
     if (o.flags & RT_RENDER_NO_SYNC) {
-        if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; }
+        if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; stats->update_wait_ms = s->update_wait_ms; }
         return RT_OK;
     }
     HIP_TRY(hipMemcpyAsync(s->counters_host, lane_counters, CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
@@ -1223,6 +1282,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         fill_stats(stats, s->counters_host);
         stats->kernel_ms = kms;
         stats->update_ms = update_ms;
+        stats->update_wait_ms = s->update_wait_ms;
         stats->frame_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     if (count && s->counters_host[CNT_OVERFLOW] != 0)
@@ -1309,6 +1369,10 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "wide") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "wide must be 0 or 1");
         s->wide = value == 1;
+    } else if (k == "gpu_tlas") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "gpu_tlas must be 0 or 1");
+        if (s->built) return fail(RT_ERR_UNSUPPORTED, "gpu_tlas is set before rt_scene_build");
+        s->gpu_tlas_sah = value == 1;
     } else if (k == "wide_merge") {
         if (value != 0 && (value < 2 || value > 4)) return fail(RT_ERR_INVALID_ARGUMENT, "wide_merge must be 0 or 2..4");
         s->wide_merge = (uint32_t)value;          // BLAS quads: next rt_scene_build; TLAS: next frame
@@ -1334,6 +1398,10 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "reserve") {
         if (value < 0 || value > 256) return fail(RT_ERR_INVALID_ARGUMENT, "reserve must be in 0..256");
         s->reserve = (uint32_t)value;
+    } else if (k == "reorder_period") {
+        if (value < 1 || value > 1024) return fail(RT_ERR_INVALID_ARGUMENT, "reorder_period must be in 1..1024");
+        s->reorder_period = (uint32_t)value;
+        for (uint32_t &p : s->sched_phase) p = 0;
     } else if (k == "reorder") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "reorder must be 0 or 1");
         if (s->reorder != (value == 1)) for (bool &v : s->sched_valid) v = false;

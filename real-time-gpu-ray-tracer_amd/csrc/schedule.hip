@@ -189,18 +189,21 @@ hipError_t launch_schedule(uint32_t *cost, uint32_t *cost_prev, uint32_t *order,
 // between two traces on one stream, cost ~35 us of idle GPU per frame (rocprofv3 trace, round 1).  8 VGPRs:
 // it fits beside a full persistent grid.
 __global__ __launch_bounds__(256) void frame_copy_kernel(uint4 *__restrict__ dst, const uint4 *__restrict__ src, uint32_t n16,
-                                                         unsigned long long *zero_counters) {
+                                                         unsigned long long *zero_counters, uint32_t *zero_queue) {
     if (zero_counters && blockIdx.x == 0 && threadIdx.x < CNT_NUM) zero_counters[threadIdx.x] = 0ull;
+    if (zero_queue && blockIdx.x == 0 && threadIdx.x < QUEUE_MAX_PARTS) zero_queue[threadIdx.x * QUEUE_STRIDE] = 0u;
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n16; i += gridDim.x * 256u) dst[i] = src[i];
 }
 
-hipError_t launch_frame_copy(void *dst, const void *src, size_t bytes, unsigned long long *zero_counters, hipStream_t stream) {
+// zero_queue (optional): the persistent launch's queue heads, reset here instead of by a fill kernel
+hipError_t launch_frame_copy(void *dst, const void *src, size_t bytes, unsigned long long *zero_counters, uint32_t *zero_queue,
+                             hipStream_t stream) {
     if (bytes % 16) return hipErrorInvalidValue;
     const uint32_t n16 = (uint32_t)(bytes / 16);
-    if (n16 == 0 && !zero_counters) return hipSuccess;
+    if (n16 == 0 && !zero_counters && !zero_queue) return hipSuccess;
     const uint32_t blocks = n16 / 256u + 1u < 64u ? n16 / 256u + 1u : 64u;
     hipLaunchKernelGGL(frame_copy_kernel, dim3(blocks), dim3(256), 0, stream, static_cast<uint4 *>(dst),
-                       static_cast<const uint4 *>(src), n16, zero_counters);
+                       static_cast<const uint4 *>(src), n16, zero_counters, zero_queue);
     return hipGetLastError();
 }
 

@@ -44,7 +44,11 @@ constexpr float FZERO = 1e-6f;          // FLOAT_ZERO_VALUE (Global.cuh:147)
 constexpr float TMIN = 0.001f;          // Kernel.cu:66
 constexpr int BLOCK = 256;              // 4 waves; each wave owns one 8x8 pixel unit
 constexpr int LDS_DEPTH = 16;           // per-lane stack entries kept in LDS
+constexpr int LDS_MATERIALS = 256;      // persistent kernel: material table in LDS up to this many slots (4 KB)
 constexpr int SPILL_DEPTH = 48;         // overflow entries in scratch (max depth 64 = reference)
+#ifndef RT_LEAN_WIDE
+#define RT_LEAN_WIDE 0                  // 1: quad trees take the lean one-pop-per-step loop (lw_*; measured slower)
+#endif
 #ifndef TRI_AHEAD
 #define TRI_AHEAD 2                     // triangle records of a leaf requested before the first test
 #endif
@@ -361,15 +365,14 @@ struct Trav {
     Stack stk;
 };
 
-template <bool WIDE = false>
-__device__ __forceinline__ void trav_init(Trav &T, const SceneGPU &sc, const f3 &o, const f3 &d) {
+// R: this frame's TLAS root (the persistent kernel holds it in SGPRs, loaded once per wave)
+__device__ __forceinline__ void trav_init(Trav &T, const TreeRoot &R, const f3 &o, const f3 &d) {
     T.wr.o = o; T.wr.d = d; prep(T.wr);
     T.lr = T.wr;
     T.tmax = __builtin_huge_valf();
     T.found = false;
     T.stk.sp = 0;
     T.stk.spilled = 0;
-    const TreeRoot &R = WIDE ? *sc.tlas_root_wide : *sc.tlas_root;      // this frame's TLAS root (HBM)
     T.cur = R.ref;
     T.cur_inst = 0;
     T.in_blas = false;
@@ -377,6 +380,23 @@ __device__ __forceinline__ void trav_init(Trav &T, const SceneGPU &sc, const f3 
     float te = 0.0f;
     T.tracing = slab(R.box, T.wr, TMIN, T.tmax, te);                     // root pop test (TLAS.cu:150)
     T.curT = te;
+}
+__device__ __forceinline__ void trav_init(Trav &T, const SceneGPU &sc, const f3 &o, const f3 &d) {
+    trav_init(T, *sc.tlas_root, o, d);
+}
+
+// The frame's TLAS root as wave-uniform values (SGPRs): read once per wave instead of per ray.
+template <bool WIDE>
+__device__ __forceinline__ TreeRoot uniform_root(const SceneGPU &sc) {
+    const float4 *p = reinterpret_cast<const float4 *>(WIDE ? sc.tlas_root_wide : sc.tlas_root);
+    const float4 a = p[0], b = p[1];
+    auto u = [](float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); };
+    TreeRoot R;
+    R.box[0] = u(a.x); R.box[1] = u(a.y); R.box[2] = u(a.z); R.box[3] = u(a.w);
+    R.box[4] = u(b.x); R.box[5] = u(b.y);
+    R.ref = (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(b.z));
+    R.height = 0;
+    return R;
 }
 
 // Process T.cur (one node pair, one TLAS leaf instance or one BLAS leaf), then choose the next node:
@@ -656,16 +676,18 @@ __device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEn
 #define RT_DIAG 0
 #endif
 // Diagnostic builds (make diag -> librtamd_diag.so): wave-uniform cycle stamps per phase.
-struct PhaseCycles { unsigned long long refill, interior, leaf, shade, iters, refill_iters; };
+struct PhaseCycles { unsigned long long refill, interior, leaf, shade, iters, refill_iters, claim, hit; };
 __device__ __forceinline__ unsigned long long stamp() {
     unsigned long long t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
     return t;
 }
 #if RT_DIAG
+#define DIAG_WAIT_VM() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
 #define DIAG_T(var) const unsigned long long var = stamp()
 #define DIAG_ADD(acc, t0) (acc) += stamp() - (t0)
 #else
+#define DIAG_WAIT_VM() (void)0
 #define DIAG_T(var) (void)0
 #define DIAG_ADD(acc, t0) (void)0
 #endif
@@ -845,6 +867,209 @@ __device__ __forceinline__ void lean_round(Trav &T, const SceneGPU &sc, LaneCoun
     DIAG_T(t1);
     if (T.tracing) {
         lean_leaf_phase<COUNT>(T, sc, cnt);
+        if (track) steps++;
+    }
+    DIAG_ADD(pc.leaf, t1);
+}
+
+// ---- lean quad traversal (FAST kernel, option "wide") ---------------------------------------
+// The quad-tree form of the lean loop: one straight-line step per iteration, built for the cost
+// model of a 64-wide wave where every divergent branch costs exec-mask bookkeeping for all lanes:
+//   * one active ray (lr: the world ray in the TLAS, the instance ray inside a BLAS).  The world ray
+//     keeps only o, d (T.wr.o / T.wr.d); crossing back into the TLAS re-derives its reciprocals
+//     (prep is deterministic, so the slabs see the same values as at trav_init);
+//   * a step pops at most one entry (cur = REF_POP marks "pop at the start of the next step") and
+//     then tests the popped node in the same step;
+//   * a quad's 1..3 far hits are written to the three LDS slots above the top without branching on
+//     their count (the slots above the top are free), and sp advances by nh - 1;
+//   * the LDS window pages its bottom half to scratch only when fewer than 3 slots are free (a
+//     uniform branch no lane takes on shallow trees), so deep trees keep the reference's capacity.
+// Leaves are processed in the same speculative while-while order as spec_* (same closest hit).
+__device__ __forceinline__ void lw_page_out(Stack &stk, SEnt *spill, LaneCount &c) {   // sp > HALF
+    if (stk.spilled + HALF > SPILL_DEPTH) {
+        c.overflow++;
+        stk.spilled = SPILL_DEPTH - HALF;
+    }
+#pragma unroll
+    for (int k = 0; k < HALF; k++) spill[stk.spilled + k] = unpack(stk.lds[k * BLOCK]);
+#pragma unroll
+    for (int k = 0; k < HALF; k++) stk.lds[k * BLOCK] = stk.lds[(k + HALF) * BLOCK];   // slots >= sp: don't care
+    stk.sp -= HALF;
+    stk.spilled += HALF;
+}
+
+__device__ __forceinline__ void lw_to_world(Trav &T) {        // back in the TLAS: the world ray is active
+    T.lr.o = T.wr.o;
+    T.lr.d = T.wr.d;
+    prep(T.lr);
+    T.in_blas = false;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void lw_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
+    uint32_t cur = T.cur;
+    float curT = T.curT;
+    if (cur == REF_POP) {                                   // pop one entry, re-test it (BLAS.cu:145)
+        if (T.stk.sp == 0 && T.stk.spilled > 0) stack_page_in(T.stk, spill);
+        if (T.stk.sp > 0) {
+            T.stk.sp--;
+            const SEnt e = unpack(T.stk.lds[T.stk.sp * BLOCK]);
+            curT = __uint_as_float(e.tn);
+            cur = curT < T.tmax ? e.ref : REF_POP;
+        } else {
+            cur = REF_NONE;
+        }
+    }
+    const bool blocked = T.pleaf != REF_NONE && T.in_blas && !ref_is_marker(cur) && !(cur & REF_BLAS);
+    if (!ref_is_marker(cur) && !blocked) {
+        if (T.in_blas && !(cur & REF_BLAS)) lw_to_world(T);
+        if (cur & REF_LEAF) {
+            if (T.pleaf == REF_NONE) { T.pleaf = cur; cur = REF_POP; }            // postpone, keep walking
+        } else {
+            const bool blas = (cur & REF_BLAS) != 0;
+            const float4 *Q = reinterpret_cast<const float4 *>((blas ? sc.blas_quads : sc.tlas_quads) + (cur & REF_INDEX_MASK));
+            const float4 lx = Q[0], hx = Q[1], ly = Q[2], hy = Q[3], lz = Q[4], hz = Q[5];
+            const uint4 R = reinterpret_cast<const uint4 *>(Q)[6];
+            if (COUNT) cnt.pairs += 2;
+            const RayP &r = T.lr;
+            float t[4];
+            bool h[4];
+            if (!r.tiny) {
+                float4 tn = make_float4(TMIN, TMIN, TMIN, TMIN), tf = make_float4(T.tmax, T.tmax, T.tmax, T.tmax);
+                slab4(lx, hx, r.inv.x, r.oinv.x, tn, tf);
+                slab4(ly, hy, r.inv.y, r.oinv.y, tn, tf);
+                slab4(lz, hz, r.inv.z, r.oinv.z, tn, tf);
+                t[0] = tn.x; t[1] = tn.y; t[2] = tn.z; t[3] = tn.w;
+                h[0] = tn.x < tf.x; h[1] = tn.y < tf.y; h[2] = tn.z < tf.z; h[3] = tn.w < tf.w;
+            } else {
+                const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+                const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
+                const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const float b[6] = {LX[k], HX[k], LY[k], HY[k], LZ[k], HZ[k]};
+                    t[k] = 0.0f;
+                    h[k] = slab_ref(b, r.o, r.d, TMIN, T.tmax, t[k]);
+                }
+            }
+            float t0 = h[0] ? t[0] : __builtin_huge_valf(), t1 = h[1] ? t[1] : __builtin_huge_valf();
+            float t2 = h[2] ? t[2] : __builtin_huge_valf(), t3 = h[3] ? t[3] : __builtin_huge_valf();
+            uint32_t r0 = R.x, r1 = R.y, r2 = R.z, r3 = R.w;
+            const uint32_t nh = (uint32_t)h[0] + (uint32_t)h[1] + (uint32_t)h[2] + (uint32_t)h[3];
+            cswap(t0, r0, t1, r1); cswap(t2, r2, t3, r3); cswap(t0, r0, t2, r2); cswap(t1, r1, t3, r3); cswap(t1, r1, t2, r2);
+            if (nh > 1) {
+                if (T.stk.sp > LDS_DEPTH - 3) lw_page_out(T.stk, spill, cnt);
+                // farthest first: slot sp + j holds hit nh-1-j (j <= nh-2); the other slots are free space
+                SEnt a, b, c;
+                a.ref = nh == 4 ? r3 : (nh == 3 ? r2 : r1);
+                a.tn = __float_as_uint(nh == 4 ? t3 : (nh == 3 ? t2 : t1));
+                b.ref = nh == 4 ? r2 : r1;
+                b.tn = __float_as_uint(nh == 4 ? t2 : t1);
+                c.ref = r1;
+                c.tn = __float_as_uint(t1);
+                T.stk.lds[T.stk.sp * BLOCK] = pack(a);
+                T.stk.lds[(T.stk.sp + 1) * BLOCK] = pack(b);
+                T.stk.lds[(T.stk.sp + 2) * BLOCK] = pack(c);
+                T.stk.sp += (int)nh - 1;
+            }
+            cur = nh ? r0 : REF_POP;
+            curT = t0;
+        }
+    }
+    T.cur = cur;
+    T.curT = curT;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void lw_leaf_phase(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
+    const uint32_t leaf = T.pleaf;
+    T.pleaf = REF_NONE;
+    if (!(leaf & REF_BLAS)) {
+        // TLAS leaf (the lane is in the TLAS): the successor and the leaf's remaining instances wait on
+        // the stack (popped in reference order), then the first instance's BLAS is entered
+        const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf);
+        if (!ref_is_marker(T.cur)) stack_push(T.stk, spill, T.cur, T.curT, cnt);
+        if (count > 1) stack_push(T.stk, spill, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
+        T.cur_inst = sc.inst_by_slot ? start : sc.tlas_slots[start];
+        const InstHot &I = sc.inst_hot[T.cur_inst];
+        if (COUNT) cnt.inst++;
+        T.lr.o = xf_point(I.inv, T.wr.o);                      // Instance.cu:26-27
+        T.lr.d = xf_vector(I.inv, T.wr.d);
+        prep(T.lr);
+        T.in_blas = true;
+        float te = 0.0f;
+        const bool h = slab(I.root_box, T.lr, TMIN, T.tmax, te);
+        T.cur = h ? I.root_ref_wide : REF_POP;
+        T.curT = te;
+    } else {
+        const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf), type = ref_leaf_type(leaf);
+        if (type == RT_PRIM_TRIANGLE) {
+            for (uint32_t k0 = 0; k0 < count; k0 += TRI_AHEAD) {
+                TriHot H[TRI_AHEAD];
+#pragma unroll
+                for (uint32_t k = 0; k < TRI_AHEAD; k++)
+                    if (k0 + k < count) {
+                        const float *src = sc.tri_hot[start + k0 + k].v0;
+                        const float3 a = *reinterpret_cast<const float3 *>(src);
+                        const float3 b = *reinterpret_cast<const float3 *>(src + 4);
+                        const float3 c = *reinterpret_cast<const float3 *>(src + 8);
+                        H[k].v0[0] = a.x; H[k].v0[1] = a.y; H[k].v0[2] = a.z;
+                        H[k].e1[0] = b.x; H[k].e1[1] = b.y; H[k].e1[2] = b.z;
+                        H[k].e2[0] = c.x; H[k].e2[1] = c.y; H[k].e2[2] = c.z;
+                    }
+#pragma unroll
+                for (uint32_t k = 0; k < TRI_AHEAD; k++) {
+                    if (k0 + k >= count) break;
+                    float t = 0.0f, u = 0.0f, v = 0.0f;
+                    if (COUNT) cnt.tri++;
+                    if (tri_test(H[k], T.lr, TMIN, T.tmax, t, u, v)) {
+                        T.found = true; T.tmax = t;
+                        T.hit.t = t; T.hit.inst = T.cur_inst; T.hit.ptype = type; T.hit.slot = start + k0 + k;
+                        T.hit.u = u; T.hit.v = v;
+                    }
+                }
+            }
+        } else {
+            for (uint32_t k = 0; k < count; k++) {
+                const uint32_t slot = start + k;
+                float t = 0.0f, u = 0.0f, v = 0.0f;
+                bool h;
+                if (type == RT_PRIM_SPHERE) {
+                    if (COUNT) cnt.sq++;
+                    h = sphere_test(sc.sph_hot[slot], T.lr, TMIN, T.tmax, t);
+                } else {
+                    if (COUNT) { cnt.sq++; cnt.quad++; }
+                    h = quad_test(sc.quad_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
+                }
+                if (h) {
+                    T.found = true; T.tmax = t;
+                    T.hit.t = t; T.hit.inst = T.cur_inst; T.hit.ptype = type; T.hit.slot = slot; T.hit.u = u; T.hit.v = v;
+                }
+            }
+        }
+        if (!ref_is_marker(T.cur) && !(T.curT < T.tmax)) T.cur = REF_POP;   // re-test the successor
+    }
+    if (T.cur == REF_POP && T.stk.empty()) T.cur = REF_NONE;
+    if (T.cur == REF_NONE) T.tracing = false;
+}
+
+template <bool COUNT>
+__device__ __forceinline__ void lw_round(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt, PhaseCycles &pc,
+                                         uint32_t &steps, bool track) {
+    DIAG_T(t0);
+    for (;;) {
+        if (T.tracing && T.pleaf == REF_NONE && T.cur == REF_NONE) T.tracing = false;   // done, no leaf left
+        if (!__any(T.tracing && T.pleaf == REF_NONE)) break;
+        if (lean_active(T)) {
+            lw_step<COUNT>(T, sc, spill, cnt);
+            if (track) steps++;
+        }
+        if (RT_DIAG) pc.iters++;
+    }
+    DIAG_ADD(pc.interior, t0);
+    DIAG_T(t1);
+    if (T.tracing) {
+        lw_leaf_phase<COUNT>(T, sc, spill, cnt);
         if (track) steps++;
     }
     DIAG_ADD(pc.leaf, t1);
@@ -1042,18 +1267,20 @@ __device__ __forceinline__ uint32_t hw_id() {
 
 __device__ __forceinline__ bool map_item(const OutputGPU &out, const CameraGPU &cam, uint32_t item,
                                          uint32_t &px, uint32_t &py, uint32_t &oi) {
+    // multiply-shift divisions (FastDiv, host-precomputed): this runs per refilled lane and per sample
     const uint32_t wunit = item >> 6, l = item & 63u;
     if (out.tile_count == 0) {
-        const uint32_t ux = wunit % out.units_x, uy = wunit / out.units_x;
+        const uint32_t uy = out.div_units_x.div(wunit), ux = wunit - uy * out.units_x;
         px = ux * 8 + (l & 7); py = uy * 8 + (l >> 3);
         oi = py * cam.width + px;
     } else {
-        const uint32_t upr = out.tile_w / 8, upt = upr * (out.tile_h / 8);
-        const uint32_t k = wunit / upt, r = wunit % upt;
+        const uint32_t k = out.div_upt.div(wunit), r = wunit - k * out.div_upt.d;
         const uint32_t t = out.tile_rank + k * out.tile_count;
-        const uint32_t lx = (r % upr) * 8 + (l & 7), ly = (r / upr) * 8 + (l >> 3);
-        px = (t % out.tiles_x) * out.tile_w + lx;
-        py = (t / out.tiles_x) * out.tile_h + ly;
+        const uint32_t ry = out.div_upr.div(r), rx = r - ry * out.div_upr.d;
+        const uint32_t lx = rx * 8 + (l & 7), ly = ry * 8 + (l >> 3);
+        const uint32_t ty = out.div_tiles_x.div(t), tx = t - ty * out.tiles_x;
+        px = tx * out.tile_w + lx;
+        py = ty * out.tile_h + ly;
         oi = k * out.tile_w * out.tile_h + ly * out.tile_w + lx;
     }
     return px < cam.width && py < cam.height;
@@ -1093,9 +1320,22 @@ __device__ __forceinline__ void write_pixel(const OutputGPU &out, uint32_t oi, f
 // work of its 64 pixels (interior steps + leaf phases + 1 per pixel).  A wave's lanes refill from
 // the unit it claimed, so a unit's total work is the time it holds a wave; units over the particle
 // cluster hold one for up to ~0.4 ms against ~20 us for a sky unit (C2, measured), and the launch
-// ends with whichever wave claimed the last heavy units.  Lanes that finished a pixel in this shade
-// step: one atomicAdd per distinct unit.
+// ends with whichever wave claimed the last heavy units.
+// RT_UNIT_COST_DEFER (default): a lane keeps one pending (unit, cost) sum and flushes it with a
+// no-return atomic just before the wave's next claim atomic, whose returned value the wave waits for
+// anyway, so the flush adds no wait of its own (vector memory counters retire in order: a returning
+// atomic's wait also covers the stores and atomics issued before it).  A lane that finishes a pixel of
+// another unit before that flushes its old sum at once.  Measured: per-shade-step atomics (below,
+// RT_UNIT_COST_DEFER=0) made each next node load wait for their memory-side completion (~11 % of C2
+// throughput, profiles/r02_ab_unit_cost.jsonl).
+#ifndef RT_UNIT_COST_DEFER
+#define RT_UNIT_COST_DEFER 1
+#endif
+// Lanes that finished a pixel in this shade step: one atomicAdd per distinct unit.
 __device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t unit, uint32_t c) {
+#ifdef RT_AB_NO_UNIT_COST
+    return;
+#endif
     uint64_t m = __ballot(fin);
     while (m) {
         const uint32_t first = (uint32_t)__builtin_ctzll(m);
@@ -1112,8 +1352,13 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                                                        uint32_t *queue, uint32_t threshold,
                                                        unsigned long long *counters) {
     __shared__ unsigned long long lds_stack[LEAN ? LEAN_DEPTH : LDS_DEPTH][BLOCK];
+    __shared__ float4 lds_mat[LDS_MATERIALS];     // the scene's materials (shading reads them per hit)
     const int tid = threadIdx.x;
     const int lane = tid & 63;
+    const bool mat_lds = sc.material_count <= LDS_MATERIALS;
+    if (mat_lds && tid < (int)sc.material_count) lds_mat[tid] = reinterpret_cast<const float4 *>(sc.materials)[tid];
+    __syncthreads();                              // once, before any wave leaves for the queue
+    const TreeRoot root = uniform_root<WIDE>(sc);
 
     Trav T;
     T.stk.lds = (LdsU2 *)&lds_stack[0][tid];
@@ -1140,9 +1385,10 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     uint32_t part = xcc % parts, tried = 0;
     const uint32_t grab = out.grab;                 // claim size (pixels)
     const bool track = out.unit_cost != nullptr;    // record unit costs for the next launch's order
+    uint32_t pend_unit = 0, pend_cost = 0;          // RT_UNIT_COST_DEFER: the lane's unflushed unit cost
     unsigned long long t_start = 0, t_exhaust = 0;
     uint32_t n_rounds = 0, n_shades = 0, n_grabs = 0;      // wave-uniform (timeline)
-    PhaseCycles pc = {0, 0, 0, 0, 0, 0};
+    PhaseCycles pc = {0, 0, 0, 0, 0, 0, 0, 0};
     if (out.timeline) t_start = __builtin_amdgcn_s_memrealtime();
 
     for (;;) {
@@ -1166,6 +1412,11 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     limit = out.order ? __builtin_amdgcn_readfirstlane(queue[(QUEUE_MAX_PARTS + part) * QUEUE_STRIDE])
                                       : p_end - p_begin;
                 }
+                DIAG_T(t_claim);
+                if (RT_UNIT_COST_DEFER && track) {   // completes under the claim's wait
+                    unit_cost_add(out.unit_cost, pend_cost != 0, pend_unit, pend_cost);
+                    pend_cost = 0;
+                }
                 uint32_t b = 0;
                 if (lane == 0) b = atomicAdd(queue + part * QUEUE_STRIDE, step);
                 b = __builtin_amdgcn_readfirstlane(__shfl(b, 0, 64));
@@ -1184,11 +1435,13 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     const uint32_t len = 64u >> (it & 3u);
                     pool_next = (it >> 4) * 64u + ((it >> 2) & 3u) * len;
                     pool_end = pool_next + len;
+                    DIAG_WAIT_VM();
                 } else {
                     b += p_begin;
                     pool_next = b;
                     pool_end = min(b + grab, p_end);
                 }
+                DIAG_ADD(pc.claim, t_claim);
                 if (!out.order && out.supertile && out.tile_count == 0 && grab == 64u) {
                     // walk the band in st x st-unit supertiles (row-major supertiles, row-major units
                     // inside): the units in flight form a compact screen region, not a full-width strip
@@ -1221,7 +1474,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     px_steps = 0;
                     f3 o, d;
                     camera_ray(cam, px, py, 0, rng, o, d);
-                    trav_init<WIDE>(T, sc, o, d);
+                    trav_init(T, root, o, d);
                     pixels++;
                 }
             }
@@ -1241,6 +1494,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             if ((uint32_t)__popcll(want) >= threshold) break;
 #if !RT_EXACT
             if constexpr (LEAN) lean_round<COUNT>(T, sc, cnt, pc, px_steps, COUNT || track);
+            else if constexpr (WIDE && RT_LEAN_WIDE) lw_round<COUNT>(T, sc, spill, cnt, pc, px_steps, COUNT || track);
             else
 #endif
                 spec_round<COUNT, WIDE>(T, sc, spill, cnt, pc, px_steps, COUNT || track);
@@ -1256,8 +1510,12 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             f3 no = T.wr.o, nd = T.wr.d;                                     // next segment
             if (T.found) {
                 if (COUNT) cnt.hits++;
+                DIAG_T(t_hit);
                 const Surface s = finalize(sc, T.wr.o, T.wr.d, T.hit);
-                const float4 m = reinterpret_cast<const float4 *>(sc.materials)[s.material & ~MAT_METAL_BIT];
+                DIAG_WAIT_VM();
+                DIAG_ADD(pc.hit, t_hit);
+                const uint32_t mi = s.material & ~MAT_METAL_BIT;
+                const float4 m = mat_lds ? lds_mat[mi] : reinterpret_cast<const float4 *>(sc.materials)[mi];
                 bool absorbed = false;
                 if (!(s.material & MAT_METAL_BIT)) {                         // Rough.cuh:14-29
                     nd = add(s.n, random_space_vector(rng));
@@ -1295,12 +1553,25 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     fin = true;
                 }
             }
-            if (has) trav_init<WIDE>(T, sc, no, nd);
+            if (has) trav_init(T, root, no, nd);
         }
-        if (track) unit_cost_add(out.unit_cost, fin, item >> 6, px_steps + 1u);
+        if (RT_UNIT_COST_DEFER) {
+            if (track && fin) {
+                const uint32_t u = item >> 6;
+                if (u != pend_unit) {
+                    if (pend_cost) atomicAdd(out.unit_cost + pend_unit, pend_cost);
+                    pend_unit = u;
+                    pend_cost = 0;
+                }
+                pend_cost += px_steps + 1u;
+            }
+        } else if (track) {
+            unit_cost_add(out.unit_cost, fin, item >> 6, px_steps + 1u);
+        }
         DIAG_ADD(pc.shade, t_shade);
     }
 
+    if (RT_UNIT_COST_DEFER && track && pend_cost) atomicAdd(out.unit_cost + pend_unit, pend_cost);
     const uint32_t wr = wave_sum(rays);
     const uint32_t wp = wave_sum(pixels);
     if (COUNT) {
@@ -1335,6 +1606,8 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             w[11] = pc.shade;
             w[12] = pc.iters;
             w[13] = pc.refill_iters;
+            w[14] = pc.claim;
+            w[15] = pc.hit;
         }
     }
 }
@@ -1418,7 +1691,7 @@ constexpr bool HAS_WIDE = true;
 #endif
 }  // namespace
 
-// variant: 0 = compiler's register budget, 4 / 5 = at least 4 / 5 waves per SIMD.
+// variant: 0 = compiler's register budget (quad trees: at least 3 waves per SIMD), 4 / 5 = at least 4 / 5 waves per SIMD.
 // lean: LDS-only-stack traversal (FAST kernel; the caller checks the tree heights).
 hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
                                                unsigned long long *counters, uint32_t *queue, uint32_t blocks,
@@ -1436,7 +1709,7 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
     }
     if (sc.wide && HAS_WIDE) {
         if (variant == 4) return launch_persistent_wpe<4, false, HAS_WIDE>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-        return launch_persistent_wpe<0, false, HAS_WIDE>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+        return launch_persistent_wpe<3, false, HAS_WIDE>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     }
     if (variant == 4) return launch_persistent_wpe<4, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     if (variant == 5) return launch_persistent_wpe<5, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
@@ -1449,7 +1722,7 @@ uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, bool lean, bool w
         if (variant == 5) return blocks_per_cu_wpe<5, HAS_LEAN>();
         return blocks_per_cu_wpe<3, HAS_LEAN>();
     }
-    if (wide && HAS_WIDE) return variant == 4 ? blocks_per_cu_wpe<4, false, HAS_WIDE>() : blocks_per_cu_wpe<0, false, HAS_WIDE>();
+    if (wide && HAS_WIDE) return variant == 4 ? blocks_per_cu_wpe<4, false, HAS_WIDE>() : blocks_per_cu_wpe<3, false, HAS_WIDE>();
     if (variant == 4) return blocks_per_cu_wpe<4, false>();
     if (variant == 5) return blocks_per_cu_wpe<5, false>();
     return blocks_per_cu_wpe<0, false>();

@@ -110,7 +110,7 @@ class Stats(C.Structure):
                 ("triangle_tests", C.c_uint64), ("sphere_quad_tests", C.c_uint64),
                 ("quad_tests", C.c_uint64), ("instance_visits", C.c_uint64), ("hits", C.c_uint64),
                 ("kernel_ms", C.c_double),
-                ("frame_ms", C.c_double), ("update_ms", C.c_double)]
+                ("frame_ms", C.c_double), ("update_ms", C.c_double), ("update_wait_ms", C.c_double)]
 
 
 class Hit(C.Structure):

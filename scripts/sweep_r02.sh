@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-2 sweeps on one GPU: overlap lanes x reserve, threshold, and the C4 per-rank shares.
-# usage: sweep_r02.sh [what]  (what: lanes | thr | c4 | all; outputs gpurun_out/sweep_*.jsonl)
+# usage: sweep_r02.sh [what]  (what: lanes | thr | c4 | reorder | all; outputs gpurun_out/sweep_*.jsonl)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 WHAT=${1:-all}
@@ -20,5 +20,40 @@ fi
 if [[ $WHAT == c4 || $WHAT == all ]]; then
   one sweep_c4.jsonl --config C4 ${C4_ARGS:-}
   for r in 0 1 2 3 4 5 6 7; do one sweep_c4.jsonl --config C4 --shard $r/8 ${C4_ARGS:-}; done
+fi
+if [[ $WHAT == split ]]; then
+  # heavy-first order with / without split claims vs screen order
+  for rep in 1 2; do for o in "--opt reorder=0" "--opt reorder=1" "--opt reorder=1 --opt split=0xFFFF" "--opt reorder=1 --opt split=0x0C0C"; do
+    one sweep_split.jsonl $o
+    one sweep_split.jsonl --config C3 $o
+  done; done
+fi
+if [[ $WHAT == period ]]; then
+  # reorder period K (costs recorded / order rebuilt once per K launches of a lane) x split claims
+  for rep in 1 2; do for o in "--opt reorder=0" "--opt reorder_period=1" "--opt reorder_period=8" "--opt reorder_period=8 --opt split=0xFFFF" "--opt reorder_period=32 --opt split=0xFFFF"; do
+    one sweep_period.jsonl $o
+  done; done
+  for o in "--opt reorder=0" "--opt reorder_period=1" "--opt reorder_period=8" "--opt reorder_period=8 --opt split=0xFFFF"; do
+    one sweep_period.jsonl --config C3 $o
+    one sweep_period.jsonl --config C4 --shard 3/8 $o
+  done
+fi
+if [[ $WHAT == period2 ]]; then
+  for rep in 1 2; do for o in "--opt reorder_period=1 --opt split=0x0C0C" "--opt reorder_period=4 --opt split=0x0C0C" "--opt reorder_period=8 --opt split=0x0C0C"; do
+    one sweep_period2.jsonl $o
+  done; done
+  for o in "--opt reorder_period=4 --opt split=0x0C0C" "--opt reorder_period=8 --opt split=0x0C0C"; do
+    one sweep_period2.jsonl --config C3 $o
+    one sweep_period2.jsonl --config C4 --shard 3/8 $o
+  done
+fi
+if [[ $WHAT == reorder ]]; then
+  # claim order on/off across the configs (heaviest-first order vs screen order)
+  for rep in 1 2; do for ro in 0 1; do
+    one sweep_reorder.jsonl --opt reorder=$ro
+    one sweep_reorder.jsonl --config C3 --opt reorder=$ro
+  done; done
+  for ro in 0 1; do for r in 0 3 5 7; do one sweep_reorder.jsonl --config C4 --shard $r/8 --opt reorder=$ro; done; done
+  for ro in 0 1; do one sweep_reorder.jsonl --config C5 --build lbvh --rebuild --steps 8 --warmup 2 --opt reorder=$ro; done
 fi
 exit 0

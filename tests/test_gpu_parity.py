@@ -285,7 +285,7 @@ def test_reorder_schedule_is_byte_identical(gpu_lib, exact):
     for f in range(4):
         ref[f] = r.render(f, exact=exact, want_rgb=True)
     tref = r.render(3, exact=exact, tiles=(64, 64, 1, 3), skip_update=True)[0]
-    r.set_option("reorder", 1).set_option("split", 8 | 10 << 8)
+    r.set_option("reorder", 1).set_option("split", 8 | 10 << 8).set_option("reorder_period", 1)
     ux, rows = W // 8, H // 8
     for f in range(4):
         rgba, rgb, st = r.render(f, exact=exact, want_rgb=True)
@@ -378,6 +378,29 @@ def test_split_claims_are_byte_identical(gpu_lib, split):
     r.set_option("reorder", 1).set_option("split", split)
     for f in range(3):
         assert np.array_equal(r.render(f)[0], ref[f]), (split, f)
+
+
+@pytest.mark.parametrize("period,lanes", [(3, 1), (8, 3)])
+def test_reorder_period_byte_identical(gpu_lib, period, lanes):
+    """Option "reorder_period" K: a lane records unit costs on one launch in K, orders its next launch
+    from them and reuses that order until the next recording; frames stay byte-identical to the
+    screen-order walk on every phase, with one and with several overlapped lanes."""
+    import torch
+    s = scenes.demo_with_particles(10)
+    W, H, F = 360, 200, 2 * period * lanes + 2
+    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(W, H, ray_trace_depth=2)
+    r.set_option("reorder", 0)
+    ref = [r.render(f)[0] for f in range(F)]
+    r.set_option("reorder", 1).set_option("reorder_period", period)
+    if lanes > 1:
+        r.set_option("overlap", lanes)
+    streams = [torch.cuda.Stream() for _ in range(lanes)]
+    bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(F)]
+    for f in range(F):
+        r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=streams[f % lanes].cuda_stream, sync=False)
+    torch.cuda.synchronize()
+    for f in range(F):
+        assert np.array_equal(bufs[f].cpu().numpy().reshape(H, W, 4), ref[f]), f
 
 
 @pytest.mark.parametrize("tiles,nl,mode", [(None, 2, "sah"), ((64, 64, 1, 3), 2, "sah"), (None, 3, "sah"),

@@ -1,0 +1,32 @@
+"""CPU check of the presorted SAH builder (csrc/bvh_build.hpp build_sah_tree, the per-frame host TLAS
+of RT_BUILD_SAH): it builds exactly build_sah_tree_nodewise's tree — random, tied, flat and degenerate
+(all centroids equal) inputs, leaf sizes 1..4 — so switching the builder changes no image."""
+import json
+import os
+import subprocess
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def checker(tmp_path_factory):
+    exe = str(tmp_path_factory.mktemp("sah") / "sah_presort_check")
+    subprocess.run(["g++", "-std=c++17", "-O2", "-D__host__=", "-D__device__=", "-o", exe,
+                    os.path.join(HERE, "cpp", "sah_presort_check.cpp")], check=True)
+    return exe
+
+
+@pytest.mark.parametrize("leaf", [1, 2, 4])
+@pytest.mark.parametrize("kind", [0, 1, 2, 3])
+@pytest.mark.parametrize("n", [1, 2, 3, 7, 73, 258, 1024])
+def test_presorted_sah_equals_nodewise(checker, n, kind, leaf):
+    r = json.loads(subprocess.run([checker, str(n), str(kind), str(leaf)], check=True, capture_output=True,
+                                  text=True).stdout)
+    assert r["same"] == 1, r
+
+
+def test_presorted_sah_is_faster_on_a_c3_tlas(checker):
+    r = json.loads(subprocess.run([checker, "258", "0", "1"], check=True, capture_output=True, text=True).stdout)
+    assert r["same"] == 1 and r["presort_ms"] < r["nodewise_ms"], r
