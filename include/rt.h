@@ -305,6 +305,10 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "reorder"   : 1 (default) = each launch claims its band's 8x8 units heaviest-first, ordered by the
  *                 traversal work the previous launch of the same layout and lane recorded per unit (schedule.hip);
  *                 0 = screen order.  Images are identical either way (the RNG is keyed by pixel).
+ *   "primary"   : FAST persistent kernel on quad trees: 1 = the first camera ray of every pixel is traced
+ *                 beforehand by one wave per 8x8 unit walking the union of its rays' paths (wave-uniform
+ *                 node / instance / primitive loads); 0 (default, measured faster) = traced inside the
+ *                 persistent kernel
  *   "reorder_period": with "reorder", K = a lane records unit costs on one launch in K and rebuilds its
  *                 claim order on the next; the other launches reuse the order (default 8; 1 = every launch)
  *   "split"     : with "reorder", heavy units are claimed in pieces shared by several waves: halves from

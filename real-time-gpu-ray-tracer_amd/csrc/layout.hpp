@@ -223,7 +223,14 @@ struct OutputGPU {
     // largest cost (traversal rounds + 1) of unit u's pixels for the next launch's order
     const uint32_t *order;
     uint32_t *unit_cost;
+    // option "primary" (FAST, quad trees): the closest hits of every pixel's first camera ray, traced by
+    // primary_packet_kernel before the persistent launch; record j = work item j (unit * 64 + lane):
+    // {t, instance record (PREC_MISS / PREC_TRACE), ptype << 28 | slot, u} + v.  Null: traced in place.
+    uint32_t *prim_rec;             // 4 words per record (16 B aligned)
+    float *prim_v;
 };
+constexpr uint32_t PREC_MISS = 0xFFFFFFFFu;    // primary record: no hit
+constexpr uint32_t PREC_TRACE = 0xFFFFFFFEu;   // primary record: not resolved (packet stack full), trace it
 constexpr uint32_t QUEUE_STRIDE = 32;         // u32 words between partition heads (128 B lines)
 constexpr uint32_t QUEUE_MAX_PARTS = 8;
 // queue block of a lane: band heads (lines 0..7), band item counts (lines 8..15)

@@ -36,6 +36,7 @@ hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, c
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
 hipError_t launch_frame_copy(void *, const void *, size_t, unsigned long long *, uint32_t *, hipStream_t);
+hipError_t launch_primary_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *, hipStream_t);
 hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t,
                            uint32_t, void *, const void *, size_t, unsigned long long *, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean, bool wide);
@@ -214,6 +215,11 @@ struct rt_scene {
     // shares, profiles/r02_sweep_period*.jsonl): quarters from level 12 and no halves
     uint32_t split = 12u | 12u << 8;
     DevBuf<uint32_t> unit_cost[NLANE], unit_order[NLANE];
+    // option "primary" (FAST persistent kernel on quad trees): per-lane records of the packet-traced
+    // first camera rays (OutputGPU::prim_rec), one per work item
+    bool primary = false;               // measured slower (C2: packet kernel 0.22 ms vs ~0.08 ms of in-kernel primary traversal)
+    DevBuf<uint32_t> prim_rec[NLANE];
+    DevBuf<float> prim_v[NLANE];
     uint32_t sched_sig[NLANE][7] = {};  // launch layout the recorded costs belong to
     // option "reorder_period" K: a lane records unit costs on one launch in K and rebuilds its order on
     // the next; the launches between reuse the order (the heaviest regions move little between frames)
@@ -283,7 +289,7 @@ struct rt_scene {
         blas_pairs.release(); blas_quads.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
         quad_hot.release(); quad_cold.release(); materials.release(); out_rgba.release(); out_rgb.release();
         timeline.release(); costmap.release();
-        for (int q = 0; q < NLANE; q++) { unit_cost[q].release(); unit_order[q].release(); }
+        for (int q = 0; q < NLANE; q++) { unit_cost[q].release(); unit_order[q].release(); prim_rec[q].release(); prim_v[q].release(); }
         delete blas_builder; delete tlas_builder;
         raw_tris.release(); raw_sph.release(); raw_quad.release(); blas_roots.release(); inst_blas.release();
         blas_wide_refs.release();
@@ -1229,6 +1235,21 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     if (s->ring_pending < rt_scene::RING) s->ring_pending++;
     s->last_stream = stream;
     HIP_TRY(hipEventRecord(s->ring_start[slot], stream));
+    if (s->use_persistent && !exact && !lean && g.wide && s->primary) {
+        // the first camera ray of every pixel, packet-traced per 8x8 unit (trace_kernel.hip)
+        const size_t n = (size_t)out.units * 64;
+        if (s->prim_rec[q].n < 4 * n) {
+            s->prim_rec[q].release();
+            s->prim_v[q].release();
+            HIP_TRY(hipMalloc(&s->prim_rec[q].p, 4 * n * sizeof(uint32_t)));
+            s->prim_rec[q].n = 4 * n;
+            HIP_TRY(hipMalloc(&s->prim_v[q].p, n * sizeof(float)));
+            s->prim_v[q].n = n;
+        }
+        out.prim_rec = s->prim_rec[q].p;
+        out.prim_v = s->prim_v[q].p;
+        HIP_TRY(launch_primary_fast(g, cam, out, count, lane_counters, stream));
+    }
     if (s->use_persistent) {
         const uint32_t cap = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false, false)
                                              : persistent_blocks_per_cu_fast(s->variant, lean, g.wide != 0));
@@ -1398,6 +1419,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "reserve") {
         if (value < 0 || value > 256) return fail(RT_ERR_INVALID_ARGUMENT, "reserve must be in 0..256");
         s->reserve = (uint32_t)value;
+    } else if (k == "primary") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "primary must be 0 or 1");
+        s->primary = value == 1;
     } else if (k == "reorder_period") {
         if (value < 1 || value > 1024) return fail(RT_ERR_INVALID_ARGUMENT, "reorder_period must be in 1..1024");
         s->reorder_period = (uint32_t)value;

@@ -1287,8 +1287,11 @@ __device__ __forceinline__ bool map_item(const OutputGPU &out, const CameraGPU &
 }
 
 // Camera ray of sample `sample` of pixel (px, py) (Kernel.cu:119-135), consuming the pixel's RNG.
+// Evaluated without FMA contraction in both kernels, so the primary packet kernel and the persistent
+// kernel regenerate bit-identical camera rays (option "primary").
 __device__ __forceinline__ void camera_ray(const CameraGPU &cam, uint32_t px, uint32_t py, uint32_t sample, Rng &rng,
                                            f3 &o, f3 &d) {
+#pragma clang fp contract(off)
     const uint32_t si = sample / cam.sqrt_s, sj = sample % cam.sqrt_s;
     const float ox = (((float)sj + rng.uniform()) * cam.recip_sqrt) - 0.5f;
     const float oy = (((float)si + rng.uniform()) * cam.recip_sqrt) - 0.5f;
@@ -1474,6 +1477,19 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     px_steps = 0;
                     f3 o, d;
                     camera_ray(cam, px, py, 0, rng, o, d);
+#if !RT_EXACT
+                    const uint4 rec = out.prim_rec ? reinterpret_cast<const uint4 *>(out.prim_rec)[item]
+                                                   : make_uint4(0u, PREC_TRACE, 0u, 0u);
+                    if (rec.y != PREC_TRACE) {          // option "primary": the packet kernel's closest hit
+                        T.wr.o = o; T.wr.d = d;
+                        T.tracing = false;
+                        T.found = rec.y != PREC_MISS;
+                        T.tmax = __uint_as_float(rec.x);
+                        T.hit.t = T.tmax; T.hit.inst = rec.y; T.hit.ptype = rec.z >> 28; T.hit.slot = rec.z & 0x0FFFFFFFu;
+                        T.hit.u = __uint_as_float(rec.w); T.hit.v = out.prim_v[item];
+                        T.stk.sp = 0; T.stk.spilled = 0; T.pleaf = REF_NONE; T.cur = REF_NONE; T.in_blas = false;
+                    } else
+#endif
                     trav_init(T, root, o, d);
                     pixels++;
                 }
@@ -1648,6 +1664,212 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const fl
     hits[i] = r;
 }
 
+#if !RT_EXACT
+// ---- primary packets (option "primary", FAST kernel on quad trees) ----------------------------
+// The first camera ray of every pixel is the same for every frame's path and the 64 of one 8x8 unit
+// are coherent (measured, C2: depth-1 launches alone took 0.233 of the 0.358 ms frame,
+// scripts/depth_probe.py), so they are traced before the persistent launch by one wave per unit that
+// walks the union of its rays' paths together: the node, instance and primitive records are
+// wave-uniform loads, the stack holds one node ref per entry (LDS) plus each lane's entry t (lanes
+// whose entry t >= their tmax sit the node out), the walk order is by the first hitting lane's entry t
+// (FAST tolerance: only ties within the 1e-6 window can resolve differently).  Every slab and
+// primitive test is the per-lane traversal's own function, so each ray's closest hit is the one the
+// persistent kernel would find.  Only sample 0 is traced here: later samples' camera jitter depends
+// on how many RNG draws the earlier paths took.  The persistent kernel shades the record (regenerating
+// the same camera ray, camera_ray is evaluated without contraction), or traces the pixel itself when
+// the wave's stack filled up (PREC_TRACE).  Measured (C2, rocprofv3): 0.22 ms for the 2.07 M primary
+// rays — each node visit is one dependent scalar-load round trip for the whole wave (~35 per packet),
+// against ~0.08 ms of primary traversal inside the persistent kernel — so the option is off by default.
+constexpr int PSTACK = 32;
+
+__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// sort 4 children by a wave-uniform key; the per-lane entry t / hit flags move with them
+__device__ __forceinline__ void cswap_pk(float &ka, uint32_t &ra, float &ta, bool &ha, float &kb, uint32_t &rb, float &tb,
+                                         bool &hb) {
+    if (kb < ka) {                       // uniform condition
+        float k = ka; ka = kb; kb = k;
+        uint32_t r = ra; ra = rb; rb = r;
+        float t = ta; ta = tb; tb = t;
+        bool h = ha; ha = hb; hb = h;
+    }
+}
+
+template <bool COUNT>
+__global__ __launch_bounds__(64) void primary_packet_kernel(SceneGPU sc, CameraGPU cam, OutputGPU out,
+                                                            unsigned long long *counters) {
+    __shared__ float tstk[PSTACK][64];       // per-lane entry t of each pushed node
+    __shared__ uint32_t rstk[PSTACK];        // the pushed node refs (wave-uniform)
+    const uint32_t lane = threadIdx.x;
+    const uint32_t item = blockIdx.x * 64u + lane;
+    uint32_t px, py, oi;
+    const bool alive = map_item(out, cam, item, px, py, oi);
+    LaneCount cnt = {0, 0, 0, 0, 0, 0, 0};
+    f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
+    if (alive) {
+        const uint32_t pixel = cam.pitch * py + px;
+        Rng rng;
+        rng.init((uint64_t)pixel ^ cam.frame_seed, pixel);                      // Kernel.cu:114
+        camera_ray(cam, px, py, 0, rng, o, d);
+    }
+    RayP wr;
+    wr.o = o; wr.d = d;
+    prep(wr);
+    RayP lr = wr;
+    float tmax = __builtin_huge_valf();
+    uint32_t h_inst = PREC_MISS, h_pslot = 0;
+    float h_u = 0.0f, h_v = 0.0f;
+    const TreeRoot root = uniform_root<true>(sc);
+    float te = __builtin_huge_valf();
+    if (alive) {
+        float t0 = 0.0f;
+        if (slab(root.box, wr, TMIN, tmax, t0)) te = t0;
+    }
+    uint32_t cur = root.ref;              // wave-uniform walk state
+    uint32_t cur_inst = 0;
+    int sp = 0;
+    bool in_blas = false, overflow = false;
+    bool have = __ballot(te < tmax) != 0;
+    while (have) {
+        const bool act = te < tmax;
+        bool pop = true;
+        if (!(cur & REF_LEAF)) {
+            // interior quad: 4 slab tests per lane against the uniform node
+            const NodeQuad *base = (cur & REF_BLAS) ? sc.blas_quads : sc.tlas_quads;
+            const float4 *Q = reinterpret_cast<const float4 *>(base + (cur & REF_INDEX_MASK));
+            const float4 lx = Q[0], hx = Q[1], ly = Q[2], hy = Q[3], lz = Q[4], hz = Q[5];
+            const uint4 R = reinterpret_cast<const uint4 *>(Q)[6];
+            const RayP &r = in_blas ? lr : wr;
+            float t[4];
+            bool h[4];
+            if (!r.tiny) {
+                float4 tn = make_float4(TMIN, TMIN, TMIN, TMIN), tf = make_float4(tmax, tmax, tmax, tmax);
+                slab4(lx, hx, r.inv.x, r.oinv.x, tn, tf);
+                slab4(ly, hy, r.inv.y, r.oinv.y, tn, tf);
+                slab4(lz, hz, r.inv.z, r.oinv.z, tn, tf);
+                t[0] = tn.x; t[1] = tn.y; t[2] = tn.z; t[3] = tn.w;
+                h[0] = tn.x < tf.x; h[1] = tn.y < tf.y; h[2] = tn.z < tf.z; h[3] = tn.w < tf.w;
+            } else {
+                const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+                const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
+                const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+#pragma unroll
+                for (int k = 0; k < 4; k++) {
+                    const float b[6] = {LX[k], HX[k], LY[k], HY[k], LZ[k], HZ[k]};
+                    t[k] = 0.0f;
+                    h[k] = slab_ref(b, r.o, r.d, TMIN, tmax, t[k]);
+                }
+            }
+            if (COUNT && act) cnt.pairs += 2;
+            float key[4];
+            uint32_t ref[4] = {R.x, R.y, R.z, R.w};
+            uint32_t nh = 0;
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                h[k] = h[k] && act;
+                const uint64_t m = __ballot(h[k]);
+                key[k] = m ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[k]), (int)__builtin_ctzll(m)))
+                           : __builtin_huge_valf();
+                nh += m ? 1u : 0u;
+                if (!h[k]) t[k] = __builtin_huge_valf();
+            }
+            if (nh) {
+                cswap_pk(key[0], ref[0], t[0], h[0], key[1], ref[1], t[1], h[1]);
+                cswap_pk(key[2], ref[2], t[2], h[2], key[3], ref[3], t[3], h[3]);
+                cswap_pk(key[0], ref[0], t[0], h[0], key[2], ref[2], t[2], h[2]);
+                cswap_pk(key[1], ref[1], t[1], h[1], key[3], ref[3], t[3], h[3]);
+                cswap_pk(key[1], ref[1], t[1], h[1], key[2], ref[2], t[2], h[2]);
+                if (sp + (int)nh - 1 > PSTACK) { overflow = true; break; }
+#pragma unroll
+                for (int k = 3; k >= 1; k--)                  // farthest first: popped nearest first
+                    if ((uint32_t)k < nh) {
+                        tstk[sp][lane] = t[k];
+                        rstk[sp] = ref[k];
+                        sp++;
+                    }
+                cur = uni(ref[0]);
+                te = t[0];
+                pop = false;
+            }
+        } else if (!(cur & REF_BLAS)) {
+            // TLAS leaf: its remaining instances wait on the stack with the leaf's entry t; enter the first
+            const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur);
+            if (count > 1) {
+                if (sp == PSTACK) { overflow = true; break; }
+                tstk[sp][lane] = te;
+                rstk[sp] = make_leaf_ref(start + 1, count - 1, 0, false);
+                sp++;
+            }
+            cur_inst = uni(sc.inst_by_slot ? start : sc.tlas_slots[start]);
+            const InstHot &I = sc.inst_hot[cur_inst];
+            if (COUNT && act) cnt.inst++;
+            lr.o = xf_point(I.inv, wr.o);                                  // Instance.cu:26-27
+            lr.d = xf_vector(I.inv, wr.d);
+            prep(lr);
+            float t0 = 0.0f;
+            const bool hb = act && slab(I.root_box, lr, TMIN, tmax, t0);
+            if (__ballot(hb)) {
+                in_blas = true;
+                cur = uni(I.root_ref_wide);
+                te = hb ? t0 : __builtin_huge_valf();
+                pop = false;
+            }
+        } else {
+            // BLAS leaf: its primitives in leaf order against each active lane's instance ray
+            const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur), type = ref_leaf_type(cur);
+            for (uint32_t k = 0; k < count; k++) {
+                const uint32_t slot = start + k;
+                float t = 0.0f, u = 0.0f, v = 0.0f;
+                bool hh = false;
+                if (type == RT_PRIM_TRIANGLE) {
+                    if (COUNT && act) cnt.tri++;
+                    if (act) hh = tri_test(sc.tri_hot[slot], lr, TMIN, tmax, t, u, v);
+                } else if (type == RT_PRIM_SPHERE) {
+                    if (COUNT && act) cnt.sq++;
+                    if (act) hh = sphere_test(sc.sph_hot[slot], lr, TMIN, tmax, t);
+                } else {
+                    if (COUNT && act) { cnt.sq++; cnt.quad++; }
+                    if (act) hh = quad_test(sc.quad_hot[slot], lr, TMIN, tmax, t, u, v);
+                }
+                if (hh) {
+                    tmax = t; h_inst = cur_inst; h_pslot = (type << 28) | slot; h_u = u; h_v = v;
+                }
+            }
+        }
+        if (pop) {
+            have = false;
+            while (sp > 0) {
+                sp--;
+                const float t = tstk[sp][lane];
+                if (__ballot(t < tmax)) {
+                    cur = uni(rstk[sp]);
+                    te = t;
+                    if (!(cur & REF_BLAS)) in_blas = false;      // back in the TLAS: world rays
+                    have = true;
+                    break;
+                }
+            }
+        }
+    }
+    if (item < out.units * 64u) {
+        const uint32_t inst = overflow ? PREC_TRACE : h_inst;
+        reinterpret_cast<uint4 *>(out.prim_rec)[item] = make_uint4(__float_as_uint(tmax), inst, h_pslot, __float_as_uint(h_u));
+        out.prim_v[item] = h_v;
+    }
+    if (COUNT) {
+        const uint32_t a = wave_sum(cnt.pairs), b = wave_sum(cnt.tri), c = wave_sum(cnt.sq), e = wave_sum(cnt.inst),
+                       f = wave_sum(cnt.quad);
+        if (lane == 0) {
+            atomicAdd(&counters[CNT_PAIRS], (unsigned long long)a);
+            atomicAdd(&counters[CNT_TRI], (unsigned long long)b);
+            atomicAdd(&counters[CNT_SPHQUAD], (unsigned long long)c);
+            atomicAdd(&counters[CNT_INST], (unsigned long long)e);
+            atomicAdd(&counters[CNT_QUAD], (unsigned long long)f);
+        }
+    }
+}
+#endif
+
 }  // namespace dev
 
 hipError_t RT_SUFFIX(launch_render)(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
@@ -1735,5 +1957,18 @@ hipError_t RT_SUFFIX(launch_trace_rays)(const SceneGPU &sc, const float *rays, u
     hipLaunchKernelGGL(trace_rays_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, stream, sc, rays, n, hits);
     return hipGetLastError();
 }
+
+#if !RT_EXACT
+// One wave per 8x8 unit; out.prim_rec / prim_v hold out.units * 64 records.
+hipError_t launch_primary_fast(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
+                               unsigned long long *counters, hipStream_t stream) {
+    using namespace dev_fast;
+    if (out.units == 0) return hipSuccess;
+    if (!out.prim_rec || !out.prim_v || !sc.wide) return hipErrorInvalidValue;
+    if (count) hipLaunchKernelGGL(primary_packet_kernel<true>, dim3(out.units), dim3(64), 0, stream, sc, cam, out, counters);
+    else hipLaunchKernelGGL(primary_packet_kernel<false>, dim3(out.units), dim3(64), 0, stream, sc, cam, out, counters);
+    return hipGetLastError();
+}
+#endif
 
 }  // namespace rtamd
