@@ -214,14 +214,17 @@ def main():
     def finish_gather():
         """(kept for the call sites: the gather is stream-ordered inside rt_render)"""
 
+    host_update = []                                       # (update_ms, part of it waiting on the GPU) per call
+
     def step(frame, sync=True, keep=False):
         """One frame; sync=False pipelines it (host TLAS build of the next frame overlaps the GPU).
         With "overlap", frame k runs on lanes[k % L] (its own trace -> gather -> assemble chain)."""
         b = frame % L if overlap else 0
         st = lanes[b].cuda_stream if overlap else stream
         fb = frame_bufs[b]
-        r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=fb.data_ptr() if fb is not None else None,
-                 stream=st, sync=sync, keep_counters=keep, tiles=tiles)
+        _, _, sts = r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=fb.data_ptr() if fb is not None else None,
+                             stream=st, sync=sync, keep_counters=keep, tiles=tiles)
+        host_update.append((sts["update_ms"], sts["update_wait_ms"]))
 
     for f in range(args.warmup):
         step(f)
@@ -231,6 +234,7 @@ def main():
     torch.cuda.synchronize()
 
     r.collect()                                            # drop warm-up timings
+    host_update.clear()
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k, sync=False, keep=True)      # counters were zeroed by collect()
@@ -240,6 +244,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    timed_update = np.asarray(host_update[:args.steps], dtype=np.float64).reshape(-1, 2)
     acc, kernel_ms = r.collect()                           # device counters + HIP-event kernel times
     rays = int(acc["rays"])
     assert len(kernel_ms) == args.steps, (len(kernel_ms), args.steps)
@@ -322,6 +327,10 @@ def main():
                           else "whole-frame throughput, serialised frames",
             "rays_per_frame": round(rays / args.steps, 1),
             "frame_latency_ms_median": round(float(np.median(lat)), 4),
+            # host side of a timed rt_render call (update callback, instance records, TLAS build, staging)
+            # and the part of it spent blocked on the GPU (a staging buffer still in use)
+            "host_update_ms_median": round(float(np.median(timed_update[:, 0])), 4),
+            "host_update_wait_ms_median": round(float(np.median(timed_update[:, 1])), 4),
             "kernel_ms": round(serial_kernel_ms, 4),
             "kernel_ms_overlapped": round(avg_kernel_ms, 4),
             "roofline": {

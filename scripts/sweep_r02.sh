@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round-2 sweeps on one GPU: overlap lanes x reserve, threshold, and the C4 per-rank shares.
-# usage: sweep_r02.sh [what]  (what: lanes | thr | c4 | reorder | all; outputs gpurun_out/sweep_*.jsonl)
+# usage: sweep_r02.sh [what]  (what: lanes | thr | c4 | reorder | split | period | period2 | shares | all; outputs gpurun_out/sweep_*.jsonl)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 WHAT=${1:-all}
@@ -9,7 +9,7 @@ one() {  # out args...
   timeout -k 10 240 python bench.py --no-cpu-baseline "$@" > gpurun_out/_one.log 2>&1
   local rc=$?
   if [ $rc -ne 0 ]; then echo "rc=$rc for $*"; tail -3 gpurun_out/_one.log; exit $rc; fi
-  tail -1 gpurun_out/_one.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'args': '$*', 'value': d['value'], 'ms_per_step': d['ms_per_step'], 'kernel_ms': d['kernel_ms'], 'kernel_ms_overlapped': d['kernel_ms_overlapped'], 'lat': d['frame_latency_ms_median']}))" | tee -a "gpurun_out/$out"
+  tail -1 gpurun_out/_one.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'args': '$*', 'value': d['value'], 'ms_per_step': d['ms_per_step'], 'kernel_ms': d['kernel_ms'], 'kernel_ms_overlapped': d['kernel_ms_overlapped'], 'lat': d['frame_latency_ms_median'], 'host_update_ms': d.get('host_update_ms_median'), 'host_wait_ms': d.get('host_update_wait_ms_median')}))" | tee -a "gpurun_out/$out"
 }
 if [[ $WHAT == lanes || $WHAT == all ]]; then
   for rep in 1 2; do for L in 2 3 4; do for rs in 0 8 16; do one sweep_lanes.jsonl --overlap $L --opt reserve=$rs; done; done; done
@@ -36,6 +36,21 @@ if [[ $WHAT == period ]]; then
   for o in "--opt reorder=0" "--opt reorder_period=1" "--opt reorder_period=8" "--opt reorder_period=8 --opt split=0xFFFF"; do
     one sweep_period.jsonl --config C3 $o
     one sweep_period.jsonl --config C4 --shard 3/8 $o
+  done
+fi
+if [[ $WHAT == lanes4 ]]; then
+  for L in 3 4; do
+    one sweep_lanes4.jsonl --overlap $L
+    one sweep_lanes4.jsonl --config C2 --shard 4/8 --overlap $L
+    one sweep_lanes4.jsonl --config C4 --shard 4/8 --overlap $L
+    one sweep_lanes4.jsonl --config C4 --overlap $L
+  done
+fi
+if [[ $WHAT == shares ]]; then
+  # N=1 frame and each rank's 1/8 share (64x64 tiles) of C4 and C2 with the library defaults
+  for cfg in C4 C2; do
+    one sweep_shares.jsonl --config $cfg
+    for r in 0 1 2 3 4 5 6 7; do one sweep_shares.jsonl --config $cfg --shard $r/8; done
   done
 fi
 if [[ $WHAT == period2 ]]; then
