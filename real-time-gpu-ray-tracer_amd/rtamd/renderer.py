@@ -131,13 +131,13 @@ class Renderer:
                                       ("rounds", np.uint32), ("shades", np.uint32), ("grabs", np.uint32),
                                       ("cyc_refill", np.uint64), ("cyc_interior", np.uint64), ("cyc_leaf", np.uint64),
                                       ("cyc_shade", np.uint64), ("iters", np.uint64), ("refill_iters", np.uint64),
-                                      ("cyc_claim", np.uint64), ("cyc_hit", np.uint64)])
+                                      ("cyc_lanes", np.uint64), ("cyc_scatter", np.uint64)])
         out["start"], out["end"], out["exhaust"] = w[:, 0], w[:, 1], w[:, 4]
         out["xcc"], out["hw_id"], out["pixels"] = w[:, 2] & 0xFFFFFFFF, w[:, 2] >> 32, w[:, 3]
         out["rounds"], out["shades"], out["grabs"] = w[:, 5], w[:, 6], w[:, 7]
         out["cyc_refill"], out["cyc_interior"], out["cyc_leaf"], out["cyc_shade"] = w[:, 8], w[:, 9], w[:, 10], w[:, 11]
         out["iters"], out["refill_iters"] = w[:, 12], w[:, 13]
-        out["cyc_claim"], out["cyc_hit"] = w[:, 14], w[:, 15]       # diagnostic builds only
+        out["cyc_lanes"], out["cyc_scatter"] = w[:, 14], w[:, 15]       # diagnostic builds only: lane refill work, scatter sampling
         return out
 
     def costmap(self):

@@ -39,9 +39,8 @@ def summarize(tl, tag):
                                                         for k in ("cyc_refill", "cyc_interior", "cyc_leaf", "cyc_shade")],
             "stamped_cycles_over_life": round(float((tl["cyc_refill"] + tl["cyc_interior"] + tl["cyc_leaf"] + tl["cyc_shade"]).sum()
                                                     / max(1.0, ((tl["end"] - tl["start"]).astype(np.float64) * 0.01 * 1e-6).sum())) / 1e9, 3),
-            "claim_hit_cycles_over_stamped": [round(float(tl[k].sum() / max(1, (tl["cyc_refill"] + tl["cyc_interior"] + tl["cyc_leaf"] + tl["cyc_shade"]).sum())), 3)
-                                              for k in ("cyc_claim", "cyc_hit")],
-            "cycles_per_claim": round(float(tl["cyc_claim"].sum() / max(1, tl["grabs"].sum())), 1),
+            "lanes_scatter_cycles_over_stamped": [round(float(tl[k].sum() / max(1, (tl["cyc_refill"] + tl["cyc_interior"] + tl["cyc_leaf"] + tl["cyc_shade"]).sum())), 3)
+                                              for k in ("cyc_lanes", "cyc_scatter")],
             "cycles_per_interior_iter": round(float(tl["cyc_interior"].sum() / max(1, tl["iters"].sum())), 1),
             "interior_iters_per_round": round(float(tl["iters"].sum() / max(1, tl["rounds"].sum())), 2),
             "cycles_per_leaf_phase": round(float(tl["cyc_leaf"].sum() / max(1, tl["rounds"].sum())), 1),
