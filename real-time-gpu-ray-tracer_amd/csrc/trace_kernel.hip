@@ -43,8 +43,18 @@ namespace RT_SUFFIX(dev) {
 constexpr float FZERO = 1e-6f;          // FLOAT_ZERO_VALUE (Global.cuh:147)
 constexpr float TMIN = 0.001f;          // Kernel.cu:66
 constexpr int BLOCK = 256;              // 4 waves; each wave owns one 8x8 pixel unit
-constexpr int LDS_DEPTH = 16;           // per-lane stack entries kept in LDS
-constexpr int LDS_MATERIALS = 256;      // persistent kernel: material table in LDS up to this many slots (4 KB)
+#ifndef RT_LDS_DEPTH
+#define RT_LDS_DEPTH 16
+#endif
+#ifndef RT_LDS_MATERIALS
+#define RT_LDS_MATERIALS 256
+#endif
+#ifndef RT_PATH_LDS
+#define RT_PATH_LDS 0                   // 1: the persistent kernel keeps path state (throughput, radiance,
+#endif                                  //    RNG, pixel, sample / depth) in LDS between shade steps
+constexpr int LDS_DEPTH = RT_LDS_DEPTH;         // per-lane stack entries kept in LDS
+constexpr int LDS_MATERIALS = RT_LDS_MATERIALS; // persistent kernel: material table in LDS up to this many slots
+constexpr int PATH_WORDS = 10;                  // RT_PATH_LDS: acc xyz, thr xyz, rng lo / hi, item, sample << 16 | depth
 constexpr int SPILL_DEPTH = 48;         // overflow entries in scratch (max depth 64 = reference)
 #ifndef RT_WIDE_PUSH3
 #define RT_WIDE_PUSH3 1                 // quad step: far hits to 3 LDS slots without branching on their count (+1.6 %)
@@ -1382,6 +1392,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                                                        unsigned long long *counters) {
     __shared__ unsigned long long lds_stack[LEAN ? LEAN_DEPTH : LDS_DEPTH][BLOCK];
     __shared__ float4 lds_mat[LDS_MATERIALS];     // the scene's materials (shading reads them per hit)
+    __shared__ uint32_t lds_path[RT_PATH_LDS ? PATH_WORDS : 1][BLOCK];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const bool mat_lds = sc.material_count <= LDS_MATERIALS;
@@ -1403,6 +1414,26 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     Rng rng;
     rng.s = 0;
     f3 acc = mk(0.0f, 0.0f, 0.0f), thr = mk(1.0f, 1.0f, 1.0f);
+    // RT_PATH_LDS: the path state lives in LDS between shade steps, so it holds no VGPRs during traversal
+    const auto save_path = [&]() {
+        if (RT_PATH_LDS) {
+            lds_path[0][tid] = __float_as_uint(acc.x); lds_path[1][tid] = __float_as_uint(acc.y);
+            lds_path[2][tid] = __float_as_uint(acc.z); lds_path[3][tid] = __float_as_uint(thr.x);
+            lds_path[4][tid] = __float_as_uint(thr.y); lds_path[5][tid] = __float_as_uint(thr.z);
+            lds_path[6][tid] = (uint32_t)rng.s; lds_path[7][tid] = (uint32_t)(rng.s >> 32);
+            lds_path[8][tid] = item; lds_path[9][tid] = sample << 16 | depth;
+        }
+    };
+    const auto load_path = [&]() {
+        if (RT_PATH_LDS) {
+            acc = mk(__uint_as_float(lds_path[0][tid]), __uint_as_float(lds_path[1][tid]), __uint_as_float(lds_path[2][tid]));
+            thr = mk(__uint_as_float(lds_path[3][tid]), __uint_as_float(lds_path[4][tid]), __uint_as_float(lds_path[5][tid]));
+            rng.s = (uint64_t)lds_path[6][tid] | ((uint64_t)lds_path[7][tid] << 32);
+            item = lds_path[8][tid];
+            const uint32_t sd = lds_path[9][tid];
+            sample = sd >> 16; depth = sd & 0xFFFFu;
+        }
+    };
     uint32_t pool_next = 0, pool_end = 0;     // wave-uniform
     uint32_t limit = 0, limit_part = ~0u;     // wave-uniform: claim positions in band `limit_part`
     bool exhausted = false;                   // wave-uniform
@@ -1515,6 +1546,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     } else
 #endif
                     trav_init(T, root, o, d);
+                    save_path();
                     pixels++;
                 }
             }
@@ -1546,6 +1578,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
         DIAG_T(t_shade);
         bool fin = false;                    // lane wrote its pixel in this step
         if (has && !T.tracing) {
+            load_path();
             rays++;
             bool path_done;
             f3 no = T.wr.o, nd = T.wr.d;                                     // next segment
@@ -1598,7 +1631,10 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     fin = true;
                 }
             }
-            if (has) trav_init(T, root, no, nd);
+            if (has) {
+                trav_init(T, root, no, nd);
+                save_path();
+            }
         }
         if (RT_UNIT_COST_DEFER) {
             if (track && fin) {
