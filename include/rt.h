@@ -322,7 +322,7 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "rebuild"   : RT_BUILD_LBVH only: 1 = rebuild every BLAS on the GPU every frame (default 0)
  *   "timeline"  : 1 = record a per-wave timeline of each persistent launch (debug)
  *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal steps (debug)
- *   "tlas_leaf" : RT_BUILD_SAH: instances per leaf of the per-frame TLAS (1..4, default 1)
+ *   "tlas_leaf" : instances per leaf of the per-frame TLAS (1..4, default 1; GPU-built TLASes: set before rt_scene_build)
  *   "blas_leaf" : RT_BUILD_SAH: primitives per BLAS leaf (1..4, default 4; set before rt_scene_build)
  *   "gpu_tlas"  : RT_BUILD_SAH: 1 = keep the host-built SAH BLASes but compute the instance records and
  *                 build the TLAS on the GPU every frame, as RT_BUILD_LBVH does (only changed instances

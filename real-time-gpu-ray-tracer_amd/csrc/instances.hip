@@ -58,7 +58,27 @@ __global__ __launch_bounds__(256) void instance_update_kernel(const InstParams *
     tcent[i] = make_float4(tc.x, tc.y, tc.z, 0.0f);
 }
 
+// GPU-built TLAS: the instance records copied into TLAS leaf-slot order (record j = the instance in slot
+// j), so entering a TLAS leaf reads its InstHot directly instead of through tlas_slots first
+__global__ __launch_bounds__(256) void slot_order_kernel(const uint32_t *__restrict__ slots, const InstHot *__restrict__ hot,
+                                                         const InstCold *__restrict__ cold, uint32_t n,
+                                                         InstHot *__restrict__ hot_s, InstCold *__restrict__ cold_s) {
+    const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t i = slots[j];
+    if (i >= n) return;
+    hot_s[j] = hot[i];
+    cold_s[j] = cold[i];
+}
+
 }  // namespace
+
+hipError_t launch_instance_slot_order(const uint32_t *slots, const InstHot *hot, const InstCold *cold, uint32_t n,
+                                      InstHot *hot_s, InstCold *cold_s, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(slot_order_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, slots, hot, cold, n, hot_s, cold_s);
+    return hipGetLastError();
+}
 
 // deltas: `count` changed instances (device memory: the uploaded part of the frame block)
 hipError_t launch_instance_update(const InstDelta *deltas, uint32_t count, InstParams *params, uint32_t n, InstHot *hot,

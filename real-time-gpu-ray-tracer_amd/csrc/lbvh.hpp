@@ -91,6 +91,9 @@ private:
     LbvhSeg *segs_ = nullptr;
     uint32_t *seg_of_ = nullptr;          // item -> segment
     float *box_ = nullptr;                // 6 floats per item (owned or caller's)
+public:
+    bool size_classes_ = false;           // TLAS: size class above the Morton code (morton_kernel)
+private:
     float4 *cent_ = nullptr;
     float *own_box_ = nullptr;
     float4 *own_cent_ = nullptr;

@@ -41,6 +41,8 @@ hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint3
                            uint32_t, void *, const void *, size_t, unsigned long long *, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean, bool wide);
 hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, const uint32_t *, uint32_t, hipStream_t);
+hipError_t launch_instance_slot_order(const uint32_t *, const InstHot *, const InstCold *, uint32_t, InstHot *, InstCold *,
+                                      hipStream_t);
 hipError_t launch_instance_update(const InstDelta *, uint32_t, InstParams *, uint32_t, InstHot *, InstCold *, float *, float4 *,
                                   hipStream_t);
 uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean, bool wide);
@@ -73,7 +75,8 @@ constexpr uint32_t BLAS_LEAF_CAP = 4;   // BLAS.cuh:17
 constexpr uint32_t TLAS_LEAF_CAP = 2;   // TLAS.cuh:22
 constexpr uint32_t SAH_LEAF_CAP = 4;    // RT_BUILD_SAH: <= 4 items per leaf (2-bit count in a leaf ref)
 constexpr uint32_t LBVH_BLAS_LEAF_CAP = 4;
-constexpr uint32_t LBVH_TLAS_LEAF_CAP = 2;   // the reference's TLAS leaf size (TLAS.cuh:22)
+// GPU TLAS leaves hold up to option "tlas_leaf" instances (default 1, as the SAH TLAS: a leaf's
+// instances are entered without their own box test; 2 = the reference's TLAS leaf size, TLAS.cuh:22)
 
 struct InstState {
     uint32_t ptype, pindex, pcount, blas;
@@ -156,7 +159,7 @@ struct rt_scene {
     //   [tlas root | tlas pairs | tlas slots | inst hot | inst cold | tlas item boxes | tlas item centroids]
     // (the root and the item arrays are used by GPU-built TLASes only)
     size_t frame_block = 0, off_root = 0, off_pairs = 0, off_slots = 0, off_hot = 0, off_cold = 0, off_tbox = 0,
-           off_tcent = 0, off_root_wide = 0, off_quads = 0, off_delta = 0;
+           off_tcent = 0, off_root_wide = 0, off_quads = 0, off_delta = 0, off_hot_s = 0, off_cold_s = 0;
     // GPU-built frames: per-instance parameters resident in HBM (instances.hip); the host stages a delta
     // (InstDelta at off_delta) only for instances whose transform or local box changed
     DevBuf<InstParams> inst_params;
@@ -262,6 +265,7 @@ struct rt_scene {
     bool blas_dirty = false;            // rt_scene_update_triangles since the last BLAS build
     uint64_t blas_builds = 0;
     hipEvent_t ev_render_done = nullptr;   // last trace launch finished (BLAS rebuilds wait on it)
+    bool tlas_size_classes = true;      // option "tlas_classes": GPU TLAS keys start with an item size class
     bool gpu_tlas_sah = false;          // option "gpu_tlas" (set before the build): RT_BUILD_SAH BLASes, per-frame TLAS on the GPU
     DevBuf<uint32_t> blas_wide_refs;    // host-built BLASes under a GPU TLAS: quad root ref per BLAS
     // instance records + TLAS built by kernels each frame: RT_BUILD_LBVH, or RT_BUILD_SAH with "gpu_tlas"
@@ -407,7 +411,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
     InstHot *hot = reinterpret_cast<InstHot *>(st + s->off_hot);
     InstCold *cold = reinterpret_cast<InstCold *>(st + s->off_cold);
     if (s->gpu_tlas()) {
-        s->block_by_slot[b] = false;                  // GPU-built TLASes keep instance order
+        s->block_by_slot[b] = false;                  // until the slot-order copy below
         // only the changed instances cross PCIe: (index, shift, cos / sin of the angles, scale, local box)
         InstDelta *dl = reinterpret_cast<InstDelta *>(st + s->off_delta);
         uint32_t nd = 0;
@@ -455,6 +459,14 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
                                                reinterpret_cast<NodeQuad *>(fd + s->off_quads),
                                                reinterpret_cast<TreeRoot *>(fd + s->off_root_wide), s->stream));
         HIP_TRY(s->tlas_builder->gather_items(reinterpret_cast<uint32_t *>(fd + s->off_slots), s->stream));
+        if (s->inst_by_slot) {
+            HIP_TRY(launch_instance_slot_order(reinterpret_cast<const uint32_t *>(fd + s->off_slots),
+                                               reinterpret_cast<const InstHot *>(fd + s->off_hot),
+                                               reinterpret_cast<const InstCold *>(fd + s->off_cold), n,
+                                               reinterpret_cast<InstHot *>(fd + s->off_hot_s),
+                                               reinterpret_cast<InstCold *>(fd + s->off_cold_s), s->stream));
+            s->block_by_slot[b] = true;
+        }
         HIP_TRY(hipEventRecord(s->ev_copied[b], s->stream));
         s->active = b;
         s->frame = frame;
@@ -518,8 +530,9 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.blas_quads = s->blas_quads.p;
     g.wide = s->wide && s->blas_quads.p != nullptr ? 1u : 0u;   // GPU-built trees: quads from collapse_wide
     g.tlas_slots = reinterpret_cast<const uint32_t *>(s->frame_dev[b] + s->off_slots);
-    g.inst_hot = reinterpret_cast<const InstHot *>(s->frame_dev[b] + s->off_hot);
-    g.inst_cold = reinterpret_cast<const InstCold *>(s->frame_dev[b] + s->off_cold);
+    const bool gpu_slots = s->gpu_tlas() && s->block_by_slot[b];   // the slot-ordered copies of GPU-built frames
+    g.inst_hot = reinterpret_cast<const InstHot *>(s->frame_dev[b] + (gpu_slots ? s->off_hot_s : s->off_hot));
+    g.inst_cold = reinterpret_cast<const InstCold *>(s->frame_dev[b] + (gpu_slots ? s->off_cold_s : s->off_cold));
     g.inst_by_slot = s->block_by_slot[b] ? 1u : 0u;   // how frame block b's instance records were staged
     g.tri_hot = s->tri_hot.p; g.tri_cold = s->tri_cold.p;
     g.sph_hot = s->sph_hot.p; g.sph_cold = s->sph_cold.p;
@@ -842,6 +855,11 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     s->off_quads = (s->off_tcent + n * 4 * sizeof(float) + 127) & ~size_t(127);
     s->off_delta = align16(s->off_quads + n * sizeof(NodeQuad));   // <= n - 1 quads
     s->frame_block = s->off_delta + (s->gpu_tlas() ? n * sizeof(InstDelta) : 0);
+    if (s->gpu_tlas()) {       // GPU-built TLAS: the instance records again, in TLAS leaf-slot order
+        s->off_hot_s = align16(s->frame_block);
+        s->off_cold_s = align16(s->off_hot_s + n * sizeof(InstHot));
+        s->frame_block = s->off_cold_s + n * sizeof(InstCold);
+    }
     if (s->gpu_tlas() && mode == RT_BUILD_SAH) {
         // host-built BLASes under the GPU TLAS: their roots (box, pair ref, quad ref) and the instance map
         std::vector<TreeRoot> roots(s->blas.size());
@@ -863,8 +881,9 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         s->inst_dirty.assign(n, 1);                                 // frame 0 uploads every instance
         delete s->tlas_builder;
         s->tlas_builder = new LbvhBuilder();
-        const std::vector<LbvhSeg> tseg{LbvhSeg{0u, (uint32_t)n, 0u, 0u, 0u, 0u, LBVH_TLAS_LEAF_CAP, 0u}};
+        const std::vector<LbvhSeg> tseg{LbvhSeg{0u, (uint32_t)n, 0u, 0u, 0u, 0u, s->tlas_leaf, 0u}};
         HIP_TRY(s->tlas_builder->init(tseg, s->stream));
+        s->tlas_builder->size_classes_ = s->tlas_size_classes;
     }
     for (int b = 0; b < rt_scene::NLANE; b++) {
         if (s->staging[b]) { (void)hipHostFree(s->staging[b]); s->staging[b] = nullptr; }
@@ -1390,6 +1409,10 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "wide") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "wide must be 0 or 1");
         s->wide = value == 1;
+    } else if (k == "tlas_classes") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_classes must be 0 or 1");
+        s->tlas_size_classes = value == 1;
+        if (s->tlas_builder) s->tlas_builder->size_classes_ = s->tlas_size_classes;
     } else if (k == "gpu_tlas") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "gpu_tlas must be 0 or 1");
         if (s->built) return fail(RT_ERR_UNSUPPORTED, "gpu_tlas is set before rt_scene_build");
