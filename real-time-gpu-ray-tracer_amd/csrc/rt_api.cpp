@@ -265,7 +265,7 @@ struct rt_scene {
     bool blas_dirty = false;            // rt_scene_update_triangles since the last BLAS build
     uint64_t blas_builds = 0;
     hipEvent_t ev_render_done = nullptr;   // last trace launch finished (BLAS rebuilds wait on it)
-    bool tlas_size_classes = true;      // option "tlas_classes": GPU TLAS keys start with an item size class
+    bool tlas_size_classes = false;     // option "tlas_classes": GPU TLAS keys start with an item size class (measured neutral)
     bool gpu_tlas_sah = false;          // option "gpu_tlas" (set before the build): RT_BUILD_SAH BLASes, per-frame TLAS on the GPU
     DevBuf<uint32_t> blas_wide_refs;    // host-built BLASes under a GPU TLAS: quad root ref per BLAS
     // instance records + TLAS built by kernels each frame: RT_BUILD_LBVH, or RT_BUILD_SAH with "gpu_tlas"
