@@ -331,7 +331,10 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 (default 1; 0 = instance order, for A/B — results are identical)
  *   "reserve"   : with "overlap", the persistent grid leaves this many workgroup slots free (default 16, two
  *                 per XCD) so the next lanes' schedule / upload / GPU TLAS kernels start beside the running launch
- *   "overlap"   : L = consecutive rt_render calls cycle through L (2..4) internal lanes (work-queue
+ *   "lds_scene" : FAST quad-tree kernel: 1 = every workgroup copies the frame's TLAS quads and, when they fit
+ *                 as well, the instance hot records into 16 KB of LDS and reads them there (default 1;
+ *                 results identical)
+ *   "overlap"   : L = consecutive rt_render calls cycle through L (2..8) internal lanes (work-queue
  *                 heads, unit costs, schedule); a launch waits only for the previous launch of its own
  *                 lane and for its frame block, so a caller that cycles L streams runs frame
  *                 k+1's launch in the CUs frame k's tail leaves idle.  The caller orders its own output

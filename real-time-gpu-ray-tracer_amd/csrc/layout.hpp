@@ -169,7 +169,14 @@ struct SceneGPU {
     uint32_t instance_count;
     uint32_t rough_count;           // material slot of metal m = rough_count + m
     uint32_t material_count;        // slots in `materials` (roughs + metals)
+    // option "lds_scene" (FAST persistent kernel, quad trees): the frame's TLAS quads (7 dwordx4 each, the
+    // pad dropped) and then, if they fit as well, the instance hot records (5 dwordx4 each) are copied into
+    // LDS_SCENE_F4 dwordx4 of LDS at the start of every workgroup; 0 = read from HBM
+    uint32_t lds_quads;             // TLAS quads in LDS (every TLAS interior ref indexes below it)
+    uint32_t lds_insts;             // instance hot records in LDS (0 or instance_count)
 };
+constexpr uint32_t LDS_SCENE_F4 = 1024;    // 16 KB per workgroup: 36 + 16 KB keeps 3 workgroups per CU (160 KB)
+constexpr uint32_t LDS_QUAD_F4 = 7, LDS_INST_F4 = 5;
 
 struct CameraGPU {                  // Camera (RendererImpl.cuh:32-61), precomputed on host
     float pixel_origin[3];

@@ -106,7 +106,7 @@ struct DevBuf {
 // rt_scene_attach_comm: this scene is rank `rank` of a `world`-rank frame.  One communicator
 // per overlap lane (split from the first), so the lanes' gathers on different streams never share one.
 struct CommState {
-    static constexpr int NLANE = 4;
+    static constexpr int NLANE = 8;
     int rank = 0, world = 1;
     uint32_t tile_w = 64, tile_h = 64;
     ncclComm_t comm[NLANE] = {};
@@ -145,6 +145,7 @@ struct rt_scene {
     DevBuf<NodePair> blas_pairs;
     DevBuf<NodeQuad> blas_quads;    // option "wide"
     bool wide = true;               // FAST persistent kernel traverses the quad trees (host-built modes)
+    bool lds_scene = true;          // quad-tree kernel: TLAS quads (+ instance hot records) in LDS when they fit
     uint32_t wide_merge = 0;        // quad trees: binary subtrees of <= wide_merge items become one leaf (set before build)
     DevBuf<TriHot> tri_hot;
     DevBuf<TriCold> tri_cold;
@@ -165,7 +166,7 @@ struct rt_scene {
     DevBuf<InstParams> inst_params;
     std::vector<uint8_t> inst_dirty;
     // frame blocks cycle through NLANE buffers, so "overlap" lanes never wait on each other's block
-    static constexpr int NLANE = 4;
+    static constexpr int NLANE = 8;
     uint8_t *staging[NLANE] = {};                 // pinned host
     uint8_t *staging_dev[NLANE] = {};             // the same, as device-visible pointers
     int pending_copy = -1;                        // rt_render: block whose upload the next launch performs
@@ -541,6 +542,16 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.instance_count = (uint32_t)s->inst.size();
     g.rough_count = (uint32_t)s->roughs.size();
     g.material_count = (uint32_t)(s->materials.n / 4);
+    // option "lds_scene": the quads the frame's TLAS refs can index (host-built: this frame's quad count;
+    // GPU-built: quad q is rooted at pair q, < n - 1) and, if they fit too, the instance hot records
+    if (s->lds_scene && g.wide) {
+        const uint32_t n = g.instance_count;
+        const uint32_t nq = s->gpu_tlas() ? (n > 1 ? n - 1 : 0) : (uint32_t)s->tlas_wide.quads.size();
+        if (nq > 0 && nq * LDS_QUAD_F4 <= LDS_SCENE_F4) {
+            g.lds_quads = nq;
+            if (nq * LDS_QUAD_F4 + n * LDS_INST_F4 <= LDS_SCENE_F4) g.lds_insts = n;
+        }
+    }
     return g;
 }
 
@@ -1406,6 +1417,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "costmap") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
         s->costmap_on = value == 1;
+    } else if (k == "lds_scene") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "lds_scene must be 0 or 1");
+        s->lds_scene = value == 1;
     } else if (k == "wide") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "wide must be 0 or 1");
         s->wide = value == 1;
@@ -1434,7 +1448,7 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         HIP_TRY(drain(s));
         s->inst_by_slot = value == 1;            // takes effect with the next frame's staging
     } else if (k == "overlap") {
-        if (value < 0 || value > rt_scene::NLANE) return fail(RT_ERR_INVALID_ARGUMENT, "overlap must be 0..4 lanes");
+        if (value < 0 || value > rt_scene::NLANE) return fail(RT_ERR_INVALID_ARGUMENT, "overlap must be 0..8 lanes");
         HIP_TRY(drain(s));
         s->lanes = value < 1 ? 1u : (uint32_t)value;
         s->overlap = s->lanes > 1;

@@ -527,6 +527,36 @@ __device__ __forceinline__ void pop_next(Trav &T, const SEnt *spill) {
 // Quad node (option "wide"): 4 slab tests on SoA bounds, hits sorted by entry t; the nearest is visited
 // next and the others are pushed farthest first (popped nearest first).  Not the reference's visit
 // order (FAST tolerance): the closest hit only differs on ties within the 1e-6 window.
+// Option "lds_scene" (SceneGPU::lds_quads / lds_insts): the frame's TLAS quads and instance hot records,
+// copied into LDS by every workgroup of the persistent quad-tree kernel at its start.  On C2 an average
+// ray visits ~1.6 quads (mostly TLAS) and enters ~1 instance, so most of its dependent loads are these.
+__shared__ float4 lds_scene[LDS_SCENE_F4];
+
+struct InstRec { float4 i0, i1, i2, box01, box2ref; };   // InstHot as 5 dwordx4 (inv rows, root box, refs)
+template <bool LDSS>
+__device__ __forceinline__ InstRec load_inst(const SceneGPU &sc, uint32_t i) {
+    InstRec r;
+    if (LDSS && sc.lds_insts) {
+        const float4 *p = lds_scene + sc.lds_quads * LDS_QUAD_F4 + i * LDS_INST_F4;
+        r.i0 = p[0]; r.i1 = p[1]; r.i2 = p[2]; r.box01 = p[3]; r.box2ref = p[4];
+    } else {
+        const float4 *p = reinterpret_cast<const float4 *>(sc.inst_hot + i);
+        r.i0 = p[0]; r.i1 = p[1]; r.i2 = p[2]; r.box01 = p[3]; r.box2ref = p[4];
+    }
+    return r;
+}
+// the workgroup's copy (before the kernel's first barrier)
+__device__ __forceinline__ void lds_scene_fill(const SceneGPU &sc) {
+    const uint32_t nq = sc.lds_quads * LDS_QUAD_F4, ni = sc.lds_insts * LDS_INST_F4;
+    const float4 *q = reinterpret_cast<const float4 *>(sc.tlas_quads);
+    for (uint32_t i = threadIdx.x; i < nq; i += BLOCK) {
+        const uint32_t k = i / LDS_QUAD_F4, j = i - k * LDS_QUAD_F4;
+        lds_scene[i] = q[k * 8 + j];
+    }
+    const float4 *h = reinterpret_cast<const float4 *>(sc.inst_hot);
+    for (uint32_t i = threadIdx.x; i < ni; i += BLOCK) lds_scene[nq + i] = h[i];
+}
+
 __device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float oinv, float4 &tn, float4 &tf) {
     const float a0 = fmaf(lo.x, inv, -oinv), b0 = fmaf(hi.x, inv, -oinv);
     const float a1 = fmaf(lo.y, inv, -oinv), b1 = fmaf(hi.y, inv, -oinv);
@@ -545,9 +575,18 @@ template <bool COUNT>
 __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
     const uint32_t cur = T.cur;
     const bool blas = (cur & REF_BLAS) != 0;
-    const float4 *Q = reinterpret_cast<const float4 *>((blas ? sc.blas_quads : sc.tlas_quads) + (cur & REF_INDEX_MASK));
-    const float4 lx = Q[0], hx = Q[1], ly = Q[2], hy = Q[3], lz = Q[4], hz = Q[5];
-    const uint4 R = reinterpret_cast<const uint4 *>(Q)[6];
+    float4 lx, hx, ly, hy, lz, hz;
+    uint4 R;
+    if (!blas && sc.lds_quads) {
+        const float4 *Q = lds_scene + (cur & REF_INDEX_MASK) * LDS_QUAD_F4;
+        lx = Q[0]; hx = Q[1]; ly = Q[2]; hy = Q[3]; lz = Q[4]; hz = Q[5];
+        const float4 r = Q[6];
+        R = make_uint4(__float_as_uint(r.x), __float_as_uint(r.y), __float_as_uint(r.z), __float_as_uint(r.w));
+    } else {
+        const float4 *Q = reinterpret_cast<const float4 *>((blas ? sc.blas_quads : sc.tlas_quads) + (cur & REF_INDEX_MASK));
+        lx = Q[0]; hx = Q[1]; ly = Q[2]; hy = Q[3]; lz = Q[4]; hz = Q[5];
+        R = reinterpret_cast<const uint4 *>(Q)[6];
+    }
     if (COUNT) cnt.pairs += 2;                       // 4 child boxes = 2 node-pair equivalents
     const RayP &r = blas ? T.lr : T.wr;
     float t[4];
@@ -658,14 +697,29 @@ __device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEn
         if (T.cur != REF_NONE) stack_push(T.stk, spill, T.cur, T.curT, cnt);
         if (count > 1) stack_push(T.stk, spill, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
         T.cur_inst = sc.inst_by_slot ? start : sc.tlas_slots[start];
-        const InstHot &I = sc.inst_hot[T.cur_inst];
         if (COUNT) cnt.inst++;
-        T.lr.o = xf_point(I.inv, T.wr.o);                      // Instance.cu:26-27
-        T.lr.d = xf_vector(I.inv, T.wr.d);
-        prep(T.lr);
         float te = 0.0f;
-        if (slab(I.root_box, T.lr, TMIN, T.tmax, te)) { T.cur = WIDE ? I.root_ref_wide : I.root_ref; T.curT = te; }
-        else pop_next(T, spill);
+#if !RT_EXACT
+        if (WIDE) {
+            const InstRec I = load_inst<true>(sc, T.cur_inst);
+            const float inv[12] = {I.i0.x, I.i0.y, I.i0.z, I.i0.w, I.i1.x, I.i1.y, I.i1.z, I.i1.w,
+                                   I.i2.x, I.i2.y, I.i2.z, I.i2.w};
+            const float box[6] = {I.box01.x, I.box01.y, I.box01.z, I.box01.w, I.box2ref.x, I.box2ref.y};
+            T.lr.o = xf_point(inv, T.wr.o);                    // Instance.cu:26-27
+            T.lr.d = xf_vector(inv, T.wr.d);
+            prep(T.lr);
+            if (slab(box, T.lr, TMIN, T.tmax, te)) { T.cur = __float_as_uint(I.box2ref.w); T.curT = te; }
+            else pop_next(T, spill);
+        } else
+#endif
+        {
+            const InstHot &I = sc.inst_hot[T.cur_inst];
+            T.lr.o = xf_point(I.inv, T.wr.o);                      // Instance.cu:26-27
+            T.lr.d = xf_vector(I.inv, T.wr.d);
+            prep(T.lr);
+            if (slab(I.root_box, T.lr, TMIN, T.tmax, te)) { T.cur = WIDE ? I.root_ref_wide : I.root_ref; T.curT = te; }
+            else pop_next(T, spill);
+        }
     } else {
         const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf), type = ref_leaf_type(leaf);
         if (type == RT_PRIM_TRIANGLE) {
@@ -1126,10 +1180,22 @@ struct Surface { f3 p, n; uint32_t material; uint32_t orig; };
 
 // Recompute the hit point / normal of the closest hit exactly as the primitive hit function and
 // Instance::hit (Instance.cu:41-45) would have stored them.
+template <bool LDSS = false>
 __device__ __forceinline__ Surface finalize(const SceneGPU &sc, const f3 &wo, const f3 &wd, const Hit &h) {
-    const InstHot &I = sc.inst_hot[h.inst];
     const InstCold &IC = sc.inst_cold[h.inst];
-    const f3 lo = xf_point(I.inv, wo), ld = xf_vector(I.inv, wd);
+    f3 lo, ld;
+#if !RT_EXACT
+    if (LDSS) {
+        const InstRec I = load_inst<true>(sc, h.inst);
+        const float inv[12] = {I.i0.x, I.i0.y, I.i0.z, I.i0.w, I.i1.x, I.i1.y, I.i1.z, I.i1.w,
+                               I.i2.x, I.i2.y, I.i2.z, I.i2.w};
+        lo = xf_point(inv, wo); ld = xf_vector(inv, wd);
+    } else
+#endif
+    {
+        const InstHot &I = sc.inst_hot[h.inst];
+        lo = xf_point(I.inv, wo); ld = xf_vector(I.inv, wd);
+    }
     const f3 p = add(lo, scl(ld, h.t));                                        // Ray::at (Ray.cuh:18-20)
     f3 n;
     Surface s;
@@ -1397,6 +1463,9 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     const int lane = tid & 63;
     const bool mat_lds = sc.material_count <= LDS_MATERIALS;
     if (mat_lds && tid < (int)sc.material_count) lds_mat[tid] = reinterpret_cast<const float4 *>(sc.materials)[tid];
+#if !RT_EXACT
+    if constexpr (WIDE) lds_scene_fill(sc);
+#endif
     __syncthreads();                              // once, before any wave leaves for the queue
     const TreeRoot root = uniform_root<WIDE>(sc);
 
@@ -1584,7 +1653,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             f3 no = T.wr.o, nd = T.wr.d;                                     // next segment
             if (T.found) {
                 if (COUNT) cnt.hits++;
-                const Surface s = finalize(sc, T.wr.o, T.wr.d, T.hit);
+                const Surface s = finalize<WIDE>(sc, T.wr.o, T.wr.d, T.hit);
                 DIAG_WAIT_VM();
                 DIAG_T(t_hit);
                 const uint32_t mi = s.material & ~MAT_METAL_BIT;

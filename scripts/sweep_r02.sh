@@ -9,10 +9,28 @@ one() {  # out args...
   timeout -k 10 240 python bench.py --no-cpu-baseline "$@" > gpurun_out/_one.log 2>&1
   local rc=$?
   if [ $rc -ne 0 ]; then echo "rc=$rc for $*"; tail -3 gpurun_out/_one.log; exit $rc; fi
-  tail -1 gpurun_out/_one.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'args': '$*', 'value': d['value'], 'ms_per_step': d['ms_per_step'], 'kernel_ms': d['kernel_ms'], 'kernel_ms_overlapped': d['kernel_ms_overlapped'], 'lat': d['frame_latency_ms_median'], 'host_update_ms': d.get('host_update_ms_median'), 'host_wait_ms': d.get('host_update_wait_ms_median')}))" | tee -a "gpurun_out/$out"
+  tail -1 gpurun_out/_one.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'args': '$*', 'hwq': '${GPU_MAX_HW_QUEUES:-}', 'value': d['value'], 'ms_per_step': d['ms_per_step'], 'kernel_ms': d['kernel_ms'], 'kernel_ms_overlapped': d['kernel_ms_overlapped'], 'lat': d['frame_latency_ms_median'], 'host_update_ms': d.get('host_update_ms_median'), 'host_wait_ms': d.get('host_update_wait_ms_median')}))" | tee -a "gpurun_out/$out"
 }
 if [[ $WHAT == lanes || $WHAT == all ]]; then
   for rep in 1 2; do for L in 2 3 4; do for rs in 0 8 16; do one sweep_lanes.jsonl --overlap $L --opt reserve=$rs; done; done; done
+fi
+if [[ $WHAT == queues ]]; then
+  # hardware queues per process (GPU_MAX_HW_QUEUES, HIP default 4) x overlap lanes: full C2 frame and 1/8 shares
+  for rep in 1; do for hq in 4 8; do for L in 3 4 6 8; do
+    GPU_MAX_HW_QUEUES=$hq one sweep_queues.jsonl --overlap $L --steps 200
+    GPU_MAX_HW_QUEUES=$hq one sweep_queues.jsonl --overlap $L --steps 200 --shard 4/8
+    GPU_MAX_HW_QUEUES=$hq one sweep_queues.jsonl --overlap $L --steps 200 --config C4 --shard 3/8
+  done; done; done
+fi
+if [[ $WHAT == lds ]]; then
+  # option "lds_scene": TLAS quads + instance hot records in LDS (1) vs HBM (0), alternating
+  for rep in 1 2; do for v in 0 1; do
+    one sweep_lds.jsonl --opt lds_scene=$v
+    one sweep_lds.jsonl --opt lds_scene=$v --shard 4/8
+    one sweep_lds.jsonl --opt lds_scene=$v --config C4 --shard 3/8
+    one sweep_lds.jsonl --opt lds_scene=$v --config C3
+    one sweep_lds.jsonl --opt lds_scene=$v --build lbvh
+  done; done
 fi
 if [[ $WHAT == thr || $WHAT == all ]]; then
   for t in 24 32 40 48; do one sweep_thr.jsonl --threshold $t ${THR_ARGS:-}; done

@@ -403,6 +403,24 @@ def test_reorder_period_byte_identical(gpu_lib, period, lanes):
         assert np.array_equal(bufs[f].cpu().numpy().reshape(H, W, 4), ref[f]), f
 
 
+@pytest.mark.parametrize("mode,particles", [("sah", 10), ("lbvh", 10), ("sah", 254)])
+def test_lds_scene_byte_identical(gpu_lib, mode, particles):
+    """Option "lds_scene": the TLAS quads (and, when they fit as well, the instance hot records) are read
+    from each workgroup's LDS copy instead of HBM.  Same operands, same order: frames are byte-identical
+    with it off, on several animated frames (the TLAS changes every frame).  254 particles: the C3 scene,
+    where only the TLAS quads fit."""
+    s = scenes.demo_with_particles(particles)
+    W, H = 320, 180
+    r = Renderer(s).build_acceleration_structure(0, mode=mode).configure_camera(W, H, ray_trace_depth=2)
+    r.set_option("lds_scene", 0)
+    ref = [r.render(f, count_work=True) for f in range(3)]
+    r.set_option("lds_scene", 1)
+    for f in range(3):
+        img, _, st = r.render(f, count_work=True)
+        assert np.array_equal(img, ref[f][0]), f
+        assert st["rays"] == ref[f][2]["rays"] and st["triangle_tests"] == ref[f][2]["triangle_tests"]
+
+
 @pytest.mark.parametrize("tiles,nl,mode", [(None, 2, "sah"), ((64, 64, 1, 3), 2, "sah"), (None, 3, "sah"),
                                            ((64, 64, 0, 2), 4, "sah"), (None, 2, "lbvh"), (None, 3, "lbvh-rebuild")])
 def test_overlap_lanes_byte_identical(gpu_lib, tiles, nl, mode):
