@@ -331,6 +331,8 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 (default 1; 0 = instance order, for A/B — results are identical)
  *   "reserve"   : with "overlap", the persistent grid leaves this many workgroup slots free (default 16, two
  *                 per XCD) so the next lanes' schedule / upload / GPU TLAS kernels start beside the running launch
+ *   "grid_pct"  : persistent grid as a percentage of the resident workgroup capacity (1..100; default 0 = auto:
+ *                 100 for serialised launches, 50 with "overlap", so two lanes' launches run side by side)
  *   "lds_scene" : FAST quad-tree kernel: 1 = every workgroup copies the frame's TLAS quads and, when they fit
  *                 as well, the instance hot records into 16 KB of LDS and reads them there (default 1;
  *                 results identical)

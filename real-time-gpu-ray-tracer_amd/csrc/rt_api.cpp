@@ -145,7 +145,12 @@ struct rt_scene {
     DevBuf<NodePair> blas_pairs;
     DevBuf<NodeQuad> blas_quads;    // option "wide"
     bool wide = true;               // FAST persistent kernel traverses the quad trees (host-built modes)
-    bool lds_scene = true;          // quad-tree kernel: TLAS quads (+ instance hot records) in LDS when they fit
+    bool lds_scene = true;
+    // option "grid_pct": the persistent grid as a percentage of the resident capacity; 0 = auto: 100 for
+    // serialised launches, 50 with "overlap", so two lanes' launches are resident side by side instead of
+    // the next one filling only the slots the previous one's tail frees (C2, 3 lanes: 0.252 -> 0.229
+    // ms/frame; a C2 1/8 share 0.115 -> 0.084; C3 1.64 -> 1.59, profiles/r02_sweep_grid2.jsonl)
+    uint32_t grid_pct = 0;          // quad-tree kernel: TLAS quads (+ instance hot records) in LDS when they fit
     uint32_t wide_merge = 0;        // quad trees: binary subtrees of <= wide_merge items become one leaf (set before build)
     DevBuf<TriHot> tri_hot;
     DevBuf<TriCold> tri_cold;
@@ -1283,7 +1288,9 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     if (s->use_persistent) {
         const uint32_t cap = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false, false)
                                              : persistent_blocks_per_cu_fast(s->variant, lean, g.wide != 0));
-        const uint32_t blocks = s->overlap && cap > 2 * s->reserve ? cap - s->reserve : cap;
+        uint32_t blocks = s->overlap && cap > 2 * s->reserve ? cap - s->reserve : cap;
+        const uint32_t pct = s->grid_pct ? s->grid_pct : (s->overlap ? 50u : 100u);
+        if (pct < 100) blocks = std::max<uint32_t>(8u, blocks * pct / 100u);
         HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, lane_counters, s->queue[q], blocks, s->threshold,
                                                        s->variant, false, reset_queue, stream)
                       : launch_render_persistent_fast(g, cam, out, count, lane_counters, s->queue[q], blocks, s->threshold,
@@ -1417,6 +1424,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "costmap") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
         s->costmap_on = value == 1;
+    } else if (k == "grid_pct") {
+        if (value < 0 || value > 100) return fail(RT_ERR_INVALID_ARGUMENT, "grid_pct must be in 0..100 (0 = auto)");
+        s->grid_pct = (uint32_t)value;
     } else if (k == "lds_scene") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "lds_scene must be 0 or 1");
         s->lds_scene = value == 1;

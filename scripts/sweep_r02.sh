@@ -22,6 +22,24 @@ if [[ $WHAT == queues ]]; then
     GPU_MAX_HW_QUEUES=$hq one sweep_queues.jsonl --overlap $L --steps 200 --config C4 --shard 3/8
   done; done; done
 fi
+if [[ $WHAT == grid ]]; then
+  # option "grid_pct": each overlapped launch takes only part of the GPU, so more than two lanes' launches
+  # run side by side (hardware queues raised to 8 so every lane has its own)
+  for lp in 3:100 3:50 4:50 6:35 6:50 8:25 8:35; do L=${lp%:*}; P=${lp#*:}
+    GPU_MAX_HW_QUEUES=8 one sweep_grid.jsonl --overlap $L --opt grid_pct=$P --steps 200 --shard 4/8
+    GPU_MAX_HW_QUEUES=8 one sweep_grid.jsonl --overlap $L --opt grid_pct=$P --steps 200 --config C4 --shard 3/8
+    GPU_MAX_HW_QUEUES=8 one sweep_grid.jsonl --overlap $L --opt grid_pct=$P --steps 200
+  done
+fi
+if [[ $WHAT == grid2 ]]; then
+  # finer grid_pct x lanes at the default 4 hardware queues; the full C2 frame is the bench line
+  for rep in 1 2; do for lp in 3:100 3:50 3:60 3:67 4:34 4:50 4:60 5:40; do L=${lp%:*}; P=${lp#*:}
+    one sweep_grid2.jsonl --overlap $L --opt grid_pct=$P --steps 200
+    one sweep_grid2.jsonl --overlap $L --opt grid_pct=$P --steps 200 --shard 4/8
+    one sweep_grid2.jsonl --overlap $L --opt grid_pct=$P --steps 200 --config C4 --shard 3/8
+  done; done
+  for lp in 3:100 3:50 4:50; do L=${lp%:*}; P=${lp#*:}; one sweep_grid2.jsonl --overlap $L --opt grid_pct=$P --config C3; done
+fi
 if [[ $WHAT == lds ]]; then
   # option "lds_scene": TLAS quads + instance hot records in LDS (1) vs HBM (0), alternating
   for rep in 1 2; do for v in 0 1; do
