@@ -146,10 +146,11 @@ struct rt_scene {
     DevBuf<NodeQuad> blas_quads;    // option "wide"
     bool wide = true;               // FAST persistent kernel traverses the quad trees (host-built modes)
     bool lds_scene = true;
-    // option "grid_pct": the persistent grid as a percentage of the resident capacity; 0 = auto: 100 for
-    // serialised launches, 50 with "overlap", so two lanes' launches are resident side by side instead of
-    // the next one filling only the slots the previous one's tail frees (C2, 3 lanes: 0.252 -> 0.229
-    // ms/frame; a C2 1/8 share 0.115 -> 0.084; C3 1.64 -> 1.59, profiles/r02_sweep_grid2.jsonl)
+    // option "grid_pct": the persistent grid as a percentage of the resident capacity; 0 = auto: 50 when
+    // another lane's launch is still in flight ("overlap"), so two lanes' launches are resident side by
+    // side instead of the next one filling only the slots the previous one's tail frees (C2, 3 lanes:
+    // 0.252 -> 0.229 ms/frame; a C2 1/8 share 0.115 -> 0.084; C3 1.64 -> 1.59,
+    // profiles/r02_sweep_grid2.jsonl), else 100 (a frame alone on the GPU takes all of it)
     uint32_t grid_pct = 0;          // quad-tree kernel: TLAS quads (+ instance hot records) in LDS when they fit
     uint32_t wide_merge = 0;        // quad trees: binary subtrees of <= wide_merge items become one leaf (set before build)
     DevBuf<TriHot> tri_hot;
@@ -1289,7 +1290,13 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         const uint32_t cap = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false, false)
                                              : persistent_blocks_per_cu_fast(s->variant, lean, g.wide != 0));
         uint32_t blocks = s->overlap && cap > 2 * s->reserve ? cap - s->reserve : cap;
-        const uint32_t pct = s->grid_pct ? s->grid_pct : (s->overlap ? 50u : 100u);
+        uint32_t pct = s->grid_pct;
+        if (pct == 0) {
+            bool partner = false;             // another lane's launch not finished yet (host query, ~1 us)
+            for (int l = 0; s->overlap && l < rt_scene::NLANE && !partner; l++)
+                partner = l != q && s->ev_lane_done[l] && hipEventQuery(s->ev_lane_done[l]) == hipErrorNotReady;
+            pct = partner ? 50u : 100u;
+        }
         if (pct < 100) blocks = std::max<uint32_t>(8u, blocks * pct / 100u);
         HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, lane_counters, s->queue[q], blocks, s->threshold,
                                                        s->variant, false, reset_queue, stream)

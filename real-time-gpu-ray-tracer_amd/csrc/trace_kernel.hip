@@ -62,6 +62,13 @@ constexpr int SPILL_DEPTH = 48;         // overflow entries in scratch (max dept
 #ifndef RT_LEAN_WIDE
 #define RT_LEAN_WIDE 0                  // 1: quad trees take the lean one-pop-per-step loop (lw_*; measured slower)
 #endif
+#ifndef RT_INLINE_INST
+#define RT_INLINE_INST 0                // 1: quad trees: a lane reaching a TLAS leaf enters the instance inside the
+                                        // interior loop (instance record from LDS) instead of in a leaf round;
+                                        // measured 25-50 % slower (C2 kernel 0.370 -> 0.463 ms, C3 2.75 -> 4.12 ms:
+                                        // lanes that no longer stop at instances diverge deeper inside the loop),
+                                        // profiles/r02_ab_inline_instance.jsonl
+#endif
 #ifndef TRI_AHEAD
 #define TRI_AHEAD 2                     // triangle records of a leaf requested before the first test
 #endif
@@ -643,12 +650,36 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
 }
 #endif
 
+#if !RT_EXACT
+// Instance::hit entry (Instance.cu:19-35) of the TLAS leaf in T.cur: the ray into the instance's space,
+// then the BLAS root (or the next stack entry if its box is missed).  Entering an instance changes no
+// tmax, so it needs no leaf round of its own: with the record in LDS ("lds_scene") it costs no memory
+// round trip either.  A lane only enters while it holds no postponed leaf (whose test needs T.lr).
+template <bool COUNT>
+__device__ __forceinline__ void enter_instance(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
+    const uint32_t start = ref_leaf_start(T.cur), count = ref_leaf_count(T.cur);
+    if (count > 1) stack_push(T.stk, spill, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
+    T.cur_inst = sc.inst_by_slot ? start : sc.tlas_slots[start];
+    if (COUNT) cnt.inst++;
+    const InstRec I = load_inst<true>(sc, T.cur_inst);
+    const float inv[12] = {I.i0.x, I.i0.y, I.i0.z, I.i0.w, I.i1.x, I.i1.y, I.i1.z, I.i1.w, I.i2.x, I.i2.y, I.i2.z, I.i2.w};
+    const float box[6] = {I.box01.x, I.box01.y, I.box01.z, I.box01.w, I.box2ref.x, I.box2ref.y};
+    T.lr.o = xf_point(inv, T.wr.o);                            // Instance.cu:26-27
+    T.lr.d = xf_vector(inv, T.wr.d);
+    prep(T.lr);
+    float te = 0.0f;
+    if (slab(box, T.lr, TMIN, T.tmax, te)) { T.cur = __float_as_uint(I.box2ref.w); T.curT = te; }
+    else pop_next(T, spill);
+}
+#endif
+
 template <bool COUNT, bool WIDE = false>
 __device__ __forceinline__ void spec_interior_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
     const uint32_t cur = T.cur;
 #if !RT_EXACT
     if (WIDE) {
         if (!(cur & REF_LEAF)) wide_interior_step<COUNT>(T, sc, spill, cnt);
+        else if (RT_INLINE_INST && !(cur & REF_BLAS)) enter_instance<COUNT>(T, sc, spill, cnt);
         else { T.pleaf = cur; pop_next(T, spill); }        // postpone, keep walking
         return;
     }

@@ -40,6 +40,16 @@ if [[ $WHAT == grid2 ]]; then
   done; done
   for lp in 3:100 3:50 4:50; do L=${lp%:*}; P=${lp#*:}; one sweep_grid2.jsonl --overlap $L --opt grid_pct=$P --config C3; done
 fi
+if [[ $WHAT == shares2 ]]; then
+  # every 1/8 share of C2 and C4 with the library defaults (3 lanes, auto grid_pct), and the full frames
+  one sweep_shares2.jsonl --steps 200
+  one sweep_shares2.jsonl --steps 200 --config C4
+  for r in 0 1 2 3 4 5 6 7; do
+    one sweep_shares2.jsonl --steps 200 --shard $r/8
+    one sweep_shares2.jsonl --steps 200 --config C4 --shard $r/8
+  done
+  for L in 2 3; do one sweep_shares2.jsonl --steps 200 --overlap $L --opt grid_pct=50; one sweep_shares2.jsonl --steps 200 --overlap $L --opt grid_pct=50 --shard 1/8; done
+fi
 if [[ $WHAT == lds ]]; then
   # option "lds_scene": TLAS quads + instance hot records in LDS (1) vs HBM (0), alternating
   for rep in 1 2; do for v in 0 1; do
