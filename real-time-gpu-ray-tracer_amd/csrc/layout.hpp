@@ -222,6 +222,7 @@ struct OutputGPU {
     uint32_t queue_parts;
     uint32_t nt_store;              // 1: RGBA8 stores are non-temporal (keep the scene in L2)
     uint32_t grab;                  // pixels claimed per queue atomic
+    uint32_t claim_items;           // ordered walk ("reorder"): consecutive order items per queue atomic (1..2)
     uint32_t supertile;             // frame mode, grab 64: walk bands in supertile x supertile units (0 = rows)
     unsigned long long *timeline;   // TIMELINE_WORDS per wave (rt.h, rt_scene_debug_read)
     uint32_t *costmap;              // COUNT launches: traversal rounds per output pixel (debug)

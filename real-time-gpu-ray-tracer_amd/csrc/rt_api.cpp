@@ -214,6 +214,7 @@ struct rt_scene {
     uint32_t queue_parts = 8;       // one band per XCD (measured with "reorder": 8 beat 4, 2 and 1 on C2)
     uint32_t nt_store = 0;
     uint32_t grab = 64;             // pixels per queue claim
+    uint32_t claim_items = 2;       // ordered walk: order items per queue atomic (option "claim_items")
     uint32_t supertile = 16;        // band walk order: st x st-unit supertiles (measured: 16 beats rows, 8 and 32)
     bool lean = false;              // FAST persistent kernel: LDS-only-stack traversal when the trees fit (measured slower on C2)
     uint32_t max_blas_height = 0;
@@ -1174,6 +1175,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     if (s->use_persistent) {
         out.queue_parts = s->queue_parts;
         out.grab = s->grab;
+        out.claim_items = s->claim_items;
         out.supertile = s->supertile;
         if (s->timeline_on) {
             const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false, false)
@@ -1431,6 +1433,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "costmap") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
         s->costmap_on = value == 1;
+    } else if (k == "claim_items") {
+        if (value < 1 || value > 2) return fail(RT_ERR_INVALID_ARGUMENT, "claim_items must be 1 or 2");
+        s->claim_items = (uint32_t)value;
     } else if (k == "grid_pct") {
         if (value < 0 || value > 100) return fail(RT_ERR_INVALID_ARGUMENT, "grid_pct must be in 0..100 (0 = auto)");
         s->grid_pct = (uint32_t)value;

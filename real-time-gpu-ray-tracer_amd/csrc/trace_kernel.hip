@@ -1535,6 +1535,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
         }
     };
     uint32_t pool_next = 0, pool_end = 0;     // wave-uniform
+    uint32_t pool2_next = 0, pool2_end = 0;   // wave-uniform: the second item of a two-item claim
     uint32_t limit = 0, limit_part = ~0u;     // wave-uniform: claim positions in band `limit_part`
     bool exhausted = false;                   // wave-uniform
     const uint32_t S2 = cam.sqrt_s * cam.sqrt_s;
@@ -1558,7 +1559,11 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
         while (need && !exhausted) {
             if (RT_DIAG) pc.refill_iters++;
             const uint32_t n_need = __popcll(need);
-            if (pool_next >= pool_end) {
+            if (pool_next >= pool_end && pool2_next < pool2_end) {      // the claim's second item
+                pool_next = pool2_next;
+                pool_end = pool2_end;
+                pool2_next = pool2_end;
+            } else if (pool_next >= pool_end) {
                 // bands: whole unit rows in frame mode (so a band can be walked in supertiles)
                 const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
                 const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
@@ -1566,7 +1571,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                 const uint32_t p_end = (rows * (part + 1) / parts) * upr * 64u;
                 // ordered walk (schedule.hip): one item per claim, a whole unit or a 1/2, 1/4 of a heavy
                 // one; the band's item count sits next to its head.  Screen walk: `grab` pixels per claim.
-                const uint32_t step = out.order ? 1u : grab;
+                const uint32_t step = out.order ? (out.claim_items > 1u ? 2u : 1u) : grab;
                 if (part != limit_part) {          // the band's item count: read once per band, off the head's line
                     limit_part = part;
                     limit = out.order ? __builtin_amdgcn_readfirstlane(queue[(QUEUE_MAX_PARTS + part) * QUEUE_STRIDE])
@@ -1590,10 +1595,19 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     continue;
                 }
                 if (out.order) {
-                    const uint32_t it = out.order[4u * (p_begin >> 6) + b];
+                    // claim_items 2: two consecutive order items per atomic, both entries read in one
+                    // round trip (the claim atomic + its dependent order read are ~2 us under load)
+                    const uint32_t *ob = out.order + 4u * (p_begin >> 6) + b;
+                    const uint32_t it = ob[0];
+                    const uint32_t it2 = step > 1u && b + 1u < limit ? ob[1] : ~0u;
                     const uint32_t len = 64u >> (it & 3u);
                     pool_next = (it >> 4) * 64u + ((it >> 2) & 3u) * len;
                     pool_end = pool_next + len;
+                    if (it2 != ~0u) {
+                        const uint32_t len2 = 64u >> (it2 & 3u);
+                        pool2_next = (it2 >> 4) * 64u + ((it2 >> 2) & 3u) * len2;
+                        pool2_end = pool2_next + len2;
+                    }
                 } else {
                     b += p_begin;
                     pool_next = b;

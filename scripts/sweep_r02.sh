@@ -50,6 +50,15 @@ if [[ $WHAT == shares2 ]]; then
   done
   for L in 2 3; do one sweep_shares2.jsonl --steps 200 --overlap $L --opt grid_pct=50; one sweep_shares2.jsonl --steps 200 --overlap $L --opt grid_pct=50 --shard 1/8; done
 fi
+if [[ $WHAT == claim ]]; then
+  # option "claim_items": order items per queue atomic (1 vs 2), alternating
+  for rep in 1 2; do for v in 1 2; do
+    one sweep_claim.jsonl --opt claim_items=$v
+    one sweep_claim.jsonl --opt claim_items=$v --shard 4/8
+    one sweep_claim.jsonl --opt claim_items=$v --config C3
+    one sweep_claim.jsonl --opt claim_items=$v --config C4 --shard 3/8
+  done; done
+fi
 if [[ $WHAT == lds ]]; then
   # option "lds_scene": TLAS quads + instance hot records in LDS (1) vs HBM (0), alternating
   for rep in 1 2; do for v in 0 1; do
