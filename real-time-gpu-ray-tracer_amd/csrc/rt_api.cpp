@@ -214,7 +214,10 @@ struct rt_scene {
     uint32_t queue_parts = 8;       // one band per XCD (measured with "reorder": 8 beat 4, 2 and 1 on C2)
     uint32_t nt_store = 0;
     uint32_t grab = 64;             // pixels per queue claim
-    uint32_t claim_items = 2;       // ordered walk: order items per queue atomic (option "claim_items")
+    // ordered walk: order items per queue atomic (option "claim_items"); 2 measured slower (C2 kernel
+    // 0.39 -> 0.48 ms, 1/8 share 0.079 -> 0.107 ms/frame: the heaviest items head the order, and a wave
+    // given two of them runs both back to back; profiles/r02_sweep_claim_items.jsonl)
+    uint32_t claim_items = 1;
     uint32_t supertile = 16;        // band walk order: st x st-unit supertiles (measured: 16 beats rows, 8 and 32)
     bool lean = false;              // FAST persistent kernel: LDS-only-stack traversal when the trees fit (measured slower on C2)
     uint32_t max_blas_height = 0;
