@@ -223,6 +223,8 @@ struct OutputGPU {
     uint32_t nt_store;              // 1: RGBA8 stores are non-temporal (keep the scene in L2)
     uint32_t grab;                  // pixels claimed per queue atomic
     uint32_t claim_items;           // ordered walk ("reorder"): consecutive order items per queue atomic (1..2)
+    uint32_t mix;                   // ordered walk: a refill's first claim takes the band's heaviest item (front),
+                                    // its further claims the lightest (back): one 64-bit head {front, back}
     uint32_t supertile;             // frame mode, grab 64: walk bands in supertile x supertile units (0 = rows)
     unsigned long long *timeline;   // TIMELINE_WORDS per wave (rt.h, rt_scene_debug_read)
     uint32_t *costmap;              // COUNT launches: traversal rounds per output pixel (debug)

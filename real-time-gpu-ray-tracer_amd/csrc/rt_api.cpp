@@ -218,6 +218,7 @@ struct rt_scene {
     // 0.39 -> 0.48 ms, 1/8 share 0.079 -> 0.107 ms/frame: the heaviest items head the order, and a wave
     // given two of them runs both back to back; profiles/r02_sweep_claim_items.jsonl)
     uint32_t claim_items = 1;
+    uint32_t mix = 0;               // option "mix" (ordered walk): heaviest item first per refill, light fill after
     uint32_t supertile = 16;        // band walk order: st x st-unit supertiles (measured: 16 beats rows, 8 and 32)
     bool lean = false;              // FAST persistent kernel: LDS-only-stack traversal when the trees fit (measured slower on C2)
     uint32_t max_blas_height = 0;
@@ -1179,6 +1180,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         out.queue_parts = s->queue_parts;
         out.grab = s->grab;
         out.claim_items = s->claim_items;
+        out.mix = s->mix;
         out.supertile = s->supertile;
         if (s->timeline_on) {
             const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false, false)
@@ -1436,6 +1438,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "costmap") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
         s->costmap_on = value == 1;
+    } else if (k == "mix") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "mix must be 0 or 1");
+        s->mix = (uint32_t)value;
     } else if (k == "claim_items") {
         if (value < 1 || value > 2) return fail(RT_ERR_INVALID_ARGUMENT, "claim_items must be 1 or 2");
         s->claim_items = (uint32_t)value;

@@ -50,7 +50,8 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
     __shared__ uint8_t nib[SCHED_NIB_UNITS / 2];               // class codes, 2 per byte (8 KB)
     __shared__ uint32_t total[SCHED_CLASSES], base[SCHED_CLASSES];
     const uint32_t part = blockIdx.x, t = threadIdx.x;
-    if (part == 0 && t < QUEUE_MAX_PARTS) queue[t * QUEUE_STRIDE] = 0u;      // every head: `parts` may change
+    if (part == 0 && t < 2 * QUEUE_MAX_PARTS) queue[(t >> 1) * QUEUE_STRIDE + (t & 1u)] = 0u;   // every head (front,
+                                                                                               // back): `parts` may change
     if (part == 0 && zero_counters && t < CNT_NUM) zero_counters[t] = 0ull;  // the lane's work counters
     // the frame's TLAS / instance block, read from pinned host staging (see launch_frame_copy): the first
     // COPY_AHEAD pieces per thread are loaded now and stored after the first cost loads have been issued,
@@ -191,7 +192,8 @@ hipError_t launch_schedule(uint32_t *cost, uint32_t *cost_prev, uint32_t *order,
 __global__ __launch_bounds__(256) void frame_copy_kernel(uint4 *__restrict__ dst, const uint4 *__restrict__ src, uint32_t n16,
                                                          unsigned long long *zero_counters, uint32_t *zero_queue) {
     if (zero_counters && blockIdx.x == 0 && threadIdx.x < CNT_NUM) zero_counters[threadIdx.x] = 0ull;
-    if (zero_queue && blockIdx.x == 0 && threadIdx.x < QUEUE_MAX_PARTS) zero_queue[threadIdx.x * QUEUE_STRIDE] = 0u;
+    if (zero_queue && blockIdx.x == 0 && threadIdx.x < 2 * QUEUE_MAX_PARTS)
+        zero_queue[(threadIdx.x >> 1) * QUEUE_STRIDE + (threadIdx.x & 1u)] = 0u;     // head words: front, back
     for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n16; i += gridDim.x * 256u) dst[i] = src[i];
 }
 

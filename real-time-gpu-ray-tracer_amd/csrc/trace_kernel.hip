@@ -1556,6 +1556,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
         // ---- refill idle lanes from the wave's pool / the global queue
         DIAG_T(t_refill);
         uint64_t need = __ballot(!has);
+        bool first_claim = true;            // wave-uniform ("mix"): this refill has not claimed yet
         while (need && !exhausted) {
             if (RT_DIAG) pc.refill_iters++;
             const uint32_t n_need = __popcll(need);
@@ -1582,8 +1583,20 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     pend_cost = 0;
                 }
                 uint32_t b = 0;
-                if (lane == 0) b = atomicAdd(queue + part * QUEUE_STRIDE, step);
-                b = __builtin_amdgcn_readfirstlane(__shfl(b, 0, 64));
+                if (out.order && out.mix) {
+                    // {front, back} in one 64-bit head: a front claim takes item f, a back claim item
+                    // limit - 1 - k; both are free exactly while f + k < limit at the atomic
+                    const bool back = !first_claim;
+                    unsigned long long old = 0;
+                    if (lane == 0) old = atomicAdd(reinterpret_cast<unsigned long long *>(queue + part * QUEUE_STRIDE),
+                                                   back ? (1ull << 32) : 1ull);
+                    const uint32_t f = __builtin_amdgcn_readfirstlane(__shfl((uint32_t)old, 0, 64));
+                    const uint32_t k = __builtin_amdgcn_readfirstlane(__shfl((uint32_t)(old >> 32), 0, 64));
+                    b = f + k >= limit ? limit : (back ? limit - 1u - k : f);
+                } else {
+                    if (lane == 0) b = atomicAdd(queue + part * QUEUE_STRIDE, step);
+                    b = __builtin_amdgcn_readfirstlane(__shfl(b, 0, 64));
+                }
                 n_grabs++;
                 if (b >= limit) {
                     if (++tried >= parts) {
@@ -1594,12 +1607,13 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     part = part + 1 == parts ? 0 : part + 1;
                     continue;
                 }
+                first_claim = false;
                 if (out.order) {
                     // claim_items 2: two consecutive order items per atomic, both entries read in one
                     // round trip (the claim atomic + its dependent order read are ~2 us under load)
                     const uint32_t *ob = out.order + 4u * (p_begin >> 6) + b;
                     const uint32_t it = ob[0];
-                    const uint32_t it2 = step > 1u && b + 1u < limit ? ob[1] : ~0u;
+                    const uint32_t it2 = step > 1u && !out.mix && b + 1u < limit ? ob[1] : ~0u;
                     const uint32_t len = 64u >> (it & 3u);
                     pool_next = (it >> 4) * 64u + ((it >> 2) & 3u) * len;
                     pool_end = pool_next + len;

@@ -59,6 +59,15 @@ if [[ $WHAT == claim ]]; then
     one sweep_claim.jsonl --opt claim_items=$v --config C4 --shard 3/8
   done; done
 fi
+if [[ $WHAT == mix ]]; then
+  # option "mix": per refill the heaviest item from the band's front, light fill from its back
+  for rep in 1 2; do for v in 0 1; do
+    one sweep_mix.jsonl --opt mix=$v
+    one sweep_mix.jsonl --opt mix=$v --shard 4/8
+    one sweep_mix.jsonl --opt mix=$v --config C3
+    one sweep_mix.jsonl --opt mix=$v --config C4 --shard 3/8
+  done; done
+fi
 if [[ $WHAT == lds ]]; then
   # option "lds_scene": TLAS quads + instance hot records in LDS (1) vs HBM (0), alternating
   for rep in 1 2; do for v in 0 1; do

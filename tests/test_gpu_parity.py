@@ -403,6 +403,35 @@ def test_reorder_period_byte_identical(gpu_lib, period, lanes):
         assert np.array_equal(bufs[f].cpu().numpy().reshape(H, W, 4), ref[f]), f
 
 
+@pytest.mark.parametrize("opts", [{"mix": 1}, {"claim_items": 2}, {"mix": 1, "claim_items": 2}, {"grid_pct": 30}])
+def test_claim_options_byte_identical(gpu_lib, opts):
+    """Claim-order options of the persistent kernel ("mix": heaviest item from a band's front, light fill
+    from its back; "claim_items" 2; a 30 % grid): which wave traces a pixel changes, the pixel's result
+    does not.  Frames on three overlapped lanes equal the screen-order walk byte for byte, across the
+    launches that record costs and the ones that claim in the recorded order, and the work counters
+    equal the serial frames'."""
+    import torch
+    s = scenes.demo_with_particles(10)
+    W, H, F = 360, 200, 12
+    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(W, H, ray_trace_depth=2)
+    r.set_option("reorder", 0)
+    ref = [r.render(f, count_work=True) for f in range(F)]
+    r.set_option("reorder", 1).set_option("reorder_period", 2).set_option("overlap", 3)
+    for k, v in opts.items():
+        r.set_option(k, v)
+    streams = [torch.cuda.Stream() for _ in range(3)]
+    bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(F)]
+    for f in range(F):
+        r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=streams[f % 3].cuda_stream, sync=False,
+                 count_work=True, keep_counters=f > 0)
+    acc, _ = r.collect()
+    torch.cuda.synchronize()
+    for f in range(F):
+        assert np.array_equal(bufs[f].cpu().numpy().reshape(H, W, 4), ref[f][0]), f
+    assert acc["rays"] == sum(x[2]["rays"] for x in ref)
+    assert acc["pixels"] == F * W * H
+
+
 @pytest.mark.parametrize("mode,particles", [("sah", 10), ("lbvh", 10), ("sah", 254)])
 def test_lds_scene_byte_identical(gpu_lib, mode, particles):
     """Option "lds_scene": the TLAS quads (and, when they fit as well, the instance hot records) are read
