@@ -69,6 +69,10 @@ constexpr int SPILL_DEPTH = 48;         // overflow entries in scratch (max dept
                                         // lanes that no longer stop at instances diverge deeper inside the loop),
                                         // profiles/r02_ab_inline_instance.jsonl
 #endif
+#ifndef RT_CHAIN_ROOT_LEAF
+#define RT_CHAIN_ROOT_LEAF 1            // quad trees: an entered instance whose BLAS root is a leaf (a sphere, a
+                                        // parallelogram, a small mesh) has it tested in the same leaf round
+#endif
 #ifndef TRI_AHEAD
 #define TRI_AHEAD 2                     // triangle records of a leaf requested before the first test
 #endif
@@ -717,9 +721,16 @@ __device__ __forceinline__ void spec_interior_step(Trav &T, const SceneGPU &sc, 
 }
 
 // Process the postponed leaf, then resume at cur (re-tested) — TLAS.cu:157-173 / BLAS.cu:153-176.
+// FAST quad trees (RT_CHAIN_ROOT_LEAF): when the entered instance's BLAS root is itself a leaf, its
+// primitives are tested in this same round, as BLAS::hit tests a leaf root right after the root box
+// (BLAS.cu:140-176) — the speculative successor waits on the stack as before and is popped (re-tested)
+// after the tests.  A segment against the demo's spheres / parallelogram then takes one round, not two.
+// Returns 1 when a root leaf was chained (it counts as a step of its own in the unit costs, so the
+// claim order's cost classes keep the scale they were tuned on).
 template <bool COUNT, bool WIDE = false>
-__device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
-    const uint32_t leaf = T.pleaf;
+__device__ __forceinline__ uint32_t spec_leaf_phase(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
+    uint32_t leaf = T.pleaf;
+    bool chained = false;
     T.pleaf = REF_NONE;
     if (!(leaf & REF_BLAS)) {
         // TLAS leaf: enter the first instance's BLAS; the speculative successor and the leaf's
@@ -739,8 +750,13 @@ __device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEn
             T.lr.o = xf_point(inv, T.wr.o);                    // Instance.cu:26-27
             T.lr.d = xf_vector(inv, T.wr.d);
             prep(T.lr);
-            if (slab(box, T.lr, TMIN, T.tmax, te)) { T.cur = __float_as_uint(I.box2ref.w); T.curT = te; }
-            else pop_next(T, spill);
+            if (slab(box, T.lr, TMIN, T.tmax, te)) {
+                T.cur = __float_as_uint(I.box2ref.w);
+                T.curT = te;
+                if (RT_CHAIN_ROOT_LEAF && (T.cur & REF_LEAF)) { leaf = T.cur; chained = true; }
+            } else {
+                pop_next(T, spill);
+            }
         } else
 #endif
         {
@@ -751,7 +767,8 @@ __device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEn
             if (slab(I.root_box, T.lr, TMIN, T.tmax, te)) { T.cur = WIDE ? I.root_ref_wide : I.root_ref; T.curT = te; }
             else pop_next(T, spill);
         }
-    } else {
+    }
+    if (leaf & REF_BLAS) {                  // the postponed BLAS leaf, or (chained) the entered BLAS's root leaf
         const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf), type = ref_leaf_type(leaf);
         if (type == RT_PRIM_TRIANGLE) {
             // every triangle record of the leaf is requested before the first test: one memory round
@@ -799,9 +816,11 @@ __device__ __forceinline__ void spec_leaf_phase(Trav &T, const SceneGPU &sc, SEn
                 }
             }
         }
-        if (T.cur != REF_NONE && !(T.curT < T.tmax)) pop_next(T, spill);   // re-test the successor
+        if (chained) pop_next(T, spill);                                   // the root leaf is done
+        else if (T.cur != REF_NONE && !(T.curT < T.tmax)) pop_next(T, spill);   // re-test the successor
     }
     if (T.cur == REF_NONE) T.tracing = false;
+    return chained ? 1u : 0u;
 }
 
 #ifndef RT_DIAG
@@ -845,8 +864,8 @@ __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *sp
     DIAG_ADD(pc.interior, t0);
     DIAG_T(t1);
     if (T.tracing) {
-        spec_leaf_phase<COUNT, WIDE>(T, sc, spill, cnt);
-        if (track) steps++;
+        const uint32_t chained = spec_leaf_phase<COUNT, WIDE>(T, sc, spill, cnt);
+        if (track) steps += 1u + chained;
     }
     DIAG_ADD(pc.leaf, t1);
 }
