@@ -334,8 +334,9 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "grid_pct"  : persistent grid as a percentage of the resident workgroup capacity (1..100; default 0 = auto:
  *                 100 for serialised launches, 50 with "overlap", so two lanes' launches run side by side)
  *   "lds_scene" : FAST quad-tree kernel: 1 = every workgroup copies the frame's TLAS quads and, when they fit
- *                 as well, the instance hot records into 16 KB of LDS and reads them there (default 1;
- *                 results identical)
+ *                 as well, the instance hot records into 19 KB of LDS and reads them there; 2 = also the
+ *                 sphere / parallelogram records and the instance cold records, while they fit (default 2;
+ *                 0 = all from HBM; results identical)
  *   "overlap"   : L = consecutive rt_render calls cycle through L (2..8) internal lanes (work-queue
  *                 heads, unit costs, schedule); a launch waits only for the previous launch of its own
  *                 lane and for its frame block, so a caller that cycles L streams runs frame

@@ -174,9 +174,14 @@ struct SceneGPU {
     // LDS_SCENE_F4 dwordx4 of LDS at the start of every workgroup; 0 = read from HBM
     uint32_t lds_quads;             // TLAS quads in LDS (every TLAS interior ref indexes below it)
     uint32_t lds_insts;             // instance hot records in LDS (0 or instance_count)
+    // further records in LDS when they fit as well (dwordx4 offsets into the region, LDS_NONE = in HBM):
+    // instance cold records (6 dwordx4 each), sphere hot / cold (1 each), parallelogram hot (5) / cold (1)
+    uint32_t lds_icold, lds_sph_hot, lds_sph_cold, lds_q_hot, lds_q_cold;
 };
-constexpr uint32_t LDS_SCENE_F4 = 1024;    // 16 KB per workgroup: 36 + 16 KB keeps 3 workgroups per CU (160 KB)
-constexpr uint32_t LDS_QUAD_F4 = 7, LDS_INST_F4 = 5;
+constexpr uint32_t LDS_NONE = 0xFFFFFFFFu;
+constexpr uint32_t LDS_SCENE_F4 = 1216;    // 19 KB per workgroup: 32 KB stack + 1 KB materials + 19 KB keeps 3
+                                           // workgroups per CU (160 KB)
+constexpr uint32_t LDS_QUAD_F4 = 7, LDS_INST_F4 = 5, LDS_ICOLD_F4 = 6, LDS_QPRIM_F4 = 5;
 
 struct CameraGPU {                  // Camera (RendererImpl.cuh:32-61), precomputed on host
     float pixel_origin[3];

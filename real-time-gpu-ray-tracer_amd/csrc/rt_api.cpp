@@ -145,7 +145,8 @@ struct rt_scene {
     DevBuf<NodePair> blas_pairs;
     DevBuf<NodeQuad> blas_quads;    // option "wide"
     bool wide = true;               // FAST persistent kernel traverses the quad trees (host-built modes)
-    bool lds_scene = true;
+    uint32_t lds_scene = 2;         // quad-tree kernel: 1 = TLAS quads (+ instance hot records) in LDS when they
+                                    // fit, 2 = also sphere / parallelogram records and instance cold records
     // option "grid_pct": the persistent grid as a percentage of the resident capacity; 0 = auto: 50 when
     // another lane's launch is still in flight ("overlap"), so two lanes' launches are resident side by
     // side instead of the next one filling only the slots the previous one's tail frees (C2, 3 lanes:
@@ -555,6 +556,8 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.material_count = (uint32_t)(s->materials.n / 4);
     // option "lds_scene": the quads the frame's TLAS refs can index (host-built: this frame's quad count;
     // GPU-built: quad q is rooted at pair q, < n - 1) and, if they fit too, the instance hot records
+    // then, in this order while they fit: sphere and parallelogram records (hot + cold), instance cold records
+    g.lds_icold = g.lds_sph_hot = g.lds_sph_cold = g.lds_q_hot = g.lds_q_cold = LDS_NONE;
     if (s->lds_scene && g.wide) {
         const uint32_t n = g.instance_count;
         const uint32_t nq = s->gpu_tlas() ? (n > 1 ? n - 1 : 0) : (uint32_t)s->tlas_wide.quads.size();
@@ -562,6 +565,13 @@ SceneGPU scene_gpu(const rt_scene *s) {
             g.lds_quads = nq;
             if (nq * LDS_QUAD_F4 + n * LDS_INST_F4 <= LDS_SCENE_F4) g.lds_insts = n;
         }
+        uint32_t at = s->lds_scene >= 2 ? g.lds_quads * LDS_QUAD_F4 + g.lds_insts * LDS_INST_F4 : LDS_SCENE_F4;
+        const uint32_t ns = (uint32_t)s->sph_hot.n, nqd = (uint32_t)s->quad_hot.n;
+        if (ns > 0 && at + 2 * ns <= LDS_SCENE_F4) { g.lds_sph_hot = at; g.lds_sph_cold = at + ns; at += 2 * ns; }
+        if (nqd > 0 && at + (LDS_QPRIM_F4 + 1) * nqd <= LDS_SCENE_F4) {
+            g.lds_q_hot = at; g.lds_q_cold = at + LDS_QPRIM_F4 * nqd; at += (LDS_QPRIM_F4 + 1) * nqd;
+        }
+        if (g.lds_insts && at + n * LDS_ICOLD_F4 <= LDS_SCENE_F4) { g.lds_icold = at; at += n * LDS_ICOLD_F4; }
     }
     return g;
 }
@@ -1448,8 +1458,8 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         if (value < 0 || value > 100) return fail(RT_ERR_INVALID_ARGUMENT, "grid_pct must be in 0..100 (0 = auto)");
         s->grid_pct = (uint32_t)value;
     } else if (k == "lds_scene") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "lds_scene must be 0 or 1");
-        s->lds_scene = value == 1;
+        if (value < 0 || value > 2) return fail(RT_ERR_INVALID_ARGUMENT, "lds_scene must be 0, 1 or 2");
+        s->lds_scene = (uint32_t)value;
     } else if (k == "wide") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "wide must be 0 or 1");
         s->wide = value == 1;

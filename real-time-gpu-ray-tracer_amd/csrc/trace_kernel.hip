@@ -47,7 +47,7 @@ constexpr int BLOCK = 256;              // 4 waves; each wave owns one 8x8 pixel
 #define RT_LDS_DEPTH 16
 #endif
 #ifndef RT_LDS_MATERIALS
-#define RT_LDS_MATERIALS 256
+#define RT_LDS_MATERIALS 64              // the scene region ("lds_scene") needs the rest of the 52 KB
 #endif
 #ifndef RT_PATH_LDS
 #define RT_PATH_LDS 0                   // 1: the persistent kernel keeps path state (throughput, radiance,
@@ -566,6 +566,32 @@ __device__ __forceinline__ void lds_scene_fill(const SceneGPU &sc) {
     }
     const float4 *h = reinterpret_cast<const float4 *>(sc.inst_hot);
     for (uint32_t i = threadIdx.x; i < ni; i += BLOCK) lds_scene[nq + i] = h[i];
+    const auto copy = [](uint32_t at, const void *src, uint32_t n4) {
+        if (at == LDS_NONE) return;
+        const float4 *p = reinterpret_cast<const float4 *>(src);
+        for (uint32_t i = threadIdx.x; i < n4; i += BLOCK) lds_scene[at + i] = p[i];
+    };
+    copy(sc.lds_icold, sc.inst_cold, sc.instance_count * LDS_ICOLD_F4);
+    copy(sc.lds_sph_hot, sc.sph_hot, sc.lds_sph_cold - sc.lds_sph_hot);
+    copy(sc.lds_sph_cold, sc.sph_cold, sc.lds_sph_cold - sc.lds_sph_hot);
+    copy(sc.lds_q_hot, sc.quad_hot, (sc.lds_q_cold - sc.lds_q_hot));
+    copy(sc.lds_q_cold, sc.quad_cold, (sc.lds_q_cold - sc.lds_q_hot) / LDS_QPRIM_F4);
+}
+// record k of an array that may be resident in the LDS scene region (at = its dwordx4 offset, LDS_NONE = HBM)
+template <typename R>
+__device__ __forceinline__ R lds_or_global(uint32_t at, const R *g, uint32_t k) {
+    constexpr uint32_t N4 = sizeof(R) / 16;
+    R r;
+    float4 *d = reinterpret_cast<float4 *>(&r);
+    if (at != LDS_NONE) {
+#pragma unroll
+        for (uint32_t j = 0; j < N4; j++) d[j] = lds_scene[at + k * N4 + j];
+    } else {
+        const float4 *p = reinterpret_cast<const float4 *>(g + k);
+#pragma unroll
+        for (uint32_t j = 0; j < N4; j++) d[j] = p[j];
+    }
+    return r;
 }
 
 __device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float oinv, float4 &tn, float4 &tf) {
@@ -721,6 +747,12 @@ __device__ __forceinline__ void spec_interior_step(Trav &T, const SceneGPU &sc, 
 }
 
 // Process the postponed leaf, then resume at cur (re-tested) — TLAS.cu:157-173 / BLAS.cu:153-176.
+// a sphere / parallelogram record: from the LDS scene region in the quad-tree kernel when resident
+#if RT_EXACT
+#define WIDE_LDS_REC(at, arr, k) (arr)[k]
+#else
+#define WIDE_LDS_REC(at, arr, k) (WIDE ? lds_or_global((at), (arr), (k)) : (arr)[k])
+#endif
 // FAST quad trees (RT_CHAIN_ROOT_LEAF): when the entered instance's BLAS root is itself a leaf, its
 // primitives are tested in this same round, as BLAS::hit tests a leaf root right after the root box
 // (BLAS.cu:140-176) — the speculative successor waits on the stack as before and is popped (re-tested)
@@ -805,10 +837,10 @@ __device__ __forceinline__ uint32_t spec_leaf_phase(Trav &T, const SceneGPU &sc,
                 bool h;
                 if (type == RT_PRIM_SPHERE) {
                     if (COUNT) cnt.sq++;
-                    h = sphere_test(sc.sph_hot[slot], T.lr, TMIN, T.tmax, t);
+                    h = sphere_test(WIDE_LDS_REC(sc.lds_sph_hot, sc.sph_hot, slot), T.lr, TMIN, T.tmax, t);
                 } else {
                     if (COUNT) { cnt.sq++; cnt.quad++; }
-                    h = quad_test(sc.quad_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
+                    h = quad_test(WIDE_LDS_REC(sc.lds_q_hot, sc.quad_hot, slot), T.lr, TMIN, T.tmax, t, u, v);
                 }
                 if (h) {
                     T.found = true; T.tmax = t;
@@ -1232,7 +1264,11 @@ struct Surface { f3 p, n; uint32_t material; uint32_t orig; };
 // Instance::hit (Instance.cu:41-45) would have stored them.
 template <bool LDSS = false>
 __device__ __forceinline__ Surface finalize(const SceneGPU &sc, const f3 &wo, const f3 &wd, const Hit &h) {
+#if !RT_EXACT
+    const InstCold IC = LDSS ? lds_or_global(sc.lds_icold, sc.inst_cold, h.inst) : sc.inst_cold[h.inst];
+#else
     const InstCold &IC = sc.inst_cold[h.inst];
+#endif
     f3 lo, ld;
 #if !RT_EXACT
     if (LDSS) {
@@ -1255,15 +1291,29 @@ __device__ __forceinline__ Surface finalize(const SceneGPU &sc, const f3 &wo, co
         n = dot(ld, nn) < 0.0f ? nn : neg(nn);
         s.material = T.material; s.orig = T.orig_index;
     } else if (h.ptype == RT_PRIM_SPHERE) {                                    // Sphere.cu:37-39
+#if !RT_EXACT
+        const SphereHot S = LDSS ? lds_or_global(sc.lds_sph_hot, sc.sph_hot, h.slot) : sc.sph_hot[h.slot];
+        const PrimCold C = LDSS ? lds_or_global(sc.lds_sph_cold, sc.sph_cold, h.slot) : sc.sph_cold[h.slot];
+#else
         const SphereHot &S = sc.sph_hot[h.slot];
+        const PrimCold &C = sc.sph_cold[h.slot];
+#endif
         const f3 outward = unit(sub(p, ld3(S.center)));
         n = dot(ld, outward) < 0.0f ? outward : neg(outward);
-        s.material = sc.sph_cold[h.slot].material; s.orig = sc.sph_cold[h.slot].orig_index;
+        s.material = C.material; s.orig = C.orig_index;
     } else {                                                                   // Parallelogram.cu:42-43
+#if !RT_EXACT
+        const float4 qn4 = LDSS && sc.lds_q_hot != LDS_NONE ? lds_scene[sc.lds_q_hot + h.slot * LDS_QPRIM_F4]
+                                                              : reinterpret_cast<const float4 *>(sc.quad_hot + h.slot)[0];
+        const PrimCold C = LDSS ? lds_or_global(sc.lds_q_cold, sc.quad_cold, h.slot) : sc.quad_cold[h.slot];
+        const f3 qn = mk(qn4.x, qn4.y, qn4.z);
+#else
         const QuadHot &Q = sc.quad_hot[h.slot];
+        const PrimCold &C = sc.quad_cold[h.slot];
         const f3 qn = ld3(Q.n);
+#endif
         n = dot(ld, qn) < 0.0f ? qn : neg(qn);
-        s.material = sc.quad_cold[h.slot].material; s.orig = sc.quad_cold[h.slot].orig_index;
+        s.material = C.material; s.orig = C.orig_index;
     }
     s.p = xf_point(IC.fwd, p);
     s.n = unit(xf_vector(IC.nrm, n));

@@ -68,6 +68,15 @@ if [[ $WHAT == mix ]]; then
     one sweep_mix.jsonl --opt mix=$v --config C4 --shard 3/8
   done; done
 fi
+if [[ $WHAT == lds2 ]]; then
+  # option "lds_scene" 1 (TLAS quads + instance hot records) vs 2 (also analytic primitives + instance cold records)
+  for rep in 1 2; do for v in 1 2; do
+    one sweep_lds2.jsonl --opt lds_scene=$v
+    one sweep_lds2.jsonl --opt lds_scene=$v --shard 4/8
+    one sweep_lds2.jsonl --opt lds_scene=$v --config C3
+    one sweep_lds2.jsonl --opt lds_scene=$v --build lbvh
+  done; done
+fi
 if [[ $WHAT == lds ]]; then
   # option "lds_scene": TLAS quads + instance hot records in LDS (1) vs HBM (0), alternating
   for rep in 1 2; do for v in 0 1; do

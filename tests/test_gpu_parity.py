@@ -443,11 +443,12 @@ def test_lds_scene_byte_identical(gpu_lib, mode, particles):
     r = Renderer(s).build_acceleration_structure(0, mode=mode).configure_camera(W, H, ray_trace_depth=2)
     r.set_option("lds_scene", 0)
     ref = [r.render(f, count_work=True) for f in range(3)]
-    r.set_option("lds_scene", 1)
-    for f in range(3):
-        img, _, st = r.render(f, count_work=True)
-        assert np.array_equal(img, ref[f][0]), f
-        assert st["rays"] == ref[f][2]["rays"] and st["triangle_tests"] == ref[f][2]["triangle_tests"]
+    for level in (1, 2):
+        r.set_option("lds_scene", level)
+        for f in range(3):
+            img, _, st = r.render(f, count_work=True)
+            assert np.array_equal(img, ref[f][0]), (level, f)
+            assert st["rays"] == ref[f][2]["rays"] and st["triangle_tests"] == ref[f][2]["triangle_tests"]
 
 
 @pytest.mark.parametrize("tiles,nl,mode", [(None, 2, "sah"), ((64, 64, 1, 3), 2, "sah"), (None, 3, "sah"),
