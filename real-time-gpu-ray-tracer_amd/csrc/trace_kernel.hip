@@ -1668,6 +1668,10 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                 }
                 n_grabs++;
                 if (b >= limit) {
+                    // the band is dry: try the next one.  `tried` counts failures over the wave's life, so a
+                    // wave retires after `parts` failed claims even if a band it left still has items: it frees
+                    // its slot for the next lane's launch (a scan of every band's head instead, stealing until
+                    // the last item, measured 45 % slower on C2: profiles/r02_ab_exit_scan.jsonl)
                     if (++tried >= parts) {
                         exhausted = true;
                         if (out.timeline) t_exhaust = __builtin_amdgcn_s_memrealtime();

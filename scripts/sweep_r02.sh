@@ -77,6 +77,16 @@ if [[ $WHAT == lds2 ]]; then
     one sweep_lds2.jsonl --opt lds_scene=$v --build lbvh
   done; done
 fi
+if [[ $WHAT == retune ]]; then
+  # knobs re-checked after lds_scene / grid_pct / chained root leaves: refill threshold, split levels, reorder period
+  for rep in 1 2; do
+    for t in 24 32 40 48 56; do one sweep_retune.jsonl --threshold $t; done
+    for sp in 2572 3084 3598 65535; do one sweep_retune.jsonl --opt split=$sp; done
+    for k in 4 16; do one sweep_retune.jsonl --opt reorder_period=$k; done
+    for t in 24 40; do one sweep_retune.jsonl --threshold $t --shard 4/8; done
+    one sweep_retune.jsonl --shard 4/8
+  done
+fi
 if [[ $WHAT == lds ]]; then
   # option "lds_scene": TLAS quads + instance hot records in LDS (1) vs HBM (0), alternating
   for rep in 1 2; do for v in 0 1; do
