@@ -339,6 +339,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
+                # the same bytes over the pipelined frame time (frames overlapped: ms_per_step), N = 1 only
+                "frac_throughput": (round(bytes_launch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
+                                    if n == 1 and not shard else None),
                 "traffic": traffic,
                 "hbm_frac_measured": round(hbm_frac, 5) if hbm_frac is not None else None,
                 "kernel": kname,
