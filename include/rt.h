@@ -331,6 +331,9 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 (default 1; 0 = instance order, for A/B — results are identical)
  *   "reserve"   : with "overlap", the persistent grid leaves this many workgroup slots free (default 16, two
  *                 per XCD) so the next lanes' schedule / upload / GPU TLAS kernels start beside the running launch
+ *   "blas_double": RT_BUILD_LBVH rebuilds (option "rebuild", rt_scene_update_triangles): 1 = write a spare BLAS
+ *                 set and swap it in, so a frame's rebuild overlaps the previous frame's trace (default 1;
+ *                 0 = one set, a rebuild waits for every lane's trace)
  *   "grid_pct"  : persistent grid as a percentage of the resident workgroup capacity (1..100; default 0 = auto:
  *                 100 for serialised launches, 50 with "overlap", so two lanes' launches run side by side)
  *   "lds_scene" : FAST quad-tree kernel: 1 = every workgroup copies the frame's TLAS quads and, when they fit

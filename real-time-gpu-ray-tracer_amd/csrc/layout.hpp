@@ -238,6 +238,7 @@ struct OutputGPU {
     // largest cost (traversal rounds + 1) of unit u's pixels for the next launch's order
     const uint32_t *order;
     uint32_t *unit_cost;
+    uint32_t cost_max;              // 1: a unit's cost is 64 x its longest path (atomicMax), not the sum of its paths
     // option "primary" (FAST, quad trees): the closest hits of every pixel's first camera ray, traced by
     // primary_packet_kernel before the persistent launch; record j = work item j (unit * 64 + lane):
     // {t, instance record (PREC_MISS / PREC_TRACE), ptype << 28 | slot, u} + v.  Null: traced in place.

@@ -152,7 +152,7 @@ struct rt_scene {
     // side instead of the next one filling only the slots the previous one's tail frees (C2, 3 lanes:
     // 0.252 -> 0.229 ms/frame; a C2 1/8 share 0.115 -> 0.084; C3 1.64 -> 1.59,
     // profiles/r02_sweep_grid2.jsonl), else 100 (a frame alone on the GPU takes all of it)
-    uint32_t grid_pct = 0;          // quad-tree kernel: TLAS quads (+ instance hot records) in LDS when they fit
+    uint32_t grid_pct = 0;
     uint32_t wide_merge = 0;        // quad trees: binary subtrees of <= wide_merge items become one leaf (set before build)
     DevBuf<TriHot> tri_hot;
     DevBuf<TriCold> tri_cold;
@@ -219,7 +219,8 @@ struct rt_scene {
     // 0.39 -> 0.48 ms, 1/8 share 0.079 -> 0.107 ms/frame: the heaviest items head the order, and a wave
     // given two of them runs both back to back; profiles/r02_sweep_claim_items.jsonl)
     uint32_t claim_items = 1;
-    uint32_t mix = 0;               // option "mix" (ordered walk): heaviest item first per refill, light fill after
+    uint32_t mix = 0;
+    uint32_t cost_max = 0;          // option "cost_max": order units by their longest path (x 64), not their summed cost               // option "mix" (ordered walk): heaviest item first per refill, light fill after
     uint32_t supertile = 16;        // band walk order: st x st-unit supertiles (measured: 16 beats rows, 8 and 32)
     bool lean = false;              // FAST persistent kernel: LDS-only-stack traversal when the trees fit (measured slower on C2)
     uint32_t max_blas_height = 0;
@@ -276,6 +277,21 @@ struct rt_scene {
     DevBuf<uint32_t> gpu_counts;        // [0] BLAS pairs written, [1] TLAS pairs written (last frame)
     bool rebuild_blas = false;          // option "rebuild": rebuild every BLAS each frame
     bool blas_dirty = false;            // rt_scene_update_triangles since the last BLAS build
+    // RT_BUILD_LBVH rebuilds (option "blas_double", default on): a rebuild writes a spare BLAS set and swaps it
+    // in, so frame k+1's rebuild runs while frame k's trace still reads the other set (C5: the rebuild no
+    // longer waits for every lane's trace).  ev_blas_lane[q]: lane q's last trace of the current set.
+    struct BlasSet {
+        DevBuf<NodePair> pairs; DevBuf<NodeQuad> quads; DevBuf<TreeRoot> roots;
+        DevBuf<TriHot> tri_hot; DevBuf<TriCold> tri_cold; DevBuf<SphereHot> sph_hot; DevBuf<PrimCold> sph_cold;
+        DevBuf<QuadHot> quad_hot; DevBuf<PrimCold> quad_cold;
+        hipEvent_t ev_lane[NLANE] = {};
+        void release() {
+            pairs.release(); quads.release(); roots.release(); tri_hot.release(); tri_cold.release();
+            sph_hot.release(); sph_cold.release(); quad_hot.release(); quad_cold.release();
+        }
+    } spare;
+    hipEvent_t ev_blas_lane[NLANE] = {};
+    bool blas_double = true;
     uint64_t blas_builds = 0;
     hipEvent_t ev_render_done = nullptr;   // last trace launch finished (BLAS rebuilds wait on it)
     bool tlas_size_classes = false;     // option "tlas_classes": GPU TLAS keys start with an item size class (measured neutral)
@@ -311,6 +327,11 @@ struct rt_scene {
         raw_tris.release(); raw_sph.release(); raw_quad.release(); blas_roots.release(); inst_blas.release();
         blas_wide_refs.release();
         gpu_counts.release(); inst_params.release();
+        spare.release();
+        for (int q = 0; q < NLANE; q++) {
+            if (ev_blas_lane[q]) (void)hipEventDestroy(ev_blas_lane[q]);
+            if (spare.ev_lane[q]) (void)hipEventDestroy(spare.ev_lane[q]);
+        }
         if (ev_render_done) (void)hipEventDestroy(ev_render_done);
         for (int b = 0; b < NLANE; b++) {
             if (staging[b]) (void)hipHostFree(staging[b]);
@@ -597,6 +618,41 @@ rt_status alloc_buf(DevBuf<T> &buf, size_t n) {
 // RT_BUILD_LBVH: rebuild every BLAS on the GPU (prep -> Morton -> sort -> Karras -> boxes -> pairs ->
 // leaf-ordered primitive records), on the scene stream, after the last trace that read them.
 rt_status gpu_build_blas(rt_scene *s) {
+    if (s->blas_double && s->blas_builds > 0) {
+        // into the spare set: wait only for the traces that read it (each lane's last one), then swap it in
+        rt_scene::BlasSet &sp = s->spare;
+        rt_status st;
+        if (sp.pairs.n != s->blas_pairs.n || sp.tri_hot.n != s->tri_hot.n || sp.sph_hot.n != s->sph_hot.n ||
+            sp.quad_hot.n != s->quad_hot.n || sp.roots.n != s->blas_roots.n) {
+            HIP_TRY(drain(s));
+            sp.release();
+            if ((st = alloc_buf(sp.pairs, s->blas_pairs.n)) != RT_OK) return st;
+            if ((st = alloc_buf(sp.quads, s->blas_quads.n)) != RT_OK) return st;
+            if ((st = alloc_buf(sp.roots, s->blas_roots.n)) != RT_OK) return st;
+            if ((st = alloc_buf(sp.tri_hot, s->tri_hot.n)) != RT_OK) return st;
+            if ((st = alloc_buf(sp.tri_cold, s->tri_cold.n)) != RT_OK) return st;
+            if ((st = alloc_buf(sp.sph_hot, s->sph_hot.n)) != RT_OK) return st;
+            if ((st = alloc_buf(sp.sph_cold, s->sph_cold.n)) != RT_OK) return st;
+            if ((st = alloc_buf(sp.quad_hot, s->quad_hot.n)) != RT_OK) return st;
+            if ((st = alloc_buf(sp.quad_cold, s->quad_cold.n)) != RT_OK) return st;
+        }
+        for (int q = 0; q < rt_scene::NLANE; q++)      // created with the first set (gpu_setup_blas); never recorded: no wait
+            HIP_TRY(hipStreamWaitEvent(s->stream, sp.ev_lane[q], 0));
+        const RawPrimsGPU raw{s->raw_tris.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
+        const PrimOutGPU out{sp.tri_hot.p, sp.tri_cold.p, sp.sph_hot.p, sp.sph_cold.p, sp.quad_hot.p, sp.quad_cold.p};
+        HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
+        HIP_TRY(s->blas_builder->build(sp.pairs.p, sp.roots.p, s->gpu_counts.p, s->stream));
+        HIP_TRY(s->blas_builder->collapse_wide(sp.pairs.p, sp.roots.p, sp.quads.p, nullptr, s->stream));
+        HIP_TRY(s->blas_builder->gather_blas(raw, out, s->stream));
+        std::swap(s->blas_pairs, sp.pairs); std::swap(s->blas_quads, sp.quads); std::swap(s->blas_roots, sp.roots);
+        std::swap(s->tri_hot, sp.tri_hot); std::swap(s->tri_cold, sp.tri_cold);
+        std::swap(s->sph_hot, sp.sph_hot); std::swap(s->sph_cold, sp.sph_cold);
+        std::swap(s->quad_hot, sp.quad_hot); std::swap(s->quad_cold, sp.quad_cold);
+        for (int q = 0; q < rt_scene::NLANE; q++) std::swap(s->ev_blas_lane[q], sp.ev_lane[q]);
+        s->blas_dirty = false;
+        s->blas_builds++;
+        return RT_OK;
+    }
     if (s->blas_builds && s->ev_render_done) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_render_done, 0));
     for (int q = 0; q < rt_scene::NLANE; q++)           // "overlap": the other lane's trace may still be running
         if (s->blas_builds && s->ev_lane_done[q]) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_lane_done[q], 0));
@@ -643,6 +699,10 @@ rt_status gpu_setup_blas(rt_scene *s, const std::vector<LbvhSeg> &segs, const ui
     for (size_t i = 0; i < ib.size(); i++) ib[i] = s->inst[i].blas;
     if ((st = upload(s->inst_blas, ib)) != RT_OK) return st;
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
+    for (int q = 0; q < rt_scene::NLANE; q++) {       // "blas_double": every trace records its lane's event from now on
+        if (!s->ev_blas_lane[q]) HIP_TRY(hipEventCreateWithFlags(&s->ev_blas_lane[q], hipEventDisableTiming));
+        if (!s->spare.ev_lane[q]) HIP_TRY(hipEventCreateWithFlags(&s->spare.ev_lane[q], hipEventDisableTiming));
+    }
     s->blas_builds = 0;
     if ((st = gpu_build_blas(s)) != RT_OK) return st;
     // one-time readback for introspection (rt_scene_get_info)
@@ -1271,6 +1331,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         s->sched_valid[q] = true;
         out.order = s->order_ok[q] ? unit_order.p : nullptr;
         out.unit_cost = track ? unit_cost.p : nullptr;
+        out.cost_max = s->cost_max;
     }
     if (s->pending_copy >= 0) {                // the frame block's upload (and the lane's counter / queue reset)
         HIP_TRY(launch_frame_copy(s->frame_dev[s->pending_copy], s->staging_dev[s->pending_copy], s->frame_block,
@@ -1348,6 +1409,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     HIP_TRY(hipEventRecord(s->ev_used[s->active], stream));
     HIP_TRY(hipEventRecord(s->ev_render_done, stream));
     HIP_TRY(hipEventRecord(s->ev_lane_done[q], stream));
+    if (s->ev_blas_lane[q]) HIP_TRY(hipEventRecord(s->ev_blas_lane[q], stream));   // "blas_double": this set's reader
     if (o.flags & RT_RENDER_NO_SYNC) {
         if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; stats->update_wait_ms = s->update_wait_ms; }
         return RT_OK;
@@ -1448,6 +1510,12 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "costmap") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
         s->costmap_on = value == 1;
+    } else if (k == "blas_double") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "blas_double must be 0 or 1");
+        s->blas_double = value == 1;
+    } else if (k == "cost_max") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "cost_max must be 0 or 1");
+        s->cost_max = (uint32_t)value;
     } else if (k == "mix") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "mix must be 0 or 1");
         s->mix = (uint32_t)value;

@@ -62,6 +62,11 @@ constexpr int SPILL_DEPTH = 48;         // overflow entries in scratch (max dept
 #ifndef RT_LEAN_WIDE
 #define RT_LEAN_WIDE 0                  // 1: quad trees take the lean one-pop-per-step loop (lw_*; measured slower)
 #endif
+#ifndef RT_HEAVY_PRIO
+#define RT_HEAVY_PRIO 0                 // 1 (measured neutral, C3 -3 %, profiles/r02_ab_heavy_prio.jsonl): ordered walk: a wave holding pixels of a split (heaviest-class) unit
+                                        // issues at raised priority (s_setprio), so the launch's critical
+                                        // paths are not queued behind light waves that have slack
+#endif
 #ifndef RT_INLINE_INST
 #define RT_INLINE_INST 0                // 1: quad trees: a lane reaching a TLAS leaf enters the instance inside the
                                         // interior loop (instance record from LDS) instead of in a leaf round;
@@ -1537,7 +1542,18 @@ __device__ __forceinline__ void write_pixel(const OutputGPU &out, uint32_t oi, f
 #define RT_UNIT_COST_DEFER 1
 #endif
 // Lanes that finished a pixel in this shade step: one atomicAdd per distinct unit.
-__device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t unit, uint32_t c) {
+__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off, 64));
+    return v;
+}
+// option "cost_max": a unit's recorded cost is 64 x the steps of its longest path (the launch ends with
+// its longest paths, which a unit's summed cost can rank mid-order); else the sum over its paths
+__device__ __forceinline__ void unit_cost_flush(uint32_t *cost, uint32_t unit, uint32_t c, bool use_max) {
+    if (use_max) atomicMax(cost + unit, c);
+    else atomicAdd(cost + unit, c);
+}
+__device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t unit, uint32_t c, bool use_max) {
 #ifdef RT_AB_NO_UNIT_COST
     return;
 #endif
@@ -1546,8 +1562,8 @@ __device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t
         const uint32_t first = (uint32_t)__builtin_ctzll(m);
         const uint32_t u = __shfl(unit, (int)first, 64);
         const bool mine = fin && unit == u;
-        const uint32_t x = wave_sum(mine ? c : 0u);
-        if ((threadIdx.x & 63u) == first) atomicAdd(cost + u, x);
+        const uint32_t x = use_max ? wave_max(mine ? c : 0u) : wave_sum(mine ? c : 0u);
+        if ((threadIdx.x & 63u) == first) unit_cost_flush(cost, u, x, use_max);
         m &= ~(uint64_t)__ballot(mine);
     }
 }
@@ -1578,6 +1594,9 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     uint32_t rays = 0, pixels = 0;
 
     bool has = false;                  // lane owns a pixel
+    bool heavy = false;                // RT_HEAVY_PRIO: the lane's pixel came from a split (heavy) item
+    bool pool_heavy = false;           // wave-uniform: the current pool is a split item
+    bool prio_up = false;              // wave-uniform: priority currently raised
     uint32_t px_steps = 0;             // traversal steps spent on the lane's pixel (COUNT cost map, reorder)
     uint32_t item = 0, sample = 0, depth = 0;
     Rng rng;
@@ -1633,6 +1652,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                 pool_next = pool2_next;
                 pool_end = pool2_end;
                 pool2_next = pool2_end;
+                pool_heavy = false;
             } else if (pool_next >= pool_end) {
                 // bands: whole unit rows in frame mode (so a band can be walked in supertiles)
                 const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
@@ -1648,7 +1668,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                                       : p_end - p_begin;
                 }
                 if (RT_UNIT_COST_DEFER && track) {   // completes under the claim's wait
-                    unit_cost_add(out.unit_cost, pend_cost != 0, pend_unit, pend_cost);
+                    unit_cost_add(out.unit_cost, pend_cost != 0, pend_unit, pend_cost, out.cost_max != 0);
                     pend_cost = 0;
                 }
                 uint32_t b = 0;
@@ -1689,6 +1709,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     const uint32_t it2 = step > 1u && !out.mix && b + 1u < limit ? ob[1] : ~0u;
                     const uint32_t len = 64u >> (it & 3u);
                     pool_next = (it >> 4) * 64u + ((it >> 2) & 3u) * len;
+                    pool_heavy = (it & 3u) != 0u;
                     pool_end = pool_next + len;
                     if (it2 != ~0u) {
                         const uint32_t len2 = 64u >> (it2 & 3u);
@@ -1698,6 +1719,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                 } else {
                     b += p_begin;
                     pool_next = b;
+                    pool_heavy = false;
                     pool_end = min(b + grab, p_end);
                 }
                 if (!out.order && out.supertile && out.tile_count == 0 && grab == 64u) {
@@ -1725,6 +1747,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                 item = pool_next + rank;
                 if (map_item(out, cam, item, px, py, oi)) {
                     has = true;
+                    heavy = pool_heavy;
                     const uint32_t pixel = cam.pitch * py + px;                    // Kernel.cu:109
                     rng.init((uint64_t)pixel ^ cam.frame_seed, pixel);              // Kernel.cu:114
                     acc = mk(0.0f, 0.0f, 0.0f);
@@ -1759,6 +1782,14 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
         if (!__any(has)) {
             if (exhausted) break;
             continue;
+        }
+        if (RT_HEAVY_PRIO && out.order) {    // raised issue priority while the wave holds a heavy pixel
+            const bool want = __any(has && heavy);
+            if (want != prio_up) {
+                if (want) __builtin_amdgcn_s_setprio(2);
+                else __builtin_amdgcn_s_setprio(0);
+                prio_up = want;
+            }
         }
         // ---- traverse while enough lanes are busy
         for (;;) {
@@ -1841,19 +1872,20 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             if (track && fin) {
                 const uint32_t u = item >> 6;
                 if (u != pend_unit) {
-                    if (pend_cost) atomicAdd(out.unit_cost + pend_unit, pend_cost);
+                    if (pend_cost) unit_cost_flush(out.unit_cost, pend_unit, pend_cost, out.cost_max != 0);
                     pend_unit = u;
                     pend_cost = 0;
                 }
-                pend_cost += px_steps + 1u;
+                pend_cost = out.cost_max ? max(pend_cost, (px_steps + 1u) * 64u) : pend_cost + px_steps + 1u;
             }
         } else if (track) {
-            unit_cost_add(out.unit_cost, fin, item >> 6, px_steps + 1u);
+            unit_cost_add(out.unit_cost, fin, item >> 6, out.cost_max ? (px_steps + 1u) * 64u : px_steps + 1u,
+                          out.cost_max != 0);
         }
         DIAG_ADD(pc.shade, t_shade);
     }
 
-    if (RT_UNIT_COST_DEFER && track && pend_cost) atomicAdd(out.unit_cost + pend_unit, pend_cost);
+    if (RT_UNIT_COST_DEFER && track && pend_cost) unit_cost_flush(out.unit_cost, pend_unit, pend_cost, out.cost_max != 0);
     const uint32_t wr = wave_sum(rays);
     const uint32_t wp = wave_sum(pixels);
     if (COUNT) {

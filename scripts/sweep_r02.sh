@@ -87,6 +87,14 @@ if [[ $WHAT == retune ]]; then
     one sweep_retune.jsonl --shard 4/8
   done
 fi
+if [[ $WHAT == costmax ]]; then
+  # option "cost_max": claim order by a unit's longest path (x 64) instead of its summed cost; split levels
+  for rep in 1 2; do for o in "--opt cost_max=0" "--opt cost_max=1" "--opt cost_max=1 --opt split=3598" "--opt cost_max=1 --opt split=65535"; do
+    one sweep_costmax.jsonl $o
+    one sweep_costmax.jsonl $o --shard 4/8
+    one sweep_costmax.jsonl $o --config C3
+  done; done
+fi
 if [[ $WHAT == lds ]]; then
   # option "lds_scene": TLAS quads + instance hot records in LDS (1) vs HBM (0), alternating
   for rep in 1 2; do for v in 0 1; do
