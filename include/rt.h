@@ -334,6 +334,8 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "blas_double": RT_BUILD_LBVH rebuilds (option "rebuild", rt_scene_update_triangles): 1 = write a spare BLAS
  *                 set and swap it in, so a frame's rebuild overlaps the previous frame's trace (default 1;
  *                 0 = one set, a rebuild waits for every lane's trace)
+ *   "merge"     : "reorder": two adjacent 8x8 units whose recorded cost is below this level (0..16; levels are
+ *                 half-octaves of steps per pixel) become one 128-pixel claim item (default 6; 0 = off)
  *   "grid_pct"  : persistent grid as a percentage of the resident workgroup capacity (1..100; default 0 = auto:
  *                 100 for serialised launches, 50 with "overlap", so two lanes' launches run side by side)
  *   "lds_scene" : FAST quad-tree kernel: 1 = every workgroup copies the frame's TLAS quads and, when they fit

@@ -38,7 +38,7 @@ hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, co
 hipError_t launch_frame_copy(void *, const void *, size_t, unsigned long long *, uint32_t *, hipStream_t);
 hipError_t launch_primary_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *, hipStream_t);
 hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t,
-                           uint32_t, void *, const void *, size_t, unsigned long long *, hipStream_t);
+                           uint32_t, uint32_t, void *, const void *, size_t, unsigned long long *, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean, bool wide);
 hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t launch_instance_slot_order(const uint32_t *, const InstHot *, const InstCold *, uint32_t, InstHot *, InstCold *,
@@ -220,7 +220,11 @@ struct rt_scene {
     // given two of them runs both back to back; profiles/r02_sweep_claim_items.jsonl)
     uint32_t claim_items = 1;
     uint32_t mix = 0;
-    uint32_t cost_max = 0;          // option "cost_max": order units by their longest path (x 64), not their summed cost               // option "mix" (ordered walk): heaviest item first per refill, light fill after
+    uint32_t cost_max = 0;
+    // option "merge": two adjacent units below this cost level share one claim item (128 pixels): 6 (sky, about
+    // 4 steps per pixel) measured C2 0.203 -> 0.199 ms/frame; 8 or 10 (also the ground) put 128-pixel items at
+    // the end of the order and lengthen the tail (profiles/r02_sweep_merge.jsonl)
+    uint32_t merge = 6;          // option "cost_max": order units by their longest path (x 64), not their summed cost               // option "mix" (ordered walk): heaviest item first per refill, light fill after
     uint32_t supertile = 16;        // band walk order: st x st-unit supertiles (measured: 16 beats rows, 8 and 32)
     bool lean = false;              // FAST persistent kernel: LDS-only-stack traversal when the trees fit (measured slower on C2)
     uint32_t max_blas_height = 0;
@@ -1318,7 +1322,8 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
             const int pc = s->pending_copy;
             HIP_TRY(launch_schedule(unit_cost.p, unit_cost.p + out.units, unit_order.p, s->queue[q], rows, upr, out.queue_parts,
-                                    do_order, s->split & 0xFFu, (s->split >> 8) & 0xFFu, pc >= 0 ? s->frame_dev[pc] : nullptr,
+                                    do_order, s->split & 0xFFu, (s->split >> 8) & 0xFFu, s->merge,
+                                    pc >= 0 ? s->frame_dev[pc] : nullptr,
                                     pc >= 0 ? s->staging_dev[pc] : nullptr, pc >= 0 ? s->frame_block : 0,
                                     zero_lane ? lane_counters : nullptr, stream));
             zero_lane = false;
@@ -1513,6 +1518,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "blas_double") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "blas_double must be 0 or 1");
         s->blas_double = value == 1;
+    } else if (k == "merge") {
+        if (value < 0 || value > 16) return fail(RT_ERR_INVALID_ARGUMENT, "merge must be in 0..16");
+        s->merge = (uint32_t)value;
     } else if (k == "cost_max") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "cost_max must be 0 or 1");
         s->cost_max = (uint32_t)value;

@@ -43,7 +43,7 @@ constexpr uint32_t COPY_AHEAD = 2;             // 16-byte frame-block pieces loa
 __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__restrict__ cost, uint32_t *__restrict__ cost_prev,
                                                                  uint32_t *__restrict__ order, uint32_t *__restrict__ queue,
                                                                  uint32_t rows, uint32_t upr, uint32_t parts, uint32_t do_order,
-                                                                 uint32_t kh, uint32_t kq, uint4 *copy_dst,
+                                                                 uint32_t kh, uint32_t kq, uint32_t km, uint4 *copy_dst,
                                                                  const uint4 *copy_src, uint32_t copy_n16,
                                                                  unsigned long long *zero_counters) {
     __shared__ uint16_t cnt[SCHED_CLASSES * SCHED_THREADS];   // per-thread class item counts -> offsets (8 KB)
@@ -125,12 +125,21 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
         if (t == 0) queue[(QUEUE_MAX_PARTS + part) * QUEUE_STRIDE] = n;
         return;
     }
-    const uint32_t per = (n + SCHED_THREADS - 1) / SCHED_THREADS;
+    // even per-thread ranges: a merged pair of light units (option "merge") never spans two threads
+    const uint32_t per = ((n + SCHED_THREADS - 1) / SCHED_THREADS + 1) & ~1u;
     const uint32_t lo = b0 + min(n, t * per), hi = b0 + min(n, (t + 1) * per);
     const auto cls = [&](uint32_t u) { return (uint32_t)(nib[(u - gbase) >> 1] >> (4 * ((u - gbase) & 1u))) & 15u; };
     for (uint32_t c = 0; c < SCHED_CLASSES; c++) cnt[c * SCHED_THREADS + t] = 0;
+    // option "merge": two adjacent light units (levels below km, pair offset even) become one 128-pixel item
+    // in the pair's heavier class, so a claim over the sky / ground serves twice the pixels
+    const auto light = [&](uint32_t c) { return (SCHED_CLASSES - 1u) - c < km; };
     for (uint32_t u = lo; u < hi; u++) {
         const uint32_t c = cls(u);
+        if (km && u + 1 < hi && light(c) && light(cls(u + 1))) {
+            cnt[min(c, cls(u + 1)) * SCHED_THREADS + t] += 1;
+            u++;
+            continue;
+        }
         cnt[c * SCHED_THREADS + t] += (uint16_t)(1u << split_log2(c, kh, kq));
     }
     __syncthreads();
@@ -163,6 +172,14 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
     // pass 2: the band's items [4 b0, 4 b0 + items) — at most 4 per unit
     uint32_t *items = order + 4u * b0;
     for (uint32_t u = lo; u < hi; u++) {
+        if (km && u + 1 < hi && light(cls(u)) && light(cls(u + 1))) {        // merged pair: log2 pieces field 3
+            const uint32_t c = min(cls(u), cls(u + 1));
+            const uint32_t at = base[c] + cnt[c * SCHED_THREADS + t];
+            cnt[c * SCHED_THREADS + t] = (uint16_t)(at - base[c] + 1u);
+            items[at] = (u << 4) | 3u;
+            u++;
+            continue;
+        }
         const uint32_t c = cls(u), ls = split_log2(c, kh, kq);
         const uint32_t at = base[c] + cnt[c * SCHED_THREADS + t];
         cnt[c * SCHED_THREADS + t] = (uint16_t)(at - base[c] + (1u << ls));
@@ -176,11 +193,11 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
 // clears the costs and the queue heads (first launch of a layout: no costs recorded yet).
 // zero_counters (optional): CNT_NUM device counters cleared before the launch that follows.
 hipError_t launch_schedule(uint32_t *cost, uint32_t *cost_prev, uint32_t *order, uint32_t *queue, uint32_t rows, uint32_t upr,
-                           uint32_t parts, bool do_order, uint32_t k_half, uint32_t k_quarter, void *copy_dst,
+                           uint32_t parts, bool do_order, uint32_t k_half, uint32_t k_quarter, uint32_t k_merge, void *copy_dst,
                            const void *copy_src, size_t copy_bytes, unsigned long long *zero_counters, hipStream_t stream) {
     if (parts == 0 || parts > QUEUE_MAX_PARTS || copy_bytes % 16) return hipErrorInvalidValue;
     hipLaunchKernelGGL(schedule_kernel, dim3(parts), dim3(SCHED_THREADS), 0, stream, cost, cost_prev, order, queue, rows, upr,
-                       parts, do_order ? 1u : 0u, k_half, k_quarter, static_cast<uint4 *>(copy_dst),
+                       parts, do_order ? 1u : 0u, k_half, k_quarter, k_merge, static_cast<uint4 *>(copy_dst),
                        static_cast<const uint4 *>(copy_src), (uint32_t)(copy_bytes / 16), zero_counters);
     return hipGetLastError();
 }

@@ -1707,13 +1707,14 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     const uint32_t *ob = out.order + 4u * (p_begin >> 6) + b;
                     const uint32_t it = ob[0];
                     const uint32_t it2 = step > 1u && !out.mix && b + 1u < limit ? ob[1] : ~0u;
-                    const uint32_t len = 64u >> (it & 3u);
-                    pool_next = (it >> 4) * 64u + ((it >> 2) & 3u) * len;
-                    pool_heavy = (it & 3u) != 0u;
+                    // log2 pieces 3: two adjacent light units (schedule option "merge"), 128 pixels
+                    const uint32_t ls = it & 3u, len = ls == 3u ? 128u : 64u >> ls;
+                    pool_next = (it >> 4) * 64u + (ls == 3u ? 0u : ((it >> 2) & 3u) * len);
+                    pool_heavy = ls == 1u || ls == 2u;
                     pool_end = pool_next + len;
                     if (it2 != ~0u) {
-                        const uint32_t len2 = 64u >> (it2 & 3u);
-                        pool2_next = (it2 >> 4) * 64u + ((it2 >> 2) & 3u) * len2;
+                        const uint32_t ls2 = it2 & 3u, len2 = ls2 == 3u ? 128u : 64u >> ls2;
+                        pool2_next = (it2 >> 4) * 64u + (ls2 == 3u ? 0u : ((it2 >> 2) & 3u) * len2);
                         pool2_end = pool2_next + len2;
                     }
                 } else {

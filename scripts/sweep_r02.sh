@@ -95,6 +95,14 @@ if [[ $WHAT == costmax ]]; then
     one sweep_costmax.jsonl $o --config C3
   done; done
 fi
+if [[ $WHAT == merge ]]; then
+  # option "merge": adjacent light units share one claim item (levels below the value)
+  for rep in 1 2; do for v in 0 6 8 10; do
+    one sweep_merge.jsonl --opt merge=$v
+    one sweep_merge.jsonl --opt merge=$v --shard 4/8
+    one sweep_merge.jsonl --opt merge=$v --config C3
+  done; done
+fi
 if [[ $WHAT == lds ]]; then
   # option "lds_scene": TLAS quads + instance hot records in LDS (1) vs HBM (0), alternating
   for rep in 1 2; do for v in 0 1; do
