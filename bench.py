@@ -222,9 +222,10 @@ def main():
         b = frame % L if overlap else 0
         st = lanes[b].cuda_stream if overlap else stream
         fb = frame_bufs[b]
+        t_call = time.perf_counter()
         _, _, sts = r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=fb.data_ptr() if fb is not None else None,
                              stream=st, sync=sync, keep_counters=keep, tiles=tiles)
-        host_update.append((sts["update_ms"], sts["update_wait_ms"]))
+        host_update.append((sts["update_ms"], sts["update_wait_ms"], (time.perf_counter() - t_call) * 1e3))
 
     for f in range(args.warmup):
         step(f)
@@ -244,7 +245,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    timed_update = np.asarray(host_update[:args.steps], dtype=np.float64).reshape(-1, 2)
+    timed_update = np.asarray(host_update[:args.steps], dtype=np.float64).reshape(-1, 3)
     acc, kernel_ms = r.collect()                           # device counters + HIP-event kernel times
     rays = int(acc["rays"])
     assert len(kernel_ms) == args.steps, (len(kernel_ms), args.steps)
@@ -331,6 +332,10 @@ def main():
             # and the part of it spent blocked on the GPU (a staging buffer still in use)
             "host_update_ms_median": round(float(np.median(timed_update[:, 0])), 4),
             "host_update_wait_ms_median": round(float(np.median(timed_update[:, 1])), 4),
+            # the whole rt_render call of a timed (pipelined) frame on the host, its waits included: when it is
+            # close to ms_per_step the frame rate is bound by the host's per-frame work, not by the GPU
+            "host_call_ms_median": round(float(np.median(timed_update[:, 2])), 4),
+            "host_busy_ms_median": round(float(np.median(timed_update[:, 2] - timed_update[:, 1])), 4),
             "kernel_ms": round(serial_kernel_ms, 4),
             "kernel_ms_overlapped": round(avg_kernel_ms, 4),
             "roofline": {

@@ -336,6 +336,13 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 0 = one set, a rebuild waits for every lane's trace)
  *   "merge"     : "reorder": two adjacent 8x8 units whose recorded cost is below this level (0..16; levels are
  *                 half-octaves of steps per pixel) become one 128-pixel claim item (default 6; 0 = off)
+ *   "group"     : RT_BUILD_SAH with a host-built TLAS: triangle instances with bit-identical transforms (each
+ *                 with a BLAS of its own) share one SAH BLAS over all their triangles, entered as one TLAS item
+ *                 while every member keeps that transform (default 1; set before rt_scene_build; hits report
+ *                 the member instance; 0 = one TLAS item per instance)
+ *   "drain"     : persistent kernel: once a wave's claims fail (queue dry), a lane whose path segment ended is
+ *                 shaded when 1/drain of the wave's remaining paths wait (1..64; default 0 = when "threshold"
+ *                 lanes wait; results identical)
  *   "grid_pct"  : persistent grid as a percentage of the resident workgroup capacity (1..100; default 0 = auto:
  *                 100 for serialised launches, 50 with "overlap", so two lanes' launches run side by side)
  *   "lds_scene" : FAST quad-tree kernel: 1 = every workgroup copies the frame's TLAS quads and, when they fit

@@ -92,7 +92,7 @@ struct alignas(16) TriHot {         // 48 B: Moller-Trumbore operands (Triangle.
 struct alignas(16) TriCold {        // 48 B: vertex normals + material + caller index
     float n0[3]; uint32_t material;     // material = slot | (type << 31)
     float n1[3]; uint32_t orig_index;
-    float n2[3]; uint32_t pad;
+    float n2[3]; uint32_t pad;          // a group's merged BLAS (option "group"): caller instance + 1, else 0
 };
 struct alignas(16) SphereHot {      // 16 B (Sphere.cu:4-49)
     float center[3]; float radius;
@@ -230,6 +230,8 @@ struct OutputGPU {
     uint32_t claim_items;           // ordered walk ("reorder"): consecutive order items per queue atomic (1..2)
     uint32_t mix;                   // ordered walk: a refill's first claim takes the band's heaviest item (front),
                                     // its further claims the lightest (back): one 64-bit head {front, back}
+    uint32_t drain;                 // option "drain": once the wave's queue is dry, shade when 1/drain of its
+                                    // remaining paths wait (0: when `threshold` lanes wait, as before)
     uint32_t supertile;             // frame mode, grab 64: walk bands in supertile x supertile units (0 = rows)
     unsigned long long *timeline;   // TIMELINE_WORDS per wave (rt.h, rt_scene_debug_read)
     uint32_t *costmap;              // COUNT launches: traversal rounds per output pixel (debug)

@@ -10,11 +10,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -94,6 +96,19 @@ struct BlasHost {
     FlatTree flat;
     FlatWide wide;                 // quad form (option "wide"; host-built modes)
     uint32_t pair_base, slot_base;
+    // a group's merged BLAS (option "group"): the members' triangle ranges {first, count, instance}
+    std::vector<std::array<uint32_t, 3>> members;
+};
+
+// Option "group" (RT_BUILD_SAH, host-built TLAS): triangle instances whose transforms are bit-identical
+// (the reference's VTK particles all carry one fixed transform, VTKReader.cu:204-215) share one instance
+// space, so one SAH BLAS over all their triangles replaces their overlapping instance boxes in the TLAS.
+// A frame uses the group while every member still has the group's transform (and its triangles and
+// bounds were not replaced since the build); otherwise that frame's TLAS takes the members one by one.
+struct InstGroup {
+    InstState st;                  // the group as one instance: the shared transform, the union of the boxes
+    std::vector<uint32_t> members;
+    bool valid = true;
 };
 
 template <typename T>
@@ -133,6 +148,11 @@ struct rt_scene {
 
     std::vector<InstState> inst;
     std::vector<BlasHost> blas;
+    size_t blas_own = 0;            // per-instance BLASes; the groups' merged BLASes follow them in `blas`
+    std::vector<InstGroup> groups;  // option "group": TLAS item n + g is group g
+    std::vector<uint32_t> group_of; // per instance: its group + 1 (0: none)
+    bool group_inst = true;         // option "group" (set before the build)
+    uint32_t frame_items[8] = {};   // per frame block: TLAS items (= instance records when staged by slot)
     Tree tlas;
     FlatTree tlas_flat;
     FlatWide tlas_wide;
@@ -224,7 +244,11 @@ struct rt_scene {
     // option "merge": two adjacent units below this cost level share one claim item (128 pixels): 6 (sky, about
     // 4 steps per pixel) measured C2 0.203 -> 0.199 ms/frame; 8 or 10 (also the ground) put 128-pixel items at
     // the end of the order and lengthen the tail (profiles/r02_sweep_merge.jsonl)
-    uint32_t merge = 6;          // option "cost_max": order units by their longest path (x 64), not their summed cost               // option "mix" (ordered walk): heaviest item first per refill, light fill after
+    uint32_t merge = 6;
+    // option "drain": after a wave's last failed claim, a lane whose segment ended shades as soon as 1/drain of the
+    // wave's remaining paths wait, instead of waiting for `threshold` lanes (which, with fewer paths left than
+    // the threshold, meant waiting for every other lane's segment)
+    uint32_t drain = 0;
     uint32_t supertile = 16;        // band walk order: st x st-unit supertiles (measured: 16 beats rows, 8 and 32)
     bool lean = false;              // FAST persistent kernel: LDS-only-stack traversal when the trees fit (measured slower on C2)
     uint32_t max_blas_height = 0;
@@ -511,8 +535,21 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         return RT_OK;
     }
     // TLAS::constructTLAS over transformed instance boxes (Renderer.cu:275, TLAS.cu:4-129)
-    std::vector<BuildItem> items(s->inst.size());
-    for (size_t i = 0; i < items.size(); i++) items[i] = {s->inst[i].tbox, s->inst[i].tcentroid, (uint32_t)i};
+    // option "group": a group still holding its transform is one item (n + g), else its members are
+    std::vector<uint8_t> intact(s->groups.size(), 0);
+    for (size_t g = 0; g < s->groups.size(); g++) {
+        const InstGroup &G = s->groups[g];
+        bool ok = G.valid;
+        for (size_t k = 0; ok && k < G.members.size(); k++)
+            ok = std::memcmp(&s->inst[G.members[k]].x, &G.st.x, sizeof(rt_xform)) == 0;
+        intact[g] = ok;
+    }
+    std::vector<BuildItem> items;
+    items.reserve(s->inst.size() + s->groups.size());
+    for (size_t i = 0; i < s->inst.size(); i++)
+        if (!s->group_of[i] || !intact[s->group_of[i] - 1]) items.push_back({s->inst[i].tbox, s->inst[i].tcentroid, (uint32_t)i});
+    for (size_t g = 0; g < s->groups.size(); g++)
+        if (intact[g]) items.push_back({s->groups[g].st.tbox, s->groups[g].st.tcentroid, (uint32_t)(s->inst.size() + g)});
     s->tlas = s->build_mode == RT_BUILD_SAH ? build_sah_tree(std::move(items), s->tlas_leaf)
                                             : build_median_tree(std::move(items), TLAS_LEAF_CAP, hm::tlas_axis_state(s->build_seed, frame));
     s->tlas_flat = flatten_tree(s->tlas, 0, 0, 0, false);
@@ -530,10 +567,12 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
     std::memcpy(st + s->off_pairs, s->tlas_flat.pairs.data(), s->tlas_flat.pairs.size() * sizeof(NodePair));
     std::memcpy(st + s->off_slots, s->tlas.refs.data(), s->tlas.refs.size() * sizeof(uint32_t));
     // instance records in TLAS leaf-slot order (SceneGPU::inst_by_slot): record j = the instance in slot j
-    const size_t nrec = s->inst_by_slot ? s->tlas.refs.size() : s->inst.size();
+    const size_t nrec = s->inst_by_slot ? s->tlas.refs.size() : s->inst.size() + s->groups.size();
     s->block_by_slot[b] = s->inst_by_slot;
+    s->frame_items[b] = (uint32_t)nrec;
     for (size_t j = 0; j < nrec; j++) {
-        const InstState &in = s->inst[s->inst_by_slot ? s->tlas.refs[j] : j];
+        const size_t id = s->inst_by_slot ? s->tlas.refs[j] : j;
+        const InstState &in = id < s->inst.size() ? s->inst[id] : s->groups[id - s->inst.size()].st;
         const BlasHost &bl = s->blas[in.blas];
         store_rows(hot[j].inv, in.inv);
         std::memcpy(hot[j].root_box, bl.flat.root_box, sizeof hot[j].root_box);
@@ -576,7 +615,7 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.sph_hot = s->sph_hot.p; g.sph_cold = s->sph_cold.p;
     g.quad_hot = s->quad_hot.p; g.quad_cold = s->quad_cold.p;
     g.materials = s->materials.p;
-    g.instance_count = (uint32_t)s->inst.size();
+    g.instance_count = s->gpu_tlas() ? (uint32_t)s->inst.size() : s->frame_items[b];   // instance records
     g.rough_count = (uint32_t)s->roughs.size();
     g.material_count = (uint32_t)(s->materials.n / 4);
     // option "lds_scene": the quads the frame's TLAS refs can index (host-built: this frame's quad count;
@@ -792,6 +831,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     s->build_mode = mode;
     s->inst.clear();
     s->blas.clear();
+    s->groups.clear();
+    s->group_of.clear();
     s->max_blas_height = 0;
     for (bool &v : s->block_by_slot) v = false;    // a rebuild may change the mode: no block is slot-ordered yet
 
@@ -867,6 +908,71 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         }
         s->inst.push_back(in);
     }
+    s->blas_own = s->blas.size();
+    s->group_of.assign(s->inst.size(), 0u);
+    if (mode == RT_BUILD_SAH && s->group_inst && !s->gpu_tlas()) {
+        // option "group": triangle instances with bit-identical transforms and a BLAS of their own
+        std::vector<uint32_t> users(s->blas.size(), 0u);
+        for (const InstState &in : s->inst) users[in.blas]++;
+        std::map<std::string, std::vector<uint32_t>> by_xform;
+        for (size_t i = 0; i < s->inst.size(); i++) {
+            const InstState &in = s->inst[i];
+            if (in.ptype != RT_PRIM_TRIANGLE || users[in.blas] != 1) continue;
+            const rt_xform &x = s->inst_desc[i].xform;
+            by_xform[std::string(reinterpret_cast<const char *>(&x), sizeof x)].push_back((uint32_t)i);
+        }
+        for (auto &kv : by_xform) {
+            if (kv.second.size() < 2) continue;
+            InstGroup g;
+            g.members = kv.second;
+            std::vector<std::array<uint32_t, 3>> ranges;
+            for (uint32_t i : g.members) ranges.push_back({s->inst[i].pindex, s->inst[i].pcount, i});
+            std::sort(ranges.begin(), ranges.end());
+            bool disjoint = true;          // every triangle of the group belongs to exactly one member
+            for (size_t k = 1; k < ranges.size(); k++)
+                disjoint = disjoint && ranges[k][0] >= ranges[k - 1][0] + ranges[k - 1][1];
+            if (!disjoint) continue;
+            const uint32_t gi = (uint32_t)s->groups.size();
+            uint64_t total = 0;
+            double c[3] = {0, 0, 0};
+            BlasHost bh;
+            bh.type = RT_PRIM_TRIANGLE;
+            for (size_t k = 0; k < g.members.size(); k++) {
+                const InstState &m = s->inst[g.members[k]];
+                g.st.box = k ? hm::Box::merge(g.st.box, m.box) : m.box;
+                for (int a = 0; a < 3; a++) c[a] += m.centroid[a];
+                total += m.pcount;
+                bh.members.push_back({m.pindex, m.pcount, g.members[k]});
+                s->group_of[g.members[k]] = gi + 1;
+            }
+            if ((uint64_t)slot_base[RT_PRIM_TRIANGLE] + total >= MAX_LEAF_SLOTS)
+                return fail(RT_ERR_UNSUPPORTED, "too many primitives of one type (2^26 leaf slots)");
+            g.st.ptype = RT_PRIM_TRIANGLE;
+            g.st.pindex = 0;
+            g.st.pcount = (uint32_t)total;
+            g.st.centroid = hm::v3((float)(c[0] / g.members.size()), (float)(c[1] / g.members.size()),
+                                   (float)(c[2] / g.members.size()));
+            g.st.x = s->inst_desc[g.members[0]].xform;
+            std::vector<BuildItem> items;
+            items.reserve(total);
+            for (const auto &mr : bh.members)
+                for (uint32_t k = 0; k < mr[1]; k++)
+                    items.push_back({prim_box(s, RT_PRIM_TRIANGLE, mr[0] + k), prim_centroid(s, RT_PRIM_TRIANGLE, mr[0] + k), mr[0] + k});
+            bh.tree = build_sah_tree(std::move(items), s->blas_leaf);
+            bh.pair_base = pair_base;
+            bh.slot_base = slot_base[RT_PRIM_TRIANGLE];
+            bh.flat = flatten_tree(bh.tree, pair_base, bh.slot_base, RT_PRIM_TRIANGLE, true);
+            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, RT_PRIM_TRIANGLE, true, s->wide_merge);
+            quad_base += (uint32_t)bh.wide.quads.size();
+            s->max_blas_height = std::max(s->max_blas_height, bh.flat.height);
+            pair_base += (uint32_t)bh.flat.pairs.size();
+            slot_base[RT_PRIM_TRIANGLE] += (uint32_t)total;
+            std::sort(bh.members.begin(), bh.members.end());
+            g.st.blas = (uint32_t)s->blas.size();
+            s->blas.push_back(std::move(bh));
+            s->groups.push_back(std::move(g));
+        }
+    }
 
     std::vector<float> mats;
     for (const auto &r : s->roughs) { mats.push_back(r.albedo.x); mats.push_back(r.albedo.y); mats.push_back(r.albedo.z); mats.push_back(0.0f); }
@@ -905,6 +1011,10 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
                 }
                 c.material = material_slot(s, t.material_type, t.material_index, mat_ok);
                 c.orig_index = pi;
+                if (!bh.members.empty()) {        // a group's BLAS: the caller instance holding triangle pi, + 1
+                    auto it = std::upper_bound(bh.members.begin(), bh.members.end(), std::array<uint32_t, 3>{pi, ~0u, ~0u});
+                    c.pad = (*(it - 1))[2] + 1u;
+                }
                 th.push_back(h); tc.push_back(c);
             } else if (bh.type == RT_PRIM_SPHERE) {
                 const rt_sphere &sp = s->spheres[pi];
@@ -938,8 +1048,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     }
     if ((st = upload(s->materials, mats)) != RT_OK) return st;
 
-    // per-frame double buffers
-    const size_t n = s->inst.size();
+    // per-frame double buffers (sized for every instance and every group as a TLAS item)
+    const size_t n = s->inst.size() + s->groups.size();
     s->off_root = 0;
     s->off_pairs = 64;
     s->off_slots = align16(s->off_pairs + n * sizeof(NodePair));
@@ -966,7 +1076,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             roots[b].height = s->blas[b].flat.height;
             wide_refs[b] = s->blas[b].wide.root_ref;
         }
-        for (size_t i = 0; i < n; i++) ib[i] = s->inst[i].blas;
+        for (size_t i = 0; i < s->inst.size(); i++) ib[i] = s->inst[i].blas;
         if ((st = upload(s->blas_roots, roots)) != RT_OK) return st;
         if ((st = upload(s->blas_wide_refs, wide_refs)) != RT_OK) return st;
         if ((st = upload(s->inst_blas, ib)) != RT_OK) return st;
@@ -1021,7 +1131,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     s->active = -1;
 
     // initial transforms, then the frame-0 update + TLAS (Renderer.cu:110-111, 148-150)
-    for (size_t i = 0; i < n; i++) instance_update(s->inst[i], s->inst_desc[i].xform);
+    for (size_t i = 0; i < s->inst.size(); i++) instance_update(s->inst[i], s->inst_desc[i].xform);
+    for (InstGroup &g : s->groups) instance_update(g.st, g.st.x);
     s->built = true;
     return frame_update(s, 0, s->stream);
 }
@@ -1255,6 +1366,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         out.grab = s->grab;
         out.claim_items = s->claim_items;
         out.mix = s->mix;
+        out.drain = s->drain;
         out.supertile = s->supertile;
         if (s->timeline_on) {
             const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false, false)
@@ -1524,6 +1636,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "cost_max") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "cost_max must be 0 or 1");
         s->cost_max = (uint32_t)value;
+    } else if (k == "drain") {
+        if (value < 0 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "drain must be in 0..64");
+        s->drain = (uint32_t)value;
     } else if (k == "mix") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "mix must be 0 or 1");
         s->mix = (uint32_t)value;
@@ -1553,6 +1668,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "split") {
         if (value < 0 || value > 0xFFFF) return fail(RT_ERR_INVALID_ARGUMENT, "split must be k_half | k_quarter << 8");
         s->split = (uint32_t)value;
+    } else if (k == "group") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "group must be 0 or 1");
+        s->group_inst = value == 1;                   // next rt_scene_build
     } else if (k == "blas_leaf") {
         if (value < 1 || value > (int64_t)SAH_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "blas_leaf must be in 1..4");
         s->blas_leaf = (uint32_t)value;
@@ -1767,6 +1885,9 @@ rt_status rt_scene_update_instances(rt_scene *s, size_t first, size_t count, con
         }
         instance_update(in, d[k].xform);
         if (s->gpu_tlas()) s->inst_dirty[i] = 1;
+        // option "group": the group's box and transform were taken at the build; its members go back to
+        // their own TLAS items for good
+        if (s->group_of[i]) s->groups[s->group_of[i] - 1].valid = false;
     }
     return RT_OK;
 }
@@ -1784,7 +1905,7 @@ void rt_scene_destroy(rt_scene *s) { delete s; }
 rt_status rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
     if (!s || !info) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
     std::memset(info, 0, sizeof *info);
-    info->blas_count = s->blas.size();
+    info->blas_count = s->blas_own;     // per-instance BLASes (the groups' merged ones are not counted)
     info->blas_node_pairs = s->blas_pair_count;
     info->blas_leaves = s->blas_leaf_count;
     info->tlas_node_pairs = s->tlas_flat.pairs.size();

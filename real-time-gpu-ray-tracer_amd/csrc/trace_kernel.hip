@@ -1263,7 +1263,7 @@ __device__ __forceinline__ bool trace(const SceneGPU &sc, const f3 &o, const f3 
 }
 
 // Record fields the shading needs (HitRecord, BasicTypes.cuh:19-31), world space.
-struct Surface { f3 p, n; uint32_t material; uint32_t orig; };
+struct Surface { f3 p, n; uint32_t material; uint32_t orig; uint32_t member; };   // member: group BLAS (option "group"): instance + 1
 
 // Recompute the hit point / normal of the closest hit exactly as the primitive hit function and
 // Instance::hit (Instance.cu:41-45) would have stored them.
@@ -1294,7 +1294,7 @@ __device__ __forceinline__ Surface finalize(const SceneGPU &sc, const f3 &wo, co
         const TriCold &T = sc.tri_cold[h.slot];
         const f3 nn = unit(add(add(scl(ld3(T.n0), (1.0f - h.u) - h.v), scl(ld3(T.n1), h.u)), scl(ld3(T.n2), h.v)));
         n = dot(ld, nn) < 0.0f ? nn : neg(nn);
-        s.material = T.material; s.orig = T.orig_index;
+        s.material = T.material; s.orig = T.orig_index; s.member = T.pad;
     } else if (h.ptype == RT_PRIM_SPHERE) {                                    // Sphere.cu:37-39
 #if !RT_EXACT
         const SphereHot S = LDSS ? lds_or_global(sc.lds_sph_hot, sc.sph_hot, h.slot) : sc.sph_hot[h.slot];
@@ -1305,7 +1305,7 @@ __device__ __forceinline__ Surface finalize(const SceneGPU &sc, const f3 &wo, co
 #endif
         const f3 outward = unit(sub(p, ld3(S.center)));
         n = dot(ld, outward) < 0.0f ? outward : neg(outward);
-        s.material = C.material; s.orig = C.orig_index;
+        s.material = C.material; s.orig = C.orig_index; s.member = 0u;
     } else {                                                                   // Parallelogram.cu:42-43
 #if !RT_EXACT
         const float4 qn4 = LDSS && sc.lds_q_hot != LDS_NONE ? lds_scene[sc.lds_q_hot + h.slot * LDS_QPRIM_F4]
@@ -1318,7 +1318,7 @@ __device__ __forceinline__ Surface finalize(const SceneGPU &sc, const f3 &wo, co
         const f3 qn = ld3(Q.n);
 #endif
         n = dot(ld, qn) < 0.0f ? qn : neg(qn);
-        s.material = C.material; s.orig = C.orig_index;
+        s.material = C.material; s.orig = C.orig_index; s.member = 0u;
     }
     s.p = xf_point(IC.fwd, p);
     s.n = unit(xf_vector(IC.nrm, n));
@@ -1793,11 +1793,16 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             }
         }
         // ---- traverse while enough lanes are busy
+        // option "drain": with the queue dry no idle lane can be refilled, and fewer paths than `threshold`
+        // may be left: a lane whose segment ended shades once 1/drain of the remaining paths wait
+        const uint32_t shade_at = exhausted && out.drain
+                                 ? max(1u, min(threshold, (uint32_t)__popcll(__ballot(has)) / out.drain))
+                                 : threshold;
         for (;;) {
             const uint64_t tr = __ballot(T.tracing);
             if (tr == 0) break;
             const uint64_t want = __ballot(!T.tracing && (has || !exhausted));
-            if ((uint32_t)__popcll(want) >= threshold) break;
+            if ((uint32_t)__popcll(want) >= shade_at) break;
 #if !RT_EXACT
             if constexpr (LEAN) lean_round<COUNT>(T, sc, cnt, pc, px_steps, COUNT || track);
             else if constexpr (WIDE && RT_LEAN_WIDE) lw_round<COUNT>(T, sc, spill, cnt, pc, px_steps, COUNT || track);
@@ -1949,7 +1954,8 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const fl
     rt_hit r;
     if (trace<false>(sc, o, d, h, T, spill, cnt)) {
         const Surface s = finalize(sc, o, d, h);
-        r.t = h.t; r.instance = sc.inst_by_slot ? sc.tlas_slots[h.inst] : h.inst; r.primitive_type = h.ptype; r.primitive_index = s.orig;
+        r.t = h.t; r.instance = s.member ? s.member - 1u : (sc.inst_by_slot ? sc.tlas_slots[h.inst] : h.inst);
+        r.primitive_type = h.ptype; r.primitive_index = s.orig;
         r.point.x = s.p.x; r.point.y = s.p.y; r.point.z = s.p.z;
         r.normal.x = s.n.x; r.normal.y = s.n.y; r.normal.z = s.n.z;
         const bool metal = (s.material & MAT_METAL_BIT) != 0;

@@ -9,7 +9,7 @@ one() {  # out args...
   timeout -k 10 240 python bench.py --no-cpu-baseline "$@" > gpurun_out/_one.log 2>&1
   local rc=$?
   if [ $rc -ne 0 ]; then echo "rc=$rc for $*"; tail -3 gpurun_out/_one.log; exit $rc; fi
-  tail -1 gpurun_out/_one.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'args': '$*', 'hwq': '${GPU_MAX_HW_QUEUES:-}', 'value': d['value'], 'ms_per_step': d['ms_per_step'], 'kernel_ms': d['kernel_ms'], 'kernel_ms_overlapped': d['kernel_ms_overlapped'], 'lat': d['frame_latency_ms_median'], 'host_update_ms': d.get('host_update_ms_median'), 'host_wait_ms': d.get('host_update_wait_ms_median')}))" | tee -a "gpurun_out/$out"
+  tail -1 gpurun_out/_one.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print(json.dumps({'args': '$*', 'hwq': '${GPU_MAX_HW_QUEUES:-}', 'value': d['value'], 'ms_per_step': d['ms_per_step'], 'kernel_ms': d['kernel_ms'], 'kernel_ms_overlapped': d['kernel_ms_overlapped'], 'lat': d['frame_latency_ms_median'], 'host_update_ms': d.get('host_update_ms_median'), 'host_wait_ms': d.get('host_update_wait_ms_median'), 'host_call_ms': d.get('host_call_ms_median'), 'host_busy_ms': d.get('host_busy_ms_median')}))" | tee -a "gpurun_out/$out"
 }
 if [[ $WHAT == lanes || $WHAT == all ]]; then
   for rep in 1 2; do for L in 2 3 4; do for rs in 0 8 16; do one sweep_lanes.jsonl --overlap $L --opt reserve=$rs; done; done; done
@@ -76,6 +76,32 @@ if [[ $WHAT == lds2 ]]; then
     one sweep_lds2.jsonl --opt lds_scene=$v --config C3
     one sweep_lds2.jsonl --opt lds_scene=$v --build lbvh
   done; done
+fi
+if [[ $WHAT == drain ]]; then
+  # option "drain": after a wave's queue is dry, shade when 1/drain of its remaining paths wait
+  for rep in 1 2; do for v in ${DRAIN_VALUES:-0 1 2 4 64}; do
+    one sweep_drain.jsonl --opt drain=$v --overlap 1
+    one sweep_drain.jsonl --opt drain=$v
+    one sweep_drain.jsonl --opt drain=$v --shard 4/8
+    one sweep_drain.jsonl --opt drain=$v --config C3
+  done; done
+fi
+if [[ $WHAT == group ]]; then
+  # option "group": instances with identical transforms share one SAH BLAS (one TLAS item)
+  for rep in 1 2; do for v in 0 1; do
+    one sweep_group.jsonl --pre-opt group=$v --overlap 1
+    one sweep_group.jsonl --pre-opt group=$v
+    one sweep_group.jsonl --pre-opt group=$v --shard 4/8
+    one sweep_group.jsonl --pre-opt group=$v --config C3
+    one sweep_group.jsonl --pre-opt group=$v --config C4 --shard 3/8
+  done; done
+fi
+if [[ $WHAT == host ]]; then
+  # host-side time per pipelined frame (host_busy: the rt_render call minus its waits on the GPU)
+  one sweep_host.jsonl
+  one sweep_host.jsonl --shard 4/8
+  one sweep_host.jsonl --config C4 --shard 3/8
+  one sweep_host.jsonl --overlap 1 --shard 4/8
 fi
 if [[ $WHAT == retune ]]; then
   # knobs re-checked after lds_scene / grid_pct / chained root leaves: refill threshold, split levels, reorder period

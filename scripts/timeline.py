@@ -62,6 +62,7 @@ def main():
     ap.add_argument("--threshold", type=int, default=8)
     ap.add_argument("--out", default="gpurun_out/timeline.npz")
     ap.add_argument("--opt", action="append", default=[], help="extra scene option key=value")
+    ap.add_argument("--pre-opt", action="append", default=[], help="scene option key=value set before the build")
     ap.add_argument("--shard", default=None, help="R/N: time rank R's 64x64-tile share of an N-rank split")
     a = ap.parse_args()
     tiles = (64, 64) + tuple(int(v) for v in a.shard.split("/")) if a.shard else None
@@ -70,8 +71,11 @@ def main():
     torch.cuda.set_device(0)
     cfg = scenes.CONFIGS[a.config]
     fb = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda")
-    r = Renderer(scenes.config_scene(cfg)).build_acceleration_structure(0, mode=a.build).configure_camera(
-        cfg.width, cfg.height)
+    r = Renderer(scenes.config_scene(cfg))
+    for kv in a.pre_opt:
+        k, v = kv.split("=")
+        r.set_option(k, int(v))
+    r.build_acceleration_structure(0, mode=a.build).configure_camera(cfg.width, cfg.height)
     r.set_option("threshold", a.threshold)
     for kv in a.opt:
         k, v = kv.split("=")

@@ -285,7 +285,10 @@ def test_reorder_schedule_is_byte_identical(gpu_lib, exact):
     for f in range(4):
         ref[f] = r.render(f, exact=exact, want_rgb=True)
     tref = r.render(3, exact=exact, tiles=(64, 64, 1, 3), skip_update=True)[0]
+    # merge 0: the order's structure below is the split-only one (merged light pairs, option "merge", are
+    # covered by test_claim_options_byte_identical)
     r.set_option("reorder", 1).set_option("split", 8 | 10 << 8).set_option("reorder_period", 1)
+    r.set_option("merge", 0)
     ux, rows = W // 8, H // 8
     for f in range(4):
         rgba, rgb, st = r.render(f, exact=exact, want_rgb=True)
@@ -404,7 +407,8 @@ def test_reorder_period_byte_identical(gpu_lib, period, lanes):
 
 
 @pytest.mark.parametrize("opts", [{"mix": 1}, {"claim_items": 2}, {"mix": 1, "claim_items": 2}, {"grid_pct": 30},
-                                  {"merge": 8}, {"merge": 16}, {"merge": 8, "claim_items": 2}])
+                                  {"merge": 8}, {"merge": 16}, {"merge": 8, "claim_items": 2},
+                                  {"drain": 1}, {"drain": 4}, {"drain": 64}])
 def test_claim_options_byte_identical(gpu_lib, opts):
     """Claim-order options of the persistent kernel ("mix": heaviest item from a band's front, light fill
     from its back; "claim_items" 2; a 30 % grid): which wave traces a pixel changes, the pixel's result
