@@ -340,6 +340,8 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 with a BLAS of its own) share one SAH BLAS over all their triangles, entered as one TLAS item
  *                 while every member keeps that transform (default 1; set before rt_scene_build; hits report
  *                 the member instance; 0 = one TLAS item per instance)
+ *   "lds_blas"  : with "lds_scene" 2 and "group": the top levels of the first group's BLAS (quads numbered level
+ *                 by level) fill the rest of the LDS scene region (default 1; 0 = from HBM; results identical)
  *   "drain"     : persistent kernel: once a wave's claims fail (queue dry), a lane whose path segment ended is
  *                 shaded when 1/drain of the wave's remaining paths wait (1..64; default 0 = when "threshold"
  *                 lanes wait; results identical)

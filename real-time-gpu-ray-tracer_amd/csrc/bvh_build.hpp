@@ -394,8 +394,10 @@ struct FlatWide {
 // merge_cap > 0: a binary subtree holding <= merge_cap items (<= 4, the leaf ref's count field) becomes
 // one leaf — its leaves are contiguous slots (the builders emit leaves depth-first, left first).  Fewer,
 // fuller leaves mean fewer leaf rounds per ray for the same primitive tests.
+// level_order: quads numbered level by level (breadth first), so the first k quads are the tree's top
+// levels (the LDS-resident part of a group's BLAS); otherwise depth first
 inline FlatWide flatten_tree_wide(const Tree &t, uint32_t quad_base, uint32_t slot_base, uint32_t ptype, bool blas,
-                                  uint32_t merge_cap = 0) {
+                                  uint32_t merge_cap = 0, bool level_order = false) {
     FlatWide f;
     const uint32_t n = (uint32_t)t.nodes.size();
     if (n == 0) return f;
@@ -411,10 +413,16 @@ inline FlatWide flatten_tree_wide(const Tree &t, uint32_t quad_base, uint32_t sl
     if (is_leaf(0)) { f.root_ref = leaf_ref(0); return f; }
     struct Todo { uint32_t node, quad, depth; };
     std::vector<Todo> todo{{0u, 0u, 1u}};
+    size_t head = 0;                               // level order: todo is a FIFO from `head`
     f.quads.emplace_back();
-    while (!todo.empty()) {
-        const Todo w = todo.back();
-        todo.pop_back();
+    while (todo.size() > head) {
+        Todo w;
+        if (level_order) {
+            w = todo[head++];
+        } else {
+            w = todo.back();
+            todo.pop_back();
+        }
         f.height = std::max(f.height, w.depth);
         uint32_t ch[4] = {t.nodes[w.node].index, t.nodes[w.node].index + 1, 0, 0};
         uint32_t nc = 2;

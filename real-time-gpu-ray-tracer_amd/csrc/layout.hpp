@@ -177,6 +177,9 @@ struct SceneGPU {
     // further records in LDS when they fit as well (dwordx4 offsets into the region, LDS_NONE = in HBM):
     // instance cold records (6 dwordx4 each), sphere hot / cold (1 each), parallelogram hot (5) / cold (1)
     uint32_t lds_icold, lds_sph_hot, lds_sph_cold, lds_q_hot, lds_q_cold;
+    // then the first lds_bqn quads of one BLAS (a group's, option "group", numbered level by level so they
+    // are its top levels): BLAS quad q in [lds_bq0, lds_bq0 + lds_bqn) is read at lds_bq_at + (q - lds_bq0) * 7
+    uint32_t lds_bq0, lds_bqn, lds_bq_at;
 };
 constexpr uint32_t LDS_NONE = 0xFFFFFFFFu;
 constexpr uint32_t LDS_SCENE_F4 = 1216;    // 19 KB per workgroup: 32 KB stack + 1 KB materials + 19 KB keeps 3

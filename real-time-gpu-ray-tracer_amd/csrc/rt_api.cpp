@@ -152,6 +152,7 @@ struct rt_scene {
     std::vector<InstGroup> groups;  // option "group": TLAS item n + g is group g
     std::vector<uint32_t> group_of; // per instance: its group + 1 (0: none)
     bool group_inst = true;         // option "group" (set before the build)
+    bool lds_blas = true;           // option "lds_blas": with "lds_scene" 2, a group BLAS's top levels in LDS
     uint32_t frame_items[8] = {};   // per frame block: TLAS items (= instance records when staged by slot)
     Tree tlas;
     FlatTree tlas_flat;
@@ -200,6 +201,12 @@ struct rt_scene {
     uint8_t *frame_dev[NLANE] = {};               // HBM
     hipEvent_t ev_copied[NLANE] = {};             // upload from staging[b] finished
     hipEvent_t ev_used[NLANE] = {};               // last kernel reading frame_dev[b] finished
+    // What the waits below use: the event last recorded for each purpose.  A trace launch records one event
+    // after it (its ring_stop timing event, or one event after a multi-GPU gather) and points every purpose
+    // it completes at that event — each event record between two kernels of a stream costs ~5 us of GPU
+    // idle time (profiles/r02_gaps.txt), and a launch completed four purposes with four records.
+    hipEvent_t r_copied[NLANE] = {}, r_used[NLANE] = {}, r_lane[NLANE] = {};
+    hipEvent_t r_done = nullptr;
     int active = -1;
 
     hipStream_t stream = nullptr;
@@ -344,8 +351,8 @@ struct rt_scene {
         (void)hipSetDevice(device);
         if (stream) (void)hipStreamSynchronize(stream);
         for (int q = 0; q < NLANE; q++)          // launches still running on caller streams
-            if (ev_lane_done[q]) (void)hipEventSynchronize(ev_lane_done[q]);
-        if (ev_render_done) (void)hipEventSynchronize(ev_render_done);
+            if (r_lane[q]) (void)hipEventSynchronize(r_lane[q]);
+        if (r_done) (void)hipEventSynchronize(r_done);
         release_comm();
         blas_pairs.release(); blas_quads.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
         quad_hot.release(); quad_cold.release(); materials.release(); out_rgba.release(); out_rgb.release();
@@ -441,7 +448,7 @@ hipError_t drain(rt_scene *s) {
     if (s->last_stream) e = hipStreamSynchronize(s->last_stream);
     if (e == hipSuccess && s->stream) e = hipStreamSynchronize(s->stream);
     for (int q = 0; q < rt_scene::NLANE && e == hipSuccess; q++)
-        if (s->ev_lane_done[q]) e = hipEventSynchronize(s->ev_lane_done[q]);
+        if (s->r_lane[q]) e = hipEventSynchronize(s->r_lane[q]);
     return e;
 }
 
@@ -455,7 +462,7 @@ hipError_t drain(rt_scene *s) {
 rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool defer = false) {
     const int b = s->active < 0 ? 0 : (s->active + 1) % rt_scene::NLANE;
     const auto w0 = std::chrono::steady_clock::now();
-    HIP_TRY(hipEventSynchronize(s->ev_copied[b]));     // staging[b] no longer read by a pending copy
+    HIP_TRY(hipEventSynchronize(s->r_copied[b]));      // staging[b] no longer read by a pending copy
     s->update_wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     if (s->update) {                                  // Renderer.cu:269
         std::vector<rt_xform> xs(s->inst.size());
@@ -495,7 +502,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
             in.box.store(d.p.box);
         }
         uint8_t *fd = s->frame_dev[b];
-        HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_used[b], 0));
+        HIP_TRY(hipStreamWaitEvent(s->stream, s->r_used[b], 0));
         // a blit kernel reading the pinned staging block, not an SDMA copy (see the host-built path below)
         if (nd) HIP_TRY(launch_frame_copy(fd + s->off_delta, s->staging_dev[b] + s->off_delta, nd * sizeof(InstDelta), nullptr, nullptr,
                                           s->stream));
@@ -530,6 +537,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
             s->block_by_slot[b] = true;
         }
         HIP_TRY(hipEventRecord(s->ev_copied[b], s->stream));
+        s->r_copied[b] = s->ev_copied[b];
         s->active = b;
         s->frame = frame;
         return RT_OK;
@@ -584,12 +592,13 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
     // Measured: the upload on a dedicated copy stream (the reference's copyStream, Renderer.cu:281-303)
     // went through an SDMA engine whose first use stalled a frame by ~7.6 ms; enqueued on the trace's
     // stream it is a ~4 us blit kernel between two traces.
-    HIP_TRY(hipStreamWaitEvent(upload, s->ev_used[b], 0));           // frame_dev[b] free on device
+    HIP_TRY(hipStreamWaitEvent(upload, s->r_used[b], 0));            // frame_dev[b] free on device
     if (defer) {
         s->pending_copy = b;
     } else {
         HIP_TRY(hipMemcpyAsync(s->frame_dev[b], st, s->frame_block, hipMemcpyHostToDevice, upload));
         HIP_TRY(hipEventRecord(s->ev_copied[b], upload));
+        s->r_copied[b] = s->ev_copied[b];
     }
     s->active = b;
     s->frame = frame;
@@ -636,6 +645,18 @@ SceneGPU scene_gpu(const rt_scene *s) {
             g.lds_q_hot = at; g.lds_q_cold = at + LDS_QPRIM_F4 * nqd; at += (LDS_QPRIM_F4 + 1) * nqd;
         }
         if (g.lds_insts && at + n * LDS_ICOLD_F4 <= LDS_SCENE_F4) { g.lds_icold = at; at += n * LDS_ICOLD_F4; }
+        // option "group": the top levels of the first group's BLAS in what is left (quads in level order)
+        if (s->lds_scene >= 2 && s->lds_blas && g.lds_insts && !s->groups.empty() && !s->gpu_tlas()) {
+            const BlasHost &bh = s->blas[s->groups[0].st.blas];
+            const uint32_t room = (LDS_SCENE_F4 - std::min(at, LDS_SCENE_F4)) / LDS_QUAD_F4;
+            const uint32_t nq_b = std::min<uint32_t>(room, (uint32_t)bh.wide.quads.size());
+            if (nq_b > 0 && !(bh.wide.root_ref & REF_LEAF)) {
+                g.lds_bq0 = bh.wide.root_ref & REF_INDEX_MASK;
+                g.lds_bqn = nq_b;
+                g.lds_bq_at = at;
+                at += nq_b * LDS_QUAD_F4;
+            }
+        }
     }
     return g;
 }
@@ -696,9 +717,9 @@ rt_status gpu_build_blas(rt_scene *s) {
         s->blas_builds++;
         return RT_OK;
     }
-    if (s->blas_builds && s->ev_render_done) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_render_done, 0));
+    if (s->blas_builds && s->r_done) HIP_TRY(hipStreamWaitEvent(s->stream, s->r_done, 0));
     for (int q = 0; q < rt_scene::NLANE; q++)           // "overlap": the other lane's trace may still be running
-        if (s->blas_builds && s->ev_lane_done[q]) HIP_TRY(hipStreamWaitEvent(s->stream, s->ev_lane_done[q], 0));
+        if (s->blas_builds && s->r_lane[q]) HIP_TRY(hipStreamWaitEvent(s->stream, s->r_lane[q], 0));
     const RawPrimsGPU raw{s->raw_tris.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
     const PrimOutGPU out{s->tri_hot.p, s->tri_cold.p, s->sph_hot.p, s->sph_cold.p, s->quad_hot.p, s->quad_cold.p};
     HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
@@ -742,6 +763,7 @@ rt_status gpu_setup_blas(rt_scene *s, const std::vector<LbvhSeg> &segs, const ui
     for (size_t i = 0; i < ib.size(); i++) ib[i] = s->inst[i].blas;
     if ((st = upload(s->inst_blas, ib)) != RT_OK) return st;
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
+    if (!s->r_done) s->r_done = s->ev_render_done;
     for (int q = 0; q < rt_scene::NLANE; q++) {       // "blas_double": every trace records its lane's event from now on
         if (!s->ev_blas_lane[q]) HIP_TRY(hipEventCreateWithFlags(&s->ev_blas_lane[q], hipEventDisableTiming));
         if (!s->spare.ev_lane[q]) HIP_TRY(hipEventCreateWithFlags(&s->spare.ev_lane[q], hipEventDisableTiming));
@@ -962,7 +984,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             bh.pair_base = pair_base;
             bh.slot_base = slot_base[RT_PRIM_TRIANGLE];
             bh.flat = flatten_tree(bh.tree, pair_base, bh.slot_base, RT_PRIM_TRIANGLE, true);
-            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, RT_PRIM_TRIANGLE, true, s->wide_merge);
+            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, RT_PRIM_TRIANGLE, true, s->wide_merge,
+                                        /*level_order=*/true);
             quad_base += (uint32_t)bh.wide.quads.size();
             s->max_blas_height = std::max(s->max_blas_height, bh.flat.height);
             pair_base += (uint32_t)bh.flat.pairs.size();
@@ -980,6 +1003,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     rt_status st;
     if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
+    if (!s->r_done) s->r_done = s->ev_render_done;
     for (bool &v : s->sched_valid) v = false;
     if (mode == RT_BUILD_LBVH) {
         if ((st = gpu_setup_blas(s, segs, slot_base)) != RT_OK) return st;
@@ -1099,6 +1123,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->frame_dev[b]), s->frame_block));
         if (!s->ev_copied[b]) HIP_TRY(hipEventCreateWithFlags(&s->ev_copied[b], hipEventDisableTiming));
         if (!s->ev_used[b]) HIP_TRY(hipEventCreateWithFlags(&s->ev_used[b], hipEventDisableTiming));
+        if (!s->r_copied[b]) s->r_copied[b] = s->ev_copied[b];
+        if (!s->r_used[b]) s->r_used[b] = s->ev_used[b];
     }
     for (uint32_t i = 0; i < rt_scene::RING; i++) {
         if (!s->ring_start[i]) HIP_TRY(hipEventCreate(&s->ring_start[i]));
@@ -1114,6 +1140,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             HIP_TRY(hipMemset(s->queue[q], 0, QUEUE_WORDS * sizeof(uint32_t)));
         }
         if (!s->ev_lane_done[q]) HIP_TRY(hipEventCreateWithFlags(&s->ev_lane_done[q], hipEventDisableTiming));
+        if (!s->r_lane[q]) s->r_lane[q] = s->ev_lane_done[q];
     }
     {
         hipDeviceProp_t prop;
@@ -1394,12 +1421,17 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     }
     s->lane = s->overlap ? (s->lane + 1) % s->lanes : 0u;
     s->last_lane = q;
-    HIP_TRY(hipStreamWaitEvent(stream, s->overlap ? s->ev_lane_done[q] : s->ev_render_done, 0));
+    HIP_TRY(hipStreamWaitEvent(stream, s->overlap ? s->r_lane[q] : s->r_done, 0));
     unsigned long long *lane_counters = s->counters + (size_t)q * CNT_NUM;   // only this lane's launches add here
     if (!(o.flags & RT_RENDER_KEEP_COUNTERS)) s->cnt_epoch++;
     bool zero_lane = s->lane_epoch[q] != s->cnt_epoch;                      // cleared before this launch
     s->lane_epoch[q] = s->cnt_epoch;
     bool reset_queue = true;
+    bool copied_here = false;                  // this call enqueued the frame block's upload on `stream`
+    // ... of this frame block: no event between the copy and the trace (each event record between two kernels
+    // of a stream costs ~4.5 us of GPU idle: copy -> trace gap 10.6 -> 6.1 us, profiles/r02_gaps.txt); its
+    // r_copied is the trace's completion event (the host waits on it only before reusing the staging buffer)
+    int copied_block = -1;
     if (s->use_persistent && s->reorder && s->grab == 64u) {
         DevBuf<uint32_t> &unit_cost = s->unit_cost[q], &unit_order = s->unit_order[q];
         if (unit_cost.n < 2 * (size_t)out.units) {        // [recorded costs | costs of the last launch (debug)]
@@ -1439,7 +1471,8 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
                                     pc >= 0 ? s->staging_dev[pc] : nullptr, pc >= 0 ? s->frame_block : 0,
                                     zero_lane ? lane_counters : nullptr, stream));
             zero_lane = false;
-            if (pc >= 0) HIP_TRY(hipEventRecord(s->ev_copied[pc], stream));
+            copied_here = pc >= 0;
+            copied_block = pc;
             s->pending_copy = -1;
             if (do_order) s->order_ok[q] = true;
             reset_queue = false;
@@ -1454,12 +1487,14 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         HIP_TRY(launch_frame_copy(s->frame_dev[s->pending_copy], s->staging_dev[s->pending_copy], s->frame_block,
                                   zero_lane ? lane_counters : nullptr, reset_queue && s->use_persistent ? s->queue[q] : nullptr,
                                   stream));
-        HIP_TRY(hipEventRecord(s->ev_copied[s->pending_copy], stream));
+        copied_block = s->pending_copy;
         s->pending_copy = -1;
         zero_lane = false;
         reset_queue = false;
+        copied_here = true;
     }
-    HIP_TRY(hipStreamWaitEvent(stream, s->ev_copied[s->active], 0));
+    // the frame block's upload: stream-ordered when this call enqueued it
+    if (!copied_here) HIP_TRY(hipStreamWaitEvent(stream, s->r_copied[s->active], 0));
     if (zero_lane) HIP_TRY(hipMemsetAsync(lane_counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
     const uint32_t slot = s->ring_head;
     s->ring_head = (s->ring_head + 1) % rt_scene::RING;
@@ -1489,7 +1524,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         if (pct == 0) {
             bool partner = false;             // another lane's launch not finished yet (host query, ~1 us)
             for (int l = 0; s->overlap && l < rt_scene::NLANE && !partner; l++)
-                partner = l != q && s->ev_lane_done[l] && hipEventQuery(s->ev_lane_done[l]) == hipErrorNotReady;
+                partner = l != q && s->r_lane[l] && hipEventQuery(s->r_lane[l]) == hipErrorNotReady;
             pct = partner ? 50u : 100u;
         }
         if (pct < 100) blocks = std::max<uint32_t>(8u, blocks * pct / 100u);
@@ -1502,6 +1537,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, lane_counters, stream)
                       : launch_render_fast(g, cam, out, count, lane_counters, stream));
     HIP_TRY(hipEventRecord(s->ring_stop[slot], stream));
+    hipEvent_t done = s->ring_stop[slot];      // the launch's one completion event (see r_used)
     if (cm) {
         // gather the ranks' slabs to rank 0 (grouped point-to-point over xGMI: each rank's bytes take
         // their own link into rank 0), then scatter them into the frame there
@@ -1523,9 +1559,12 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             HIP_TRY(launch_assemble(cm->gathered[q].p, (uint32_t)(sb / (4ull * cm->tile_w * cm->tile_h)), cm->tile_w,
                                     cm->tile_h, (uint32_t)cm->world, W, H, frame_out, stream));
     }
-    HIP_TRY(hipEventRecord(s->ev_used[s->active], stream));
-    HIP_TRY(hipEventRecord(s->ev_render_done, stream));
-    HIP_TRY(hipEventRecord(s->ev_lane_done[q], stream));
+    if (cm) {                                  // after the gather + assemble
+        HIP_TRY(hipEventRecord(s->ev_lane_done[q], stream));
+        done = s->ev_lane_done[q];
+    }
+    s->r_used[s->active] = s->r_done = s->r_lane[q] = done;
+    if (copied_block >= 0) s->r_copied[copied_block] = done;
     if (s->ev_blas_lane[q]) HIP_TRY(hipEventRecord(s->ev_blas_lane[q], stream));   // "blas_double": this set's reader
     if (o.flags & RT_RENDER_NO_SYNC) {
         if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; stats->update_wait_ms = s->update_wait_ms; }
@@ -1575,12 +1614,12 @@ rt_status rt_trace_rays(rt_scene *s, const float *rays, size_t n, uint32_t flags
     if (e != hipSuccess) { (void)hipFree(d_rays); return fail(RT_ERR_OUT_OF_MEMORY, "hipMalloc hits"); }
     const SceneGPU g = scene_gpu(s);
     e = hipMemcpyAsync(d_rays, rays, n * 6 * sizeof(float), hipMemcpyHostToDevice, s->stream);
-    if (e == hipSuccess) e = hipStreamWaitEvent(s->stream, s->ev_copied[s->active], 0);
+    if (e == hipSuccess) e = hipStreamWaitEvent(s->stream, s->r_copied[s->active], 0);
     if (e == hipSuccess)
         e = (flags & RT_RENDER_EXACT) ? launch_trace_rays_exact(g, d_rays, (uint32_t)n, d_hits, s->stream)
                                       : launch_trace_rays_fast(g, d_rays, (uint32_t)n, d_hits, s->stream);
     if (e == hipSuccess) e = hipEventRecord(s->ev_used[s->active], s->stream);
-    if (e == hipSuccess && s->ev_render_done) e = hipEventRecord(s->ev_render_done, s->stream);
+    if (e == hipSuccess) { s->r_used[s->active] = s->ev_used[s->active]; s->r_done = s->ev_used[s->active]; }
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     if (e == hipSuccess) e = hipMemcpy(hits, d_hits, n * sizeof(rt_hit), hipMemcpyDeviceToHost);
     (void)hipFree(d_rays);
@@ -1668,6 +1707,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "split") {
         if (value < 0 || value > 0xFFFF) return fail(RT_ERR_INVALID_ARGUMENT, "split must be k_half | k_quarter << 8");
         s->split = (uint32_t)value;
+    } else if (k == "lds_blas") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "lds_blas must be 0 or 1");
+        s->lds_blas = value == 1;
     } else if (k == "group") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "group must be 0 or 1");
         s->group_inst = value == 1;                   // next rt_scene_build
@@ -1896,7 +1938,7 @@ rt_status rt_synchronize(rt_scene *s) {
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(drain(s));
-    if (s->ev_render_done) HIP_TRY(hipEventSynchronize(s->ev_render_done));
+    if (s->r_done) HIP_TRY(hipEventSynchronize(s->r_done));
     return RT_OK;
 }
 

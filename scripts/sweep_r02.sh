@@ -103,6 +103,24 @@ if [[ $WHAT == host ]]; then
   one sweep_host.jsonl --config C4 --shard 3/8
   one sweep_host.jsonl --overlap 1 --shard 4/8
 fi
+if [[ $WHAT == lanes8 ]]; then
+  # many frames in flight for a rank's share: L lanes x P % grids, 8 hardware queues
+  for lp in 3:0 6:15 8:12 8:15 8:20; do L=${lp%:*}; P=${lp#*:}
+    GPU_MAX_HW_QUEUES=8 one sweep_lanes8.jsonl --overlap $L --opt grid_pct=$P --steps 200 --shard 4/8
+  done
+  for lp in 8:12 8:25; do L=${lp%:*}; P=${lp#*:}
+    GPU_MAX_HW_QUEUES=8 one sweep_lanes8.jsonl --overlap $L --opt grid_pct=$P --steps 200
+  done
+fi
+if [[ $WHAT == ldsblas ]]; then
+  # option "lds_blas": the group BLAS's top levels in the LDS scene region
+  for rep in 1 2; do for v in 0 1; do
+    one sweep_ldsblas.jsonl --opt lds_blas=$v
+    one sweep_ldsblas.jsonl --opt lds_blas=$v --overlap 1
+    one sweep_ldsblas.jsonl --opt lds_blas=$v --shard 4/8
+    one sweep_ldsblas.jsonl --opt lds_blas=$v --config C3
+  done; done
+fi
 if [[ $WHAT == retune ]]; then
   # knobs re-checked after lds_scene / grid_pct / chained root leaves: refill threshold, split levels, reorder period
   for rep in 1 2; do

@@ -408,7 +408,7 @@ def test_reorder_period_byte_identical(gpu_lib, period, lanes):
 
 @pytest.mark.parametrize("opts", [{"mix": 1}, {"claim_items": 2}, {"mix": 1, "claim_items": 2}, {"grid_pct": 30},
                                   {"merge": 8}, {"merge": 16}, {"merge": 8, "claim_items": 2},
-                                  {"drain": 1}, {"drain": 4}, {"drain": 64}])
+                                  {"drain": 1}, {"drain": 4}, {"drain": 64}, {"lds_blas": 0}])
 def test_claim_options_byte_identical(gpu_lib, opts):
     """Claim-order options of the persistent kernel ("mix": heaviest item from a band's front, light fill
     from its back; "claim_items" 2; a 30 % grid): which wave traces a pixel changes, the pixel's result
