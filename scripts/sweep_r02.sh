@@ -121,6 +121,24 @@ if [[ $WHAT == ldsblas ]]; then
     one sweep_ldsblas.jsonl --opt lds_blas=$v --config C3
   done; done
 fi
+if [[ $WHAT == lanes8b ]]; then
+  # frames in flight for a rank's share after one completion event per launch: lanes x grid share x hw queues
+  for cfg in "4:0:4" "4:0:8" "6:0:8" "6:20:8" "8:15:8" "8:0:8"; do IFS=: read L P Q <<< "$cfg"
+    GPU_MAX_HW_QUEUES=$Q one sweep_lanes8b.jsonl --overlap $L --opt grid_pct=$P --steps 200 --shard 4/8
+  done
+  for cfg in "4:0:4" "4:0:8" "6:0:8"; do IFS=: read L P Q <<< "$cfg"
+    GPU_MAX_HW_QUEUES=$Q one sweep_lanes8b.jsonl --overlap $L --opt grid_pct=$P --steps 200
+    GPU_MAX_HW_QUEUES=$Q one sweep_lanes8b.jsonl --overlap $L --opt grid_pct=$P --steps 200 --config C4 --shard 3/8
+  done
+  one sweep_lanes8b.jsonl --steps 200 --config C4 --shard 3/8
+  one sweep_lanes8b.jsonl --steps 200 --config C4
+fi
+if [[ $WHAT == shares3 ]]; then
+  # share defaults of bench.py (6 lanes, 20 % grids, 8 hardware queues) over several ranks, and the full frames
+  for r in 0 2 4 6; do one sweep_shares3.jsonl --steps 200 --shard $r/8; one sweep_shares3.jsonl --steps 200 --config C4 --shard $r/8; done
+  one sweep_shares3.jsonl --steps 200 --config C4
+  one sweep_shares3.jsonl --steps 200
+fi
 if [[ $WHAT == retune ]]; then
   # knobs re-checked after lds_scene / grid_pct / chained root leaves: refill threshold, split levels, reorder period
   for rep in 1 2; do
