@@ -325,7 +325,7 @@ def main():
                                                 else "single-gpu"))),
                 "overlap_lanes": L,
                 "tile": TILE,
-                "threshold": args.threshold if args.threshold is not None else 32,
+                "threshold": args.threshold if args.threshold is not None else "auto (64 at depth x spp <= 2, else 40)",
                 "options": args.pre_opt + args.opt,
                 "kernel": ("EXACT" if args.exact else "FAST") + (" persistent" if args.kernel else " grid"),
                 "bvh": args.build,

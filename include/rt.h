@@ -298,7 +298,8 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
 /* Tuning knobs (defaults are the tuned values):
  *   "kernel"    : 0 = one-thread-per-pixel grid kernel, 1 = persistent-wave megakernel (default)
  *   "threshold" : persistent kernel — lanes that must be waiting before a wave leaves the
- *                 traversal loop to shade / regenerate (1..64, default 32)
+ *                 traversal loop to shade / regenerate (1..64; default 0 = auto: 64 when depth x samples <= 2,
+ *                 else 40)
  *   "variant"   : persistent kernel register budget: 0 = compiler's choice, 4 / 5 = at least
  *                 4 / 5 waves per SIMD
  *   "queue_parts": persistent kernel work-queue bands (1..8, default 8; a wave starts on band XCC_ID % parts)

@@ -235,7 +235,11 @@ struct rt_scene {
     int last_lane = 0;              // lane of the last rt_render
     hipEvent_t ev_lane_done[NLANE] = {};   // last trace launch of each lane finished
     uint32_t cus = 0;
-    uint32_t threshold = 32;          // measured with "reorder" + "wide" + 2 overlap lanes: 32-48 beat 16
+    // option "threshold" (lanes waiting before a wave leaves traversal to shade and refill); 0 = auto: 64 when
+    // a pixel's path has at most two segments (depth x samples <= 2: the wave then shades and refills all its
+    // lanes at once), else 40 (C2 0.194 -> 0.184 ms/frame, serialised 0.35 -> 0.33 ms; C3 at 64 would lose
+    // 23 %, 40 ties 32; profiles/r02_sweep_thr2.jsonl)
+    uint32_t threshold = 0;
     uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4, 5)
     double update_wait_ms = 0.0;    // last frame_update: time blocked on ev_copied (GPU progress)
     bool use_persistent = true;
@@ -1528,9 +1532,10 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             pct = partner ? 50u : 100u;
         }
         if (pct < 100) blocks = std::max<uint32_t>(8u, blocks * pct / 100u);
-        HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, lane_counters, s->queue[q], blocks, s->threshold,
+        const uint32_t thr = s->threshold ? s->threshold : (cam.depth * cam.sqrt_s * cam.sqrt_s <= 2u ? 64u : 40u);
+        HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, lane_counters, s->queue[q], blocks, thr,
                                                        s->variant, false, reset_queue, stream)
-                      : launch_render_persistent_fast(g, cam, out, count, lane_counters, s->queue[q], blocks, s->threshold,
+                      : launch_render_persistent_fast(g, cam, out, count, lane_counters, s->queue[q], blocks, thr,
                                                       s->variant, lean, reset_queue, stream));
     }
     else
@@ -1635,7 +1640,7 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "kernel must be 0 or 1");
         s->use_persistent = value == 1;
     } else if (k == "threshold") {
-        if (value < 1 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "threshold must be in 1..64");
+        if (value < 0 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "threshold must be in 0..64 (0 = auto)");
         s->threshold = (uint32_t)value;
     } else if (k == "variant") {
         if (value != 0 && value != 4 && value != 5) return fail(RT_ERR_INVALID_ARGUMENT, "variant must be 0, 4 or 5");

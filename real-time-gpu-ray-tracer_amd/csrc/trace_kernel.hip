@@ -1599,10 +1599,44 @@ __device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t
     }
 }
 
+#ifndef RT_ARGS_LDS
+#define RT_ARGS_LDS 0                   // kernel arguments read from LDS copies (fewer live SGPRs, fewer spills):
+                                        // 1 = the camera, 2 = + the output block, 3 = + the scene block
+#endif
+template <typename A>
+__device__ __forceinline__ void args_to_lds(A &dst, const A &src) {
+    static_assert(sizeof(A) % 4 == 0 && sizeof(A) / 4 <= BLOCK, "argument block copied one dword per thread");
+    if (threadIdx.x < sizeof(A) / 4)
+        reinterpret_cast<uint32_t *>(&dst)[threadIdx.x] = reinterpret_cast<const uint32_t *>(&src)[threadIdx.x];
+}
 template <bool COUNT, bool LEAN, bool WIDE>
-__device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out,
-                                                       uint32_t *queue, uint32_t threshold,
+__device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, const CameraGPU &cam_arg,
+                                                       const OutputGPU &out_arg, uint32_t *queue, uint32_t threshold,
                                                        unsigned long long *counters) {
+#if RT_ARGS_LDS >= 1
+    __shared__ CameraGPU lds_cam;
+    args_to_lds(lds_cam, cam_arg);
+    const CameraGPU &cam = lds_cam;
+#else
+    const CameraGPU &cam = cam_arg;
+#endif
+#if RT_ARGS_LDS >= 2
+    __shared__ OutputGPU lds_out;
+    args_to_lds(lds_out, out_arg);
+    const OutputGPU &out = lds_out;
+#else
+    const OutputGPU &out = out_arg;
+#endif
+#if RT_ARGS_LDS >= 3
+    __shared__ SceneGPU lds_sc;
+    args_to_lds(lds_sc, sc_arg);
+    const SceneGPU &sc = lds_sc;
+#else
+    const SceneGPU &sc = sc_arg;
+#endif
+#if RT_ARGS_LDS >= 1
+    __syncthreads();                              // the argument copies, before the scene fill reads them
+#endif
     __shared__ unsigned long long lds_stack[LEAN ? LEAN_DEPTH : LDS_DEPTH][BLOCK];
     __shared__ float4 lds_mat[LDS_MATERIALS];     // the scene's materials (shading reads them per hit)
     __shared__ uint32_t lds_path[RT_PATH_LDS ? PATH_WORDS : 1][BLOCK];

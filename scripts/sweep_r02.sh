@@ -149,6 +149,33 @@ if [[ $WHAT == retune ]]; then
     one sweep_retune.jsonl --shard 4/8
   done
 fi
+if [[ $WHAT == retune2 ]]; then
+  # knobs re-checked after groups / flat quads / reciprocal slabs / one event per launch, pipelined and serialised
+  for rep in 1 2; do for ov in "" "--overlap 1"; do
+    for t in 24 32 40 48; do one sweep_retune2.jsonl --threshold $t $ov; done
+    for sp in 2572 3598 65535; do one sweep_retune2.jsonl --opt split=$sp $ov; done
+    for k in 4 16; do one sweep_retune2.jsonl --opt reorder_period=$k $ov; done
+  done; done
+fi
+if [[ $WHAT == thr2 ]]; then
+  # refill threshold 32..64 after the session-3 changes: full frame, serialised, a share, C3
+  for rep in 1 2; do for t in 32 40 48 56 64; do
+    one sweep_thr2.jsonl --threshold $t
+    one sweep_thr2.jsonl --threshold $t --overlap 1
+    one sweep_thr2.jsonl --threshold $t --shard 4/8
+    one sweep_thr2.jsonl --threshold $t --config C3
+  done; done
+fi
+if [[ $WHAT == thrauto ]]; then
+  # auto threshold (64 at depth x spp <= 2, else 40) vs 32 on the other configurations
+  for rep in 1 2; do for t in 32 0; do
+    one sweep_thrauto.jsonl --threshold $t --config C4
+    one sweep_thrauto.jsonl --threshold $t --config C4 --shard 3/8
+    one sweep_thrauto.jsonl --threshold $t --shard 0/8
+    one sweep_thrauto.jsonl --threshold $t --build lbvh
+  done; done
+  for t in 32 0; do one sweep_thrauto.jsonl --threshold $t --config C5 --build lbvh --rebuild --steps 20 --warmup 3; done
+fi
 if [[ $WHAT == costmax ]]; then
   # option "cost_max": claim order by a unit's longest path (x 64) instead of its summed cost; split levels
   for rep in 1 2; do for o in "--opt cost_max=0" "--opt cost_max=1" "--opt cost_max=1 --opt split=3598" "--opt cost_max=1 --opt split=65535"; do
