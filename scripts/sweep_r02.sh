@@ -176,6 +176,22 @@ if [[ $WHAT == thrauto ]]; then
   done; done
   for t in 32 0; do one sweep_thrauto.jsonl --threshold $t --config C5 --build lbvh --rebuild --steps 20 --warmup 3; done
 fi
+if [[ $WHAT == order2 ]]; then
+  # claim-order knobs under the auto threshold: merged light pairs, heavy-unit quarters
+  for rep in 1 2; do for o in "--opt merge=0" "--opt merge=6" "--opt merge=8" "--opt split=65535" "--opt split=2570"; do
+    one sweep_order2.jsonl $o
+    one sweep_order2.jsonl $o --overlap 1
+    one sweep_order2.jsonl $o --shard 4/8
+  done; done
+fi
+if [[ $WHAT == drain2 ]]; then
+  # option "drain" under the auto threshold (64 for C2: a wave otherwise shades only when all its lanes are idle)
+  for rep in 1 2; do for v in 0 2 4 16; do
+    one sweep_drain2.jsonl --opt drain=$v
+    one sweep_drain2.jsonl --opt drain=$v --overlap 1
+    one sweep_drain2.jsonl --opt drain=$v --shard 4/8
+  done; done
+fi
 if [[ $WHAT == costmax ]]; then
   # option "cost_max": claim order by a unit's longest path (x 64) instead of its summed cost; split levels
   for rep in 1 2; do for o in "--opt cost_max=0" "--opt cost_max=1" "--opt cost_max=1 --opt split=3598" "--opt cost_max=1 --opt split=65535"; do
