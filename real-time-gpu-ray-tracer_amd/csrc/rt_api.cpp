@@ -213,6 +213,7 @@ struct rt_scene {
     // per-frame kernel timing ring for pipelined frames (rt_scene_collect)
     static constexpr uint32_t RING = 256;
     hipEvent_t ring_start[RING] = {}, ring_stop[RING] = {};
+    hipEvent_t ring_post[RING] = {};     // multi-GPU frames: the launch's completion event after its gather
     uint32_t ring_head = 0, ring_pending = 0;
     hipStream_t last_stream = nullptr;
     // persistent megakernel: work-queue head, grid size (#CUs x resident blocks), refill threshold
@@ -387,6 +388,7 @@ struct rt_scene {
         for (uint32_t i = 0; i < RING; i++) {
             if (ring_start[i]) (void)hipEventDestroy(ring_start[i]);
             if (ring_stop[i]) (void)hipEventDestroy(ring_stop[i]);
+            if (ring_post[i]) (void)hipEventDestroy(ring_post[i]);
         }
         if (stream) (void)hipStreamDestroy(stream);
     }
@@ -1133,6 +1135,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     for (uint32_t i = 0; i < rt_scene::RING; i++) {
         if (!s->ring_start[i]) HIP_TRY(hipEventCreate(&s->ring_start[i]));
         if (!s->ring_stop[i]) HIP_TRY(hipEventCreate(&s->ring_stop[i]));
+        if (!s->ring_post[i]) HIP_TRY(hipEventCreateWithFlags(&s->ring_post[i], hipEventDisableTiming));
     }
     if (!s->counters) {
         HIP_TRY(hipMalloc(&s->counters, rt_scene::NLANE * CNT_NUM * sizeof(unsigned long long)));
@@ -1564,9 +1567,9 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             HIP_TRY(launch_assemble(cm->gathered[q].p, (uint32_t)(sb / (4ull * cm->tile_w * cm->tile_h)), cm->tile_w,
                                     cm->tile_h, (uint32_t)cm->world, W, H, frame_out, stream));
     }
-    if (cm) {                                  // after the gather + assemble
-        HIP_TRY(hipEventRecord(s->ev_lane_done[q], stream));
-        done = s->ev_lane_done[q];
+    if (cm) {                                  // after the gather + assemble; one event per launch, never one
+        HIP_TRY(hipEventRecord(s->ring_post[slot], stream));   // re-recorded by the lane's next frame (the
+        done = s->ring_post[slot];                              // staging / block waits must see this launch)
     }
     s->r_used[s->active] = s->r_done = s->r_lane[q] = done;
     if (copied_block >= 0) s->r_copied[copied_block] = done;
