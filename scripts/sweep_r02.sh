@@ -192,6 +192,15 @@ if [[ $WHAT == drain2 ]]; then
     one sweep_drain2.jsonl --opt drain=$v --shard 4/8
   done; done
 fi
+if [[ $WHAT == leaf2 ]]; then
+  # SAH BLAS leaf size with instance groups and the auto threshold
+  for rep in 1 2; do for v in 2 3 4; do
+    one sweep_leaf2.jsonl --pre-opt blas_leaf=$v
+    one sweep_leaf2.jsonl --pre-opt blas_leaf=$v --overlap 1
+    one sweep_leaf2.jsonl --pre-opt blas_leaf=$v --shard 4/8
+    one sweep_leaf2.jsonl --pre-opt blas_leaf=$v --config C3
+  done; done
+fi
 if [[ $WHAT == costmax ]]; then
   # option "cost_max": claim order by a unit's longest path (x 64) instead of its summed cost; split levels
   for rep in 1 2; do for o in "--opt cost_max=0" "--opt cost_max=1" "--opt cost_max=1 --opt split=3598" "--opt cost_max=1 --opt split=65535"; do
