@@ -431,7 +431,8 @@ rt_status rt_scene_export_blas(const rt_scene *scene, uint32_t blas_index,
                                uint32_t *n_nodes, uint32_t *n_prims);
 
 /* Export the current TLAS (include/AS/TLAS.cuh:24-39) in the same form; prim_refs receive
- * instance indices. */
+ * instance indices (option "group": a ref >= instance_count is group ref - instance_count, standing for
+ * its member instances in this frame). */
 rt_status rt_scene_export_tlas(const rt_scene *scene,
                                float *node_boxes, uint32_t *node_count_index,
                                uint32_t *instance_refs, uint32_t *n_nodes, uint32_t *n_refs);
