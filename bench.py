@@ -6,7 +6,7 @@
 
 A step is one frame of the reference's render loop (src/Global/Renderer.cu:264-317): the
 instance update callback (Main.cu updateInstance, native), the host TLAS rebuild + upload,
-and the trace kernel over the frame — for N > 1 each rank traces its interleaved 64x64
+and the trace kernel over the frame — for N > 1 each rank traces its interleaved 32x32
 screen tiles, and the library gathers the tiles to rank 0 over RCCL and assembles the frame there,
 inside rt_render (rt_scene_attach_comm; torch.distributed only broadcasts the RCCL id and runs the
 barriers and the max-over-ranks timing).  Scene, BVHs and framebuffer stay in HBM; nothing is
@@ -28,7 +28,7 @@ sys.path.insert(0, os.path.join(REPO, "real-time-gpu-ray-tracer_amd"))
 
 METRIC = "Mrays/sec + ms/frame, 1920×1080 1spp primary+shadow, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-TILE = 64
+TILE = 32
 
 # SURVEY §8(d) algorithmic bytes (the roofline's `achieved`):
 #   B = 32 N_aabb + 36 N_tri + 32 N_sph_or_quad + 48 N_inst + 32 per ray (state in/out) + 4 per pixel
@@ -58,7 +58,9 @@ def parse():
                                                  "(per-rank cost study; no gather)")
     p.add_argument("--opt", action="append", default=[], help="extra rt_scene_set_option key=value (A/B studies)")
     p.add_argument("--pre-opt", action="append", default=[], help="rt_scene_set_option key=value before the build")
-    p.add_argument("--tile", type=int, default=64, help="N > 1 screen-tile edge in pixels (multiple of 8)")
+    # 32: the ranks' shares balance better than with 64 (slowest C4 1/8 share 0.064 -> 0.059 ms/frame, C2
+    # equal; profiles/r02_sweep_tile2.jsonl)
+    p.add_argument("--tile", type=int, default=32, help="N > 1 screen-tile edge in pixels (multiple of 8)")
     p.add_argument("--attach-comm", action="store_true",
                    help="N = 1: run the multi-GPU frame path anyway (a world-1 RCCL communicator: tiles + assemble)")
     p.add_argument("--no-cpu-baseline", action="store_true")

@@ -201,6 +201,13 @@ if [[ $WHAT == leaf2 ]]; then
     one sweep_leaf2.jsonl --pre-opt blas_leaf=$v --config C3
   done; done
 fi
+if [[ $WHAT == tile2 ]]; then
+  # screen-tile edge for the rank shares (balance of the slowest share)
+  for t in 32 64; do for r in 0 2 4 6; do
+    one sweep_tile2.jsonl --steps 200 --shard $r/8 --tile $t
+    one sweep_tile2.jsonl --steps 200 --config C4 --shard $r/8 --tile $t
+  done; done
+fi
 if [[ $WHAT == costmax ]]; then
   # option "cost_max": claim order by a unit's longest path (x 64) instead of its summed cost; split levels
   for rep in 1 2; do for o in "--opt cost_max=0" "--opt cost_max=1" "--opt cost_max=1 --opt split=3598" "--opt cost_max=1 --opt split=65535"; do
