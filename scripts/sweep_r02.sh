@@ -208,6 +208,12 @@ if [[ $WHAT == tile2 ]]; then
     one sweep_tile2.jsonl --steps 200 --config C4 --shard $r/8 --tile $t
   done; done
 fi
+if [[ $WHAT == lanes3 ]]; then
+  # whole-frame lanes x reserve after the session-3 changes
+  for rep in 1 2; do for cfg in "3 16" "3 0" "3 8" "2 16" "4 16"; do set -- $cfg
+    one sweep_lanes3.jsonl --overlap $1 --opt reserve=$2
+  done; done
+fi
 if [[ $WHAT == costmax ]]; then
   # option "cost_max": claim order by a unit's longest path (x 64) instead of its summed cost; split levels
   for rep in 1 2; do for o in "--opt cost_max=0" "--opt cost_max=1" "--opt cost_max=1 --opt split=3598" "--opt cost_max=1 --opt split=65535"; do
