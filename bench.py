@@ -162,12 +162,13 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     n = max(1, world)
     # a rank's 1/N share (N > 1, or the one-GPU --shard study) is bounded by its longest paths, not by its
-    # work: more frames in flight pay there (6 lanes with 20 % grids and 8 hardware queues per process:
-    # C2 1/8 share 0.067 -> 0.060 ms/frame, C4 0.090 -> 0.074; profiles/r02_sweep_lanes8b.jsonl), while a
+    # work: more frames in flight pay there (8 lanes with 15 % grids and 12 hardware queues per process, so
+    # every lane and the RCCL communicators' streams get queues of their own: C2 1/8 share 0.067 -> 0.045
+    # ms/frame, C4 0.090 -> 0.054; profiles/r02_sweep_lanes8b.jsonl, r02_sweep_lanes8c.jsonl), while a
     # whole frame on one GPU is best with 3 lanes and the default 4 queues.  Set before HIP initialises.
     share = n > 1 or args.shard is not None
-    if share and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"       # (the pool's boxes export 4, HIP's default)
+    if share and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 12:
+        os.environ["GPU_MAX_HW_QUEUES"] = "12"      # (the pool's boxes export 4, HIP's default)
 
     import numpy as np
     import torch
@@ -193,11 +194,11 @@ def main():
     for kv in args.opt:
         k, v = kv.split("=")
         r.set_option(k, int(v, 0))
-    # measured (profiles/r02_sweep_lanes.jsonl, r02_sweep_lanes8b.jsonl): 3 lanes at N = 1,
-    # 6 lanes on 20 % grids for a rank's 1/N share
-    L = max(1, args.overlap if args.overlap is not None else (6 if share else 3))
+    # measured (profiles/r02_sweep_lanes.jsonl, r02_sweep_lanes8c.jsonl): 3 lanes at N = 1,
+    # 8 lanes on 15 % grids for a rank's 1/N share
+    L = max(1, args.overlap if args.overlap is not None else (8 if share else 3))
     if share and args.overlap is None and not any(kv.startswith("grid_pct=") for kv in args.opt):
-        r.set_option("grid_pct", 20)
+        r.set_option("grid_pct", 15)
     overlap = L > 1
     if overlap:
         r.set_option("overlap", L)

@@ -214,6 +214,13 @@ if [[ $WHAT == lanes3 ]]; then
     one sweep_lanes3.jsonl --overlap $1 --opt reserve=$2
   done; done
 fi
+if [[ $WHAT == lanes8c ]]; then
+  # more frames in flight for a share (after one event per launch, auto threshold, 32x32 tiles)
+  for cfg in "6:20:8" "8:15:8" "8:15:12" "8:12:12" "7:17:12"; do IFS=: read L P Q <<< "$cfg"
+    GPU_MAX_HW_QUEUES=$Q one sweep_lanes8c.jsonl --overlap $L --opt grid_pct=$P --steps 200 --shard 4/8 --tile 32
+    GPU_MAX_HW_QUEUES=$Q one sweep_lanes8c.jsonl --overlap $L --opt grid_pct=$P --steps 200 --config C4 --shard 2/8 --tile 32
+  done
+fi
 if [[ $WHAT == costmax ]]; then
   # option "cost_max": claim order by a unit's longest path (x 64) instead of its summed cost; split levels
   for rep in 1 2; do for o in "--opt cost_max=0" "--opt cost_max=1" "--opt cost_max=1 --opt split=3598" "--opt cost_max=1 --opt split=65535"; do
