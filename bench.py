@@ -196,9 +196,8 @@ def main():
         r.set_option(k, int(v, 0))
     # measured (profiles/r02_sweep_lanes.jsonl, r02_sweep_lanes8c.jsonl): 3 lanes at N = 1,
     # 8 lanes on 15 % grids for a rank's 1/N share
+    # (the library's auto grid then gives each of 8 lanes' launches 15 % of the GPU while others are in flight)
     L = max(1, args.overlap if args.overlap is not None else (8 if share else 3))
-    if share and args.overlap is None and not any(kv.startswith("grid_pct=") for kv in args.opt):
-        r.set_option("grid_pct", 15)
     overlap = L > 1
     if overlap:
         r.set_option("overlap", L)

@@ -347,7 +347,8 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 shaded when 1/drain of the wave's remaining paths wait (1..64; default 0 = when "threshold"
  *                 lanes wait; results identical)
  *   "grid_pct"  : persistent grid as a percentage of the resident workgroup capacity (1..100; default 0 = auto:
- *                 100 for serialised launches, 50 with "overlap", so two lanes' launches run side by side)
+ *                 100 when no other lane's launch is in flight, else 50 with up to 3 lanes and 120 / lanes
+ *                 (at least 12) with more, so several lanes' launches run side by side)
  *   "lds_scene" : FAST quad-tree kernel: 1 = every workgroup copies the frame's TLAS quads and, when they fit
  *                 as well, the instance hot records into 19 KB of LDS and reads them there; 2 = also the
  *                 sphere / parallelogram records and the instance cold records, while they fit (default 2;
