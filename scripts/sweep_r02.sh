@@ -221,6 +221,12 @@ if [[ $WHAT == lanes8c ]]; then
     GPU_MAX_HW_QUEUES=$Q one sweep_lanes8c.jsonl --overlap $L --opt grid_pct=$P --steps 200 --config C4 --shard 2/8 --tile 32
   done
 fi
+if [[ $WHAT == lanes4 ]]; then
+  # whole frame: lanes with the lane-scaled auto grid and more hardware queues
+  for rep in 1 2; do for cfg in "3:4" "4:12" "5:12" "6:12" "8:12"; do IFS=: read L Q <<< "$cfg"
+    GPU_MAX_HW_QUEUES=$Q one sweep_lanes4.jsonl --overlap $L
+  done; done
+fi
 if [[ $WHAT == costmax ]]; then
   # option "cost_max": claim order by a unit's longest path (x 64) instead of its summed cost; split levels
   for rep in 1 2; do for o in "--opt cost_max=0" "--opt cost_max=1" "--opt cost_max=1 --opt split=3598" "--opt cost_max=1 --opt split=65535"; do

@@ -46,6 +46,32 @@ def test_world1_comm_frames_equal_single_launch(gpu_lib):
     assert np.array_equal(r.render(2)[0], ref[2])       # detached: whole-frame launches again
 
 
+def test_world1_comm_eight_lanes_many_frames(gpu_lib):
+    """The multi-GPU share settings (8 lanes, the lane-scaled auto grid, 32x32 tiles): 24 frames cycled over
+    8 caller streams without waiting, more frames than frame blocks, so staging buffers and frame blocks are
+    reused while other lanes' traces, gathers and assembles are still in flight; every frame must equal its
+    single-launch frame (the per-launch completion events order each reuse after the launch that read it)."""
+    import torch
+    s = scenes.demo_with_particles(12)
+    W, H = 352, 208
+    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(W, H, ray_trace_depth=2)
+    F, L = 24, 8
+    ref = [r.render(f)[0] for f in range(F)]
+    r.attach_comm(Renderer.comm_unique_id(), 0, 1, 32, 32)
+    r.set_option("overlap", L)
+    lanes = [torch.cuda.Stream() for _ in range(L)]
+    bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(F)]
+    torch.cuda.synchronize()
+    for f in range(F):
+        r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=lanes[f % L].cuda_stream, sync=False)
+    r.synchronize()
+    torch.cuda.synchronize()
+    for f in range(F):
+        assert np.array_equal(bufs[f].cpu().numpy().reshape(H, W, 4), ref[f]), f
+    r.set_option("overlap", 0)
+    r.detach_comm()
+
+
 def test_comm_rejects_tiles_and_rgb(gpu_lib):
     s = scenes.demo_scene()
     r = Renderer(s).build_acceleration_structure(0).configure_camera(64, 64)
