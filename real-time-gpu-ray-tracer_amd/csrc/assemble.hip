@@ -15,7 +15,8 @@ namespace rtamd {
 // for a 1080p frame.)
 __global__ __launch_bounds__(256) void assemble_kernel(const uint32_t *__restrict__ gathered, uint32_t slab_tiles,
                                                        uint32_t tile_w, uint32_t tile_h, uint32_t tile_count,
-                                                       uint32_t width, uint32_t height, uint32_t *__restrict__ frame) {
+                                                       uint32_t width, uint32_t height, uint32_t *__restrict__ frame,
+                                                       bool frame_aligned) {
     const uint32_t g = blockIdx.x;
     const uint32_t rank = g / slab_tiles, k = g - rank * slab_tiles;
     const uint32_t t = rank + k * tile_count;
@@ -24,7 +25,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(const uint32_t *__restric
     const uint32_t x0 = (t % tiles_x) * tile_w, y0 = (t / tiles_x) * tile_h;
     const uint32_t *src = gathered + (size_t)g * tile_w * tile_h;
     const uint32_t per = (tile_w & 3u) == 0 ? 4u : 1u;                    // pixels per thread step (a row piece)
-    const bool vec = per == 4u && (width & 3u) == 0;
+    const bool vec = per == 4u && (width & 3u) == 0 && frame_aligned;   // 16 B stores need a 16 B-aligned frame
     for (uint32_t q = threadIdx.x; q < tile_w * tile_h / per; q += blockDim.x) {
         const uint32_t p = per * q, row = p / tile_w, col = p - row * tile_w;
         const uint32_t y = y0 + row, x = x0 + col;
@@ -45,7 +46,7 @@ hipError_t launch_assemble(const void *gathered, uint32_t slab_tiles, uint32_t t
     if (tile_w == 0 || tile_h == 0 || blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
     hipLaunchKernelGGL(assemble_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream,
                        static_cast<const uint32_t *>(gathered), slab_tiles, tile_w, tile_h, tile_count, width, height,
-                       static_cast<uint32_t *>(frame));
+                       static_cast<uint32_t *>(frame), (reinterpret_cast<uintptr_t>(frame) & 15u) == 0);
     return hipGetLastError();
 }
 

@@ -227,6 +227,14 @@ if [[ $WHAT == lanes4 ]]; then
     GPU_MAX_HW_QUEUES=$Q one sweep_lanes4.jsonl --overlap $L
   done; done
 fi
+if [[ $WHAT == order3 ]]; then
+  # claim-order cost and period under the auto threshold
+  for rep in 1 2; do for o in "--opt cost_max=0" "--opt cost_max=1" "--opt reorder_period=4" "--opt reorder_period=16"; do
+    one sweep_order3.jsonl $o
+    one sweep_order3.jsonl $o --overlap 1
+    one sweep_order3.jsonl $o --shard 4/8
+  done; done
+fi
 if [[ $WHAT == costmax ]]; then
   # option "cost_max": claim order by a unit's longest path (x 64) instead of its summed cost; split levels
   for rep in 1 2; do for o in "--opt cost_max=0" "--opt cost_max=1" "--opt cost_max=1 --opt split=3598" "--opt cost_max=1 --opt split=65535"; do
