@@ -28,7 +28,9 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 1u
+/* 2: rt_stats gained update_wait_ms; rt_comm_* / rt_slab_tiles / rt_tile_pixels / rt_scene_detach_comm;
+ *    rt_camera_move / rt_frame_pacer_* / rt_comm_set_timeout (round 3) */
+#define RT_ABI_VERSION 2u
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -204,6 +206,7 @@ typedef struct rt_stats {
     double update_wait_ms;     /* part of update_ms blocked on the GPU (a staging buffer still
                                   read by an earlier frame's copy); the rest is host compute */
 } rt_stats;
+/* sizeof(rt_stats) == 96 on LP64; a caller built against a different layout gets RT_ABI_VERSION != 2 */
 
 /* Closest-hit record for rt_trace_rays (per-ray parity tests). */
 typedef struct rt_hit {
@@ -300,23 +303,16 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "threshold" : persistent kernel — lanes that must be waiting before a wave leaves the
  *                 traversal loop to shade / regenerate (1..64; default 0 = auto: 64 when depth x samples <= 2,
  *                 else 40)
- *   "variant"   : persistent kernel register budget: 0 = compiler's choice, 4 / 5 = at least
- *                 4 / 5 waves per SIMD
+ *   "variant"   : persistent kernel register budget: 0 = compiler's choice, 4 = at least 4 waves per SIMD
  *   "queue_parts": persistent kernel work-queue bands (1..8, default 8; a wave starts on band XCC_ID % parts)
  *   "reorder"   : 1 (default) = each launch claims its band's 8x8 units heaviest-first, ordered by the
  *                 traversal work the previous launch of the same layout and lane recorded per unit (schedule.hip);
  *                 0 = screen order.  Images are identical either way (the RNG is keyed by pixel).
- *   "primary"   : FAST persistent kernel on quad trees: 1 = the first camera ray of every pixel is traced
- *                 beforehand by one wave per 8x8 unit walking the union of its rays' paths (wave-uniform
- *                 node / instance / primitive loads); 0 (default, measured faster) = traced inside the
- *                 persistent kernel
  *   "reorder_period": with "reorder", K = a lane records unit costs on one launch in K and rebuilds its
  *                 claim order on the next; the other launches reuse the order (default 8; 1 = every launch)
  *   "split"     : with "reorder", heavy units are claimed in pieces shared by several waves: halves from
  *                 cost level k_half, quarters from k_quarter (value k_half | k_quarter << 8, levels 0..15 =
  *                 half-octaves of a unit's mean traversal steps per pixel; 0xFF = never; default 12 | 12 << 8)
- *   "lean"      : 1 = FAST persistent kernel uses the LDS-only-stack traversal (default 0) when the
- *                 TLAS height + deepest BLAS height + 2 <= 24
  *   "nt_store"  : 1 = non-temporal RGBA8 stores
  *   "grab"      : pixels claimed per work-queue atomic (multiple of 8, default 64)
  *   "supertile" : walk each band in supertile x supertile units of 8x8 pixels (default 16; 0 = rows)
@@ -343,9 +339,6 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 the member instance; 0 = one TLAS item per instance)
  *   "lds_blas"  : with "lds_scene" 2 and "group": the top levels of the first group's BLAS (quads numbered level
  *                 by level) fill the rest of the LDS scene region (default 1; 0 = from HBM; results identical)
- *   "drain"     : persistent kernel: once a wave's claims fail (queue dry), a lane whose path segment ended is
- *                 shaded when 1/drain of the wave's remaining paths wait (1..64; default 0 = when "threshold"
- *                 lanes wait; results identical)
  *   "grid_pct"  : persistent grid as a percentage of the resident workgroup capacity (1..100; default 0 = auto:
  *                 100 when no other lane's launch is in flight, else 50 with up to 3 lanes and 120 / lanes
  *                 (at least 12) with more, so several lanes' launches run side by side)

@@ -230,11 +230,6 @@ struct OutputGPU {
     uint32_t queue_parts;
     uint32_t nt_store;              // 1: RGBA8 stores are non-temporal (keep the scene in L2)
     uint32_t grab;                  // pixels claimed per queue atomic
-    uint32_t claim_items;           // ordered walk ("reorder"): consecutive order items per queue atomic (1..2)
-    uint32_t mix;                   // ordered walk: a refill's first claim takes the band's heaviest item (front),
-                                    // its further claims the lightest (back): one 64-bit head {front, back}
-    uint32_t drain;                 // option "drain": once the wave's queue is dry, shade when 1/drain of its
-                                    // remaining paths wait (0: when `threshold` lanes wait, as before)
     uint32_t supertile;             // frame mode, grab 64: walk bands in supertile x supertile units (0 = rows)
     unsigned long long *timeline;   // TIMELINE_WORDS per wave (rt.h, rt_scene_debug_read)
     uint32_t *costmap;              // COUNT launches: traversal rounds per output pixel (debug)
@@ -244,14 +239,7 @@ struct OutputGPU {
     const uint32_t *order;
     uint32_t *unit_cost;
     uint32_t cost_max;              // 1: a unit's cost is 64 x its longest path (atomicMax), not the sum of its paths
-    // option "primary" (FAST, quad trees): the closest hits of every pixel's first camera ray, traced by
-    // primary_packet_kernel before the persistent launch; record j = work item j (unit * 64 + lane):
-    // {t, instance record (PREC_MISS / PREC_TRACE), ptype << 28 | slot, u} + v.  Null: traced in place.
-    uint32_t *prim_rec;             // 4 words per record (16 B aligned)
-    float *prim_v;
 };
-constexpr uint32_t PREC_MISS = 0xFFFFFFFFu;    // primary record: no hit
-constexpr uint32_t PREC_TRACE = 0xFFFFFFFEu;   // primary record: not resolved (packet stack full), trace it
 constexpr uint32_t QUEUE_STRIDE = 32;         // u32 words between partition heads (128 B lines)
 constexpr uint32_t QUEUE_MAX_PARTS = 8;
 // queue block of a lane: band heads (lines 0..7), band item counts (lines 8..15)
@@ -273,7 +261,6 @@ __host__ __device__ inline uint32_t split_log2(uint32_t cls, uint32_t k_half, ui
     return k >= k_quarter ? 2u : (k >= k_half ? 1u : 0u);
 }
 constexpr uint32_t TIMELINE_WORDS = 16;
-constexpr uint32_t LEAN_STACK = 24;       // LDS stack entries of the lean traversal
 
 // Counter slots (device uint64 array)
 enum CounterSlot : uint32_t {

@@ -34,20 +34,19 @@ hipError_t launch_trace_rays_exact(const SceneGPU &, const float *, uint32_t, rt
 hipError_t launch_trace_rays_fast(const SceneGPU &, const float *, uint32_t, rt_hit *, hipStream_t);
 hipError_t launch_assemble(const void *, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, void *, hipStream_t);
 hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
-                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
+                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
-                                         uint32_t *, uint32_t, uint32_t, uint32_t, bool, bool, hipStream_t);
+                                         uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
 hipError_t launch_frame_copy(void *, const void *, size_t, unsigned long long *, uint32_t *, hipStream_t);
-hipError_t launch_primary_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *, hipStream_t);
 hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t,
                            uint32_t, uint32_t, void *, const void *, size_t, unsigned long long *, hipStream_t);
-uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool lean, bool wide);
+uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool wide);
 hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t launch_instance_slot_order(const uint32_t *, const InstHot *, const InstCold *, uint32_t, InstHot *, InstCold *,
                                       hipStream_t);
 hipError_t launch_instance_update(const InstDelta *, uint32_t, InstParams *, uint32_t, InstHot *, InstCold *, float *, float4 *,
                                   hipStream_t);
-uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool lean, bool wide);
+uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool wide);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -241,28 +240,18 @@ struct rt_scene {
     // lanes at once), else 40 (C2 0.194 -> 0.184 ms/frame, serialised 0.35 -> 0.33 ms; C3 at 64 would lose
     // 23 %, 40 ties 32; profiles/r02_sweep_thr2.jsonl)
     uint32_t threshold = 0;
-    uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4, 5)
+    uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4)
     double update_wait_ms = 0.0;    // last frame_update: time blocked on ev_copied (GPU progress)
     bool use_persistent = true;
     uint32_t queue_parts = 8;       // one band per XCD (measured with "reorder": 8 beat 4, 2 and 1 on C2)
     uint32_t nt_store = 0;
     uint32_t grab = 64;             // pixels per queue claim
-    // ordered walk: order items per queue atomic (option "claim_items"); 2 measured slower (C2 kernel
-    // 0.39 -> 0.48 ms, 1/8 share 0.079 -> 0.107 ms/frame: the heaviest items head the order, and a wave
-    // given two of them runs both back to back; profiles/r02_sweep_claim_items.jsonl)
-    uint32_t claim_items = 1;
-    uint32_t mix = 0;
     uint32_t cost_max = 0;
     // option "merge": two adjacent units below this cost level share one claim item (128 pixels): 6 (sky, about
     // 4 steps per pixel) measured C2 0.203 -> 0.199 ms/frame; 8 or 10 (also the ground) put 128-pixel items at
     // the end of the order and lengthen the tail (profiles/r02_sweep_merge.jsonl)
     uint32_t merge = 6;
-    // option "drain": after a wave's last failed claim, a lane whose segment ended shades as soon as 1/drain of the
-    // wave's remaining paths wait, instead of waiting for `threshold` lanes (which, with fewer paths left than
-    // the threshold, meant waiting for every other lane's segment)
-    uint32_t drain = 0;
     uint32_t supertile = 16;        // band walk order: st x st-unit supertiles (measured: 16 beats rows, 8 and 32)
-    bool lean = false;              // FAST persistent kernel: LDS-only-stack traversal when the trees fit (measured slower on C2)
     uint32_t max_blas_height = 0;
     bool timeline_on = false;
     bool costmap_on = false;
@@ -272,11 +261,6 @@ struct rt_scene {
     // shares, profiles/r02_sweep_period*.jsonl): quarters from level 12 and no halves
     uint32_t split = 12u | 12u << 8;
     DevBuf<uint32_t> unit_cost[NLANE], unit_order[NLANE];
-    // option "primary" (FAST persistent kernel on quad trees): per-lane records of the packet-traced
-    // first camera rays (OutputGPU::prim_rec), one per work item
-    bool primary = false;               // measured slower (C2: packet kernel 0.22 ms vs ~0.08 ms of in-kernel primary traversal)
-    DevBuf<uint32_t> prim_rec[NLANE];
-    DevBuf<float> prim_v[NLANE];
     uint32_t sched_sig[NLANE][7] = {};  // launch layout the recorded costs belong to
     // option "reorder_period" K: a lane records unit costs on one launch in K and rebuilds its order on
     // the next; the launches between reuse the order (the heaviest regions move little between frames)
@@ -362,7 +346,7 @@ struct rt_scene {
         blas_pairs.release(); blas_quads.release(); tri_hot.release(); tri_cold.release(); sph_hot.release(); sph_cold.release();
         quad_hot.release(); quad_cold.release(); materials.release(); out_rgba.release(); out_rgb.release();
         timeline.release(); costmap.release();
-        for (int q = 0; q < NLANE; q++) { unit_cost[q].release(); unit_order[q].release(); prim_rec[q].release(); prim_v[q].release(); }
+        for (int q = 0; q < NLANE; q++) { unit_cost[q].release(); unit_order[q].release(); }
         delete blas_builder; delete tlas_builder;
         raw_tris.release(); raw_sph.release(); raw_quad.release(); blas_roots.release(); inst_blas.release();
         blas_wide_refs.release();
@@ -1393,18 +1377,13 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     const bool exact = (o.flags & RT_RENDER_EXACT) != 0;
     const bool count = (o.flags & RT_RENDER_COUNT_WORK) != 0;
 
-    // lean traversal: FAST kernel, LDS-only stack deep enough for TLAS + deepest BLAS (+ 2 resume entries)
-    const bool lean = !exact && s->lean && !s->gpu_tlas() && s->tlas_flat.height + s->max_blas_height + 2 <= LEAN_STACK;
     if (s->use_persistent) {
         out.queue_parts = s->queue_parts;
         out.grab = s->grab;
-        out.claim_items = s->claim_items;
-        out.mix = s->mix;
-        out.drain = s->drain;
         out.supertile = s->supertile;
         if (s->timeline_on) {
-            const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false, false)
-                                                    : persistent_blocks_per_cu_fast(s->variant, lean, g.wide != 0));
+            const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false)
+                                                    : persistent_blocks_per_cu_fast(s->variant, g.wide != 0));
             const size_t words = (size_t)blocks * 4 * TIMELINE_WORDS;
             if (s->timeline.n < words) {
                 s->timeline.release();
@@ -1508,24 +1487,9 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     if (s->ring_pending < rt_scene::RING) s->ring_pending++;
     s->last_stream = stream;
     HIP_TRY(hipEventRecord(s->ring_start[slot], stream));
-    if (s->use_persistent && !exact && !lean && g.wide && s->primary) {
-        // the first camera ray of every pixel, packet-traced per 8x8 unit (trace_kernel.hip)
-        const size_t n = (size_t)out.units * 64;
-        if (s->prim_rec[q].n < 4 * n) {
-            s->prim_rec[q].release();
-            s->prim_v[q].release();
-            HIP_TRY(hipMalloc(&s->prim_rec[q].p, 4 * n * sizeof(uint32_t)));
-            s->prim_rec[q].n = 4 * n;
-            HIP_TRY(hipMalloc(&s->prim_v[q].p, n * sizeof(float)));
-            s->prim_v[q].n = n;
-        }
-        out.prim_rec = s->prim_rec[q].p;
-        out.prim_v = s->prim_v[q].p;
-        HIP_TRY(launch_primary_fast(g, cam, out, count, lane_counters, stream));
-    }
     if (s->use_persistent) {
-        const uint32_t cap = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false, false)
-                                             : persistent_blocks_per_cu_fast(s->variant, lean, g.wide != 0));
+        const uint32_t cap = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false)
+                                             : persistent_blocks_per_cu_fast(s->variant, g.wide != 0));
         uint32_t blocks = s->overlap && cap > 2 * s->reserve ? cap - s->reserve : cap;
         uint32_t pct = s->grid_pct;
         if (pct == 0) {
@@ -1539,9 +1503,9 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         if (pct < 100) blocks = std::max<uint32_t>(8u, blocks * pct / 100u);
         const uint32_t thr = s->threshold ? s->threshold : (cam.depth * cam.sqrt_s * cam.sqrt_s <= 2u ? 64u : 40u);
         HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, lane_counters, s->queue[q], blocks, thr,
-                                                       s->variant, false, reset_queue, stream)
+                                                       s->variant, reset_queue, stream)
                       : launch_render_persistent_fast(g, cam, out, count, lane_counters, s->queue[q], blocks, thr,
-                                                      s->variant, lean, reset_queue, stream));
+                                                      s->variant, reset_queue, stream));
     }
     else
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, lane_counters, stream)
@@ -1648,14 +1612,11 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         if (value < 0 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "threshold must be in 0..64 (0 = auto)");
         s->threshold = (uint32_t)value;
     } else if (k == "variant") {
-        if (value != 0 && value != 4 && value != 5) return fail(RT_ERR_INVALID_ARGUMENT, "variant must be 0, 4 or 5");
+        if (value != 0 && value != 4) return fail(RT_ERR_INVALID_ARGUMENT, "variant must be 0 or 4");
         s->variant = (uint32_t)value;
     } else if (k == "queue_parts") {
         if (value < 1 || value > (int64_t)QUEUE_MAX_PARTS) return fail(RT_ERR_INVALID_ARGUMENT, "queue_parts must be in 1..8");
         s->queue_parts = (uint32_t)value;
-    } else if (k == "lean") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "lean must be 0 or 1");
-        s->lean = value == 1;
     } else if (k == "nt_store") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "nt_store must be 0 or 1");
         s->nt_store = (uint32_t)value;
@@ -1685,15 +1646,6 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "cost_max") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "cost_max must be 0 or 1");
         s->cost_max = (uint32_t)value;
-    } else if (k == "drain") {
-        if (value < 0 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "drain must be in 0..64");
-        s->drain = (uint32_t)value;
-    } else if (k == "mix") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "mix must be 0 or 1");
-        s->mix = (uint32_t)value;
-    } else if (k == "claim_items") {
-        if (value < 1 || value > 2) return fail(RT_ERR_INVALID_ARGUMENT, "claim_items must be 1 or 2");
-        s->claim_items = (uint32_t)value;
     } else if (k == "grid_pct") {
         if (value < 0 || value > 100) return fail(RT_ERR_INVALID_ARGUMENT, "grid_pct must be in 0..100 (0 = auto)");
         s->grid_pct = (uint32_t)value;
@@ -1742,9 +1694,6 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "reserve") {
         if (value < 0 || value > 256) return fail(RT_ERR_INVALID_ARGUMENT, "reserve must be in 0..256");
         s->reserve = (uint32_t)value;
-    } else if (k == "primary") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "primary must be 0 or 1");
-        s->primary = value == 1;
     } else if (k == "reorder_period") {
         if (value < 1 || value > 1024) return fail(RT_ERR_INVALID_ARGUMENT, "reorder_period must be in 1..1024");
         s->reorder_period = (uint32_t)value;

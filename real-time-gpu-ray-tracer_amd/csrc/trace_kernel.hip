@@ -49,38 +49,12 @@ constexpr int BLOCK = 256;              // 4 waves; each wave owns one 8x8 pixel
 #ifndef RT_LDS_MATERIALS
 #define RT_LDS_MATERIALS 64              // the scene region ("lds_scene") needs the rest of the 52 KB
 #endif
-#ifndef RT_PATH_LDS
-#define RT_PATH_LDS 0                   // 1: the persistent kernel keeps path state (throughput, radiance,
-#endif                                  //    RNG, pixel, sample / depth) in LDS between shade steps
 constexpr int LDS_DEPTH = RT_LDS_DEPTH;         // per-lane stack entries kept in LDS
 constexpr int LDS_MATERIALS = RT_LDS_MATERIALS; // persistent kernel: material table in LDS up to this many slots
-constexpr int PATH_WORDS = 10;                  // RT_PATH_LDS: acc xyz, thr xyz, rng lo / hi, item, sample << 16 | depth
 constexpr int SPILL_DEPTH = 48;         // overflow entries in scratch (max depth 64 = reference)
-#ifndef RT_WIDE_PUSH3
-#define RT_WIDE_PUSH3 1                 // quad step: far hits to 3 LDS slots without branching on their count (+1.6 %)
-#endif
-#ifndef RT_LEAN_WIDE
-#define RT_LEAN_WIDE 0                  // 1: quad trees take the lean one-pop-per-step loop (lw_*; measured slower)
-#endif
-#ifndef RT_HEAVY_PRIO
-#define RT_HEAVY_PRIO 0                 // 1 (measured neutral, C3 -3 %, profiles/r02_ab_heavy_prio.jsonl): ordered walk: a wave holding pixels of a split (heaviest-class) unit
-                                        // issues at raised priority (s_setprio), so the launch's critical
-                                        // paths are not queued behind light waves that have slack
-#endif
-#ifndef RT_INLINE_INST
-#define RT_INLINE_INST 0                // 1: quad trees: a lane reaching a TLAS leaf enters the instance inside the
-                                        // interior loop (instance record from LDS) instead of in a leaf round;
-                                        // measured 25-50 % slower (C2 kernel 0.370 -> 0.463 ms, C3 2.75 -> 4.12 ms:
-                                        // lanes that no longer stop at instances diverge deeper inside the loop),
-                                        // profiles/r02_ab_inline_instance.jsonl
-#endif
 #ifndef RT_CHAIN_ROOT_LEAF
 #define RT_CHAIN_ROOT_LEAF 1            // quad trees: an entered instance whose BLAS root is a leaf (a sphere, a
                                         // parallelogram, a small mesh) has it tested in the same leaf round
-#endif
-#ifndef RT_FLAT_QUADS
-#define RT_FLAT_QUADS 1                 // quad nodes read through one generic (flat) pointer, LDS or HBM: no
-                                        // branch + register copies per step (C2 -2 %, serialised -3 %, C3 -3 %)
 #endif
 #ifndef RT_WIDE_TINY
 #define RT_WIDE_TINY 0                  // 1: quad steps take the reference's parallel-axis slab (BoundingBox.cu:44-50)
@@ -189,8 +163,7 @@ struct RayP {
 __device__ __forceinline__ void prep(RayP &r) {
 #if !RT_EXACT
     r.tiny = fabsf(r.d.x) < FZERO || fabsf(r.d.y) < FZERO || fabsf(r.d.z) < FZERO;
-    // |d| < 1e-20 -> +-1e-20: finite reciprocals, so the branch-free slab of the lean traversal
-    // never forms 0 * inf
+    // |d| < 1e-20 -> +-1e-20: finite reciprocals, so a branch-free slab never forms 0 * inf
     const auto nz = [](float x) { return fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x; };
     r.inv = mk(rcp(nz(r.d.x)), rcp(nz(r.d.y)), rcp(nz(r.d.z)));
     r.oinv = mk(r.o.x * r.inv.x, r.o.y * r.inv.y, r.o.z * r.inv.z);
@@ -392,7 +365,7 @@ __device__ __forceinline__ SEnt stack_pop(Stack &stk, const SEnt *spill) {   // 
 
 // Page the bottom half of the LDS window out when fewer than 3 slots are free (sp > HALF; slots >= sp
 // are free space, moved along harmlessly).
-__device__ __forceinline__ void lw_page_out(Stack &stk, SEnt *spill, LaneCount &c) {   // sp > HALF
+__device__ __forceinline__ void stack_page_out3(Stack &stk, SEnt *spill, LaneCount &c) {   // sp > HALF
     if (stk.spilled + HALF > SPILL_DEPTH) {
         c.overflow++;
         stk.spilled = SPILL_DEPTH - HALF;
@@ -419,7 +392,6 @@ struct Trav {
     Hit hit;
     bool found;
     bool tracing;
-    bool in_blas;          // lean traversal: lr holds the instance ray (else lr == wr)
     Stack stk;
 };
 
@@ -433,7 +405,6 @@ __device__ __forceinline__ void trav_init(Trav &T, const TreeRoot &R, const f3 &
     T.stk.spilled = 0;
     T.cur = R.ref;
     T.cur_inst = 0;
-    T.in_blas = false;
     T.pleaf = REF_NONE;
     float te = 0.0f;
     T.tracing = slab(R.box, T.wr, TMIN, T.tmax, te);                     // root pop test (TLAS.cu:150)
@@ -638,7 +609,6 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
     const bool blas = (cur & REF_BLAS) != 0;
     float4 lx, hx, ly, hy, lz, hz;
     uint4 R;
-#if RT_FLAT_QUADS
     // one code path: a generic pointer into the LDS scene region or HBM (flat loads serve both)
     {
         const uint32_t qi = cur & REF_INDEX_MASK, qb = qi - sc.lds_bq0;
@@ -649,18 +619,6 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
         lx = Q[0]; hx = Q[1]; ly = Q[2]; hy = Q[3]; lz = Q[4]; hz = Q[5];
         R = reinterpret_cast<const uint4 *>(Q)[6];
     }
-#else
-    if (!blas && sc.lds_quads) {
-        const float4 *Q = lds_scene + (cur & REF_INDEX_MASK) * LDS_QUAD_F4;
-        lx = Q[0]; hx = Q[1]; ly = Q[2]; hy = Q[3]; lz = Q[4]; hz = Q[5];
-        const float4 r = Q[6];
-        R = make_uint4(__float_as_uint(r.x), __float_as_uint(r.y), __float_as_uint(r.z), __float_as_uint(r.w));
-    } else {
-        const float4 *Q = reinterpret_cast<const float4 *>((blas ? sc.blas_quads : sc.tlas_quads) + (cur & REF_INDEX_MASK));
-        lx = Q[0]; hx = Q[1]; ly = Q[2]; hy = Q[3]; lz = Q[4]; hz = Q[5];
-        R = reinterpret_cast<const uint4 *>(Q)[6];
-    }
-#endif
     if (COUNT) cnt.pairs += 2;                       // 4 child boxes = 2 node-pair equivalents
     const RayP &r = blas ? T.lr : T.wr;
     float t[4];
@@ -690,11 +648,10 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
     if (nh == 0) { pop_next(T, spill); return; }
     // sort the 4 (t, ref) ascending; misses (t = inf) sink to the end
     cswap(t0, r0, t1, r1); cswap(t2, r2, t3, r3); cswap(t0, r0, t2, r2); cswap(t1, r1, t3, r3); cswap(t1, r1, t2, r2);
-#if RT_WIDE_PUSH3
     // the 1..3 far hits go to the three LDS slots above the top without branching on their count
     // (farthest first; the slots past the new top are free space), after one page-out check
     if (nh > 1) {
-        if (T.stk.sp > LDS_DEPTH - 3) lw_page_out(T.stk, spill, cnt);
+        if (T.stk.sp > LDS_DEPTH - 3) stack_page_out3(T.stk, spill, cnt);
         SEnt a, b, c;
         a.ref = nh == 4 ? r3 : (nh == 3 ? r2 : r1);
         a.tn = __float_as_uint(nh == 4 ? t3 : (nh == 3 ? t2 : t1));
@@ -707,36 +664,8 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
         T.stk.lds[(T.stk.sp + 2) * BLOCK] = pack(c);
         T.stk.sp += (int)nh - 1;
     }
-#else
-    if (nh > 3) stack_push(T.stk, spill, r3, t3, cnt);
-    if (nh > 2) stack_push(T.stk, spill, r2, t2, cnt);
-    if (nh > 1) stack_push(T.stk, spill, r1, t1, cnt);
-#endif
     T.cur = r0;
     T.curT = t0;
-}
-#endif
-
-#if !RT_EXACT
-// Instance::hit entry (Instance.cu:19-35) of the TLAS leaf in T.cur: the ray into the instance's space,
-// then the BLAS root (or the next stack entry if its box is missed).  Entering an instance changes no
-// tmax, so it needs no leaf round of its own: with the record in LDS ("lds_scene") it costs no memory
-// round trip either.  A lane only enters while it holds no postponed leaf (whose test needs T.lr).
-template <bool COUNT>
-__device__ __forceinline__ void enter_instance(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
-    const uint32_t start = ref_leaf_start(T.cur), count = ref_leaf_count(T.cur);
-    if (count > 1) stack_push(T.stk, spill, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
-    T.cur_inst = sc.inst_by_slot ? start : sc.tlas_slots[start];
-    if (COUNT) cnt.inst++;
-    const InstRec I = load_inst<true>(sc, T.cur_inst);
-    const float inv[12] = {I.i0.x, I.i0.y, I.i0.z, I.i0.w, I.i1.x, I.i1.y, I.i1.z, I.i1.w, I.i2.x, I.i2.y, I.i2.z, I.i2.w};
-    const float box[6] = {I.box01.x, I.box01.y, I.box01.z, I.box01.w, I.box2ref.x, I.box2ref.y};
-    T.lr.o = xf_point(inv, T.wr.o);                            // Instance.cu:26-27
-    T.lr.d = xf_vector(inv, T.wr.d);
-    prep(T.lr);
-    float te = 0.0f;
-    if (slab(box, T.lr, TMIN, T.tmax, te)) { T.cur = __float_as_uint(I.box2ref.w); T.curT = te; }
-    else pop_next(T, spill);
 }
 #endif
 
@@ -746,7 +675,6 @@ __device__ __forceinline__ void spec_interior_step(Trav &T, const SceneGPU &sc, 
 #if !RT_EXACT
     if (WIDE) {
         if (!(cur & REF_LEAF)) wide_interior_step<COUNT>(T, sc, spill, cnt);
-        else if (RT_INLINE_INST && !(cur & REF_BLAS)) enter_instance<COUNT>(T, sc, spill, cnt);
         else { T.pleaf = cur; pop_next(T, spill); }        // postpone, keep walking
         return;
     }
@@ -938,352 +866,6 @@ __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *sp
     }
     DIAG_ADD(pc.leaf, t1);
 }
-
-constexpr int LEAN_DEPTH = (int)LEAN_STACK;   // lean traversal: LDS-only stack entries
-#if !RT_EXACT
-// ---- lean traversal (FAST kernel on shallow trees) ----------------------------------------
-// Same speculative while-while order as spec_*, written for a short, mostly straight-line loop body
-// (divergent branches cost exec-mask bookkeeping on every step):
-//   * the stack lives in LDS only (LEAN_DEPTH entries; the host picks this path only when the TLAS
-//     height + the deepest BLAS height + 2 fits), so push/pop carry no paging code;
-//   * a step pops at most one entry: a lane that needs a node marks cur = REF_POP and pops at the
-//     start of its next step; a popped entry that fails its re-test (entry t >= tmax) is marked
-//     REF_POP again, so the reference's pop loop becomes one pop per step;
-//   * push is unconditional (the slot above the top is scratch space; sp only advances on a push);
-//   * one active ray: lr is the world ray in the TLAS and the instance ray inside a BLAS; a lane
-//     holding a postponed BLAS leaf does not cross back into the TLAS until the leaf is tested;
-//   * branch-free slabs on clamped reciprocals (prep), no parallel-axis path.
-constexpr uint32_t REF_POP = 0xFFFFFFFEu;    // marker: pop the next entry (leaf bit + type 3)
-__device__ __forceinline__ bool ref_is_marker(uint32_t r) { return (r & 0xF0000000u) == 0xF0000000u; }
-
-__device__ __forceinline__ bool slab_lean(float x0, float x1, float y0, float y1, float z0, float z1, const RayP &r,
-                                          float tmax, float &te) {
-    const float tx1 = fmaf(x0, r.inv.x, -r.oinv.x), tx2 = fmaf(x1, r.inv.x, -r.oinv.x);
-    const float ty1 = fmaf(y0, r.inv.y, -r.oinv.y), ty2 = fmaf(y1, r.inv.y, -r.oinv.y);
-    const float tz1 = fmaf(z0, r.inv.z, -r.oinv.z), tz2 = fmaf(z1, r.inv.z, -r.oinv.z);
-    const float lo = fmaxf(fmaxf(TMIN, fminf(tx1, tx2)), fmaxf(fminf(ty1, ty2), fminf(tz1, tz2)));
-    const float hi = fminf(fminf(tmax, fmaxf(tx1, tx2)), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
-    te = lo;
-    return lo < hi;
-}
-__device__ __forceinline__ void lean_push(Trav &T, uint32_t ref, float tn, bool do_push, LaneCount &c) {
-    SEnt e;
-    e.ref = ref;
-    e.tn = __float_as_uint(tn);
-    const int slot = T.stk.sp < LEAN_DEPTH ? T.stk.sp : LEAN_DEPTH - 1;
-    if (do_push) {
-        if (T.stk.sp >= LEAN_DEPTH) c.overflow++;
-        T.stk.lds[slot * BLOCK] = pack(e);
-        T.stk.sp = min(T.stk.sp + 1, LEAN_DEPTH);
-    }
-}
-
-// One step of a lane that may step: pop / re-test, postpone a leaf, or test a node pair.
-template <bool COUNT>
-__device__ __forceinline__ void lean_step(Trav &T, const SceneGPU &sc, LaneCount &cnt) {
-    uint32_t cur = T.cur;
-    float curT = T.curT;
-    if (cur == REF_POP) {                                   // pop one entry, re-test it (BLAS.cu:145)
-        const int top = T.stk.sp > 0 ? T.stk.sp - 1 : 0;
-        const SEnt e = unpack(T.stk.lds[top * BLOCK]);
-        if (T.stk.sp > 0) {
-            T.stk.sp = top;
-            cur = __uint_as_float(e.tn) < T.tmax ? e.ref : REF_POP;
-            curT = __uint_as_float(e.tn);
-        } else {
-            cur = REF_NONE;
-        }
-    }
-    const bool blocked = T.pleaf != REF_NONE && T.in_blas && !ref_is_marker(cur) && !(cur & REF_BLAS);
-    if (!ref_is_marker(cur) && !blocked) {
-        if (T.in_blas && !(cur & REF_BLAS)) { T.lr = T.wr; T.in_blas = false; }   // back in the TLAS
-        if (cur & REF_LEAF) {
-            if (T.pleaf == REF_NONE) { T.pleaf = cur; cur = REF_POP; }            // postpone, keep walking
-        } else {
-            const NodePair *P = ((cur & REF_BLAS) ? sc.blas_pairs : sc.tlas_pairs) + (cur & REF_INDEX_MASK);
-            const float4 *P4 = reinterpret_cast<const float4 *>(P);
-            const float4 A = P4[0], B = P4[1], C = P4[2];
-            const uint4 D = reinterpret_cast<const uint4 *>(P)[3];
-            if (COUNT) cnt.pairs++;
-            float e0, e1;
-            const bool h0 = slab_lean(A.x, A.y, A.z, A.w, B.x, B.y, T.lr, T.tmax, e0);
-            const bool h1 = slab_lean(B.z, B.w, C.x, C.y, C.z, C.w, T.lr, T.tmax, e1);
-            const bool right_near = h0 && h1 && e0 > e1;          // TLAS.cu:185-192 ordering
-            lean_push(T, right_near ? D.x : D.y, right_near ? e0 : e1, h0 && h1, cnt);
-            const bool go0 = h0 && !right_near;
-            cur = go0 ? D.x : (h1 ? D.y : REF_POP);
-            curT = go0 ? e0 : e1;
-        }
-    }
-    T.cur = cur;
-    T.curT = curT;
-}
-
-template <bool COUNT>
-__device__ __forceinline__ void lean_leaf_phase(Trav &T, const SceneGPU &sc, LaneCount &cnt) {
-    const uint32_t leaf = T.pleaf;
-    T.pleaf = REF_NONE;
-    if (!(leaf & REF_BLAS)) {
-        // TLAS leaf (lane is in the TLAS: lr == wr): successor and remaining instances wait on the stack
-        const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf);
-        lean_push(T, T.cur, T.curT, !ref_is_marker(T.cur), cnt);
-        lean_push(T, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), count > 1, cnt);
-        T.cur_inst = sc.inst_by_slot ? start : sc.tlas_slots[start];
-        const InstHot &I = sc.inst_hot[T.cur_inst];
-        if (COUNT) cnt.inst++;
-        T.lr.o = xf_point(I.inv, T.wr.o);                      // Instance.cu:26-27
-        T.lr.d = xf_vector(I.inv, T.wr.d);
-        prep(T.lr);
-        T.in_blas = true;
-        float te;
-        const bool h = slab_lean(I.root_box[0], I.root_box[1], I.root_box[2], I.root_box[3], I.root_box[4],
-                                 I.root_box[5], T.lr, T.tmax, te);
-        T.cur = h ? I.root_ref : REF_POP;
-        T.curT = te;
-    } else {
-        const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf), type = ref_leaf_type(leaf);
-        for (uint32_t k = 0; k < count; k++) {
-            const uint32_t slot = start + k;
-            float t = 0.0f, u = 0.0f, v = 0.0f;
-            bool h;
-            if (type == RT_PRIM_TRIANGLE) {
-                if (COUNT) cnt.tri++;
-                h = tri_test(sc.tri_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
-            } else if (type == RT_PRIM_SPHERE) {
-                if (COUNT) cnt.sq++;
-                h = sphere_test(sc.sph_hot[slot], T.lr, TMIN, T.tmax, t);
-            } else {
-                if (COUNT) { cnt.sq++; cnt.quad++; }
-                h = quad_test(sc.quad_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
-            }
-            if (h) {
-                T.found = true; T.tmax = t;
-                T.hit.t = t; T.hit.inst = T.cur_inst; T.hit.ptype = type; T.hit.slot = slot; T.hit.u = u; T.hit.v = v;
-            }
-        }
-        if (!ref_is_marker(T.cur) && !(T.curT < T.tmax)) T.cur = REF_POP;   // re-test the successor
-    }
-    if (T.cur == REF_POP && T.stk.sp == 0) T.cur = REF_NONE;
-    if (T.cur == REF_NONE) T.tracing = false;
-}
-
-// lane takes a step this iteration: tracing, not finished, and not waiting at a second leaf
-__device__ __forceinline__ bool lean_active(const Trav &T) {
-    return T.tracing && T.cur != REF_NONE && !(T.pleaf != REF_NONE && (T.cur & REF_LEAF) && !ref_is_marker(T.cur));
-}
-
-template <bool COUNT>
-__device__ __forceinline__ void lean_round(Trav &T, const SceneGPU &sc, LaneCount &cnt, PhaseCycles &pc,
-                                           uint32_t &steps, bool track) {
-    DIAG_T(t0);
-    for (;;) {
-        if (T.tracing && T.pleaf == REF_NONE && T.cur == REF_NONE) T.tracing = false;   // done, no leaf left
-        if (!__any(T.tracing && T.pleaf == REF_NONE)) break;
-        if (lean_active(T)) {
-            lean_step<COUNT>(T, sc, cnt);
-            if (track) steps++;
-        }
-        if (RT_DIAG) pc.iters++;
-    }
-    DIAG_ADD(pc.interior, t0);
-    DIAG_T(t1);
-    if (T.tracing) {
-        lean_leaf_phase<COUNT>(T, sc, cnt);
-        if (track) steps++;
-    }
-    DIAG_ADD(pc.leaf, t1);
-}
-
-// ---- lean quad traversal (FAST kernel, option "wide") ---------------------------------------
-// The quad-tree form of the lean loop: one straight-line step per iteration, built for the cost
-// model of a 64-wide wave where every divergent branch costs exec-mask bookkeeping for all lanes:
-//   * one active ray (lr: the world ray in the TLAS, the instance ray inside a BLAS).  The world ray
-//     keeps only o, d (T.wr.o / T.wr.d); crossing back into the TLAS re-derives its reciprocals
-//     (prep is deterministic, so the slabs see the same values as at trav_init);
-//   * a step pops at most one entry (cur = REF_POP marks "pop at the start of the next step") and
-//     then tests the popped node in the same step;
-//   * a quad's 1..3 far hits are written to the three LDS slots above the top without branching on
-//     their count (the slots above the top are free), and sp advances by nh - 1;
-//   * the LDS window pages its bottom half to scratch only when fewer than 3 slots are free (a
-//     uniform branch no lane takes on shallow trees), so deep trees keep the reference's capacity.
-// Leaves are processed in the same speculative while-while order as spec_* (same closest hit).
-__device__ __forceinline__ void lw_to_world(Trav &T) {        // back in the TLAS: the world ray is active
-    T.lr.o = T.wr.o;
-    T.lr.d = T.wr.d;
-    prep(T.lr);
-    T.in_blas = false;
-}
-
-template <bool COUNT>
-__device__ __forceinline__ void lw_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
-    uint32_t cur = T.cur;
-    float curT = T.curT;
-    if (cur == REF_POP) {                                   // pop one entry, re-test it (BLAS.cu:145)
-        if (T.stk.sp == 0 && T.stk.spilled > 0) stack_page_in(T.stk, spill);
-        if (T.stk.sp > 0) {
-            T.stk.sp--;
-            const SEnt e = unpack(T.stk.lds[T.stk.sp * BLOCK]);
-            curT = __uint_as_float(e.tn);
-            cur = curT < T.tmax ? e.ref : REF_POP;
-        } else {
-            cur = REF_NONE;
-        }
-    }
-    const bool blocked = T.pleaf != REF_NONE && T.in_blas && !ref_is_marker(cur) && !(cur & REF_BLAS);
-    if (!ref_is_marker(cur) && !blocked) {
-        if (T.in_blas && !(cur & REF_BLAS)) lw_to_world(T);
-        if (cur & REF_LEAF) {
-            if (T.pleaf == REF_NONE) { T.pleaf = cur; cur = REF_POP; }            // postpone, keep walking
-        } else {
-            const bool blas = (cur & REF_BLAS) != 0;
-            const float4 *Q = reinterpret_cast<const float4 *>((blas ? sc.blas_quads : sc.tlas_quads) + (cur & REF_INDEX_MASK));
-            const float4 lx = Q[0], hx = Q[1], ly = Q[2], hy = Q[3], lz = Q[4], hz = Q[5];
-            const uint4 R = reinterpret_cast<const uint4 *>(Q)[6];
-            if (COUNT) cnt.pairs += 2;
-            const RayP &r = T.lr;
-            float t[4];
-            bool h[4];
-            if (!r.tiny) {
-                float4 tn = make_float4(TMIN, TMIN, TMIN, TMIN), tf = make_float4(T.tmax, T.tmax, T.tmax, T.tmax);
-                slab4(lx, hx, r.inv.x, r.oinv.x, tn, tf);
-                slab4(ly, hy, r.inv.y, r.oinv.y, tn, tf);
-                slab4(lz, hz, r.inv.z, r.oinv.z, tn, tf);
-                t[0] = tn.x; t[1] = tn.y; t[2] = tn.z; t[3] = tn.w;
-                h[0] = tn.x < tf.x; h[1] = tn.y < tf.y; h[2] = tn.z < tf.z; h[3] = tn.w < tf.w;
-            } else {
-                const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
-                const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
-                const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const float b[6] = {LX[k], HX[k], LY[k], HY[k], LZ[k], HZ[k]};
-                    t[k] = 0.0f;
-                    h[k] = slab_ref(b, r.o, r.d, TMIN, T.tmax, t[k]);
-                }
-            }
-            float t0 = h[0] ? t[0] : __builtin_huge_valf(), t1 = h[1] ? t[1] : __builtin_huge_valf();
-            float t2 = h[2] ? t[2] : __builtin_huge_valf(), t3 = h[3] ? t[3] : __builtin_huge_valf();
-            uint32_t r0 = R.x, r1 = R.y, r2 = R.z, r3 = R.w;
-            const uint32_t nh = (uint32_t)h[0] + (uint32_t)h[1] + (uint32_t)h[2] + (uint32_t)h[3];
-            cswap(t0, r0, t1, r1); cswap(t2, r2, t3, r3); cswap(t0, r0, t2, r2); cswap(t1, r1, t3, r3); cswap(t1, r1, t2, r2);
-            if (nh > 1) {
-                if (T.stk.sp > LDS_DEPTH - 3) lw_page_out(T.stk, spill, cnt);
-                // farthest first: slot sp + j holds hit nh-1-j (j <= nh-2); the other slots are free space
-                SEnt a, b, c;
-                a.ref = nh == 4 ? r3 : (nh == 3 ? r2 : r1);
-                a.tn = __float_as_uint(nh == 4 ? t3 : (nh == 3 ? t2 : t1));
-                b.ref = nh == 4 ? r2 : r1;
-                b.tn = __float_as_uint(nh == 4 ? t2 : t1);
-                c.ref = r1;
-                c.tn = __float_as_uint(t1);
-                T.stk.lds[T.stk.sp * BLOCK] = pack(a);
-                T.stk.lds[(T.stk.sp + 1) * BLOCK] = pack(b);
-                T.stk.lds[(T.stk.sp + 2) * BLOCK] = pack(c);
-                T.stk.sp += (int)nh - 1;
-            }
-            cur = nh ? r0 : REF_POP;
-            curT = t0;
-        }
-    }
-    T.cur = cur;
-    T.curT = curT;
-}
-
-template <bool COUNT>
-__device__ __forceinline__ void lw_leaf_phase(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
-    const uint32_t leaf = T.pleaf;
-    T.pleaf = REF_NONE;
-    if (!(leaf & REF_BLAS)) {
-        // TLAS leaf (the lane is in the TLAS): the successor and the leaf's remaining instances wait on
-        // the stack (popped in reference order), then the first instance's BLAS is entered
-        const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf);
-        if (!ref_is_marker(T.cur)) stack_push(T.stk, spill, T.cur, T.curT, cnt);
-        if (count > 1) stack_push(T.stk, spill, make_leaf_ref(start + 1, count - 1, 0, false), -__builtin_huge_valf(), cnt);
-        T.cur_inst = sc.inst_by_slot ? start : sc.tlas_slots[start];
-        const InstHot &I = sc.inst_hot[T.cur_inst];
-        if (COUNT) cnt.inst++;
-        T.lr.o = xf_point(I.inv, T.wr.o);                      // Instance.cu:26-27
-        T.lr.d = xf_vector(I.inv, T.wr.d);
-        prep(T.lr);
-        T.in_blas = true;
-        float te = 0.0f;
-        const bool h = slab(I.root_box, T.lr, TMIN, T.tmax, te);
-        T.cur = h ? I.root_ref_wide : REF_POP;
-        T.curT = te;
-    } else {
-        const uint32_t start = ref_leaf_start(leaf), count = ref_leaf_count(leaf), type = ref_leaf_type(leaf);
-        if (type == RT_PRIM_TRIANGLE) {
-            for (uint32_t k0 = 0; k0 < count; k0 += TRI_AHEAD) {
-                TriHot H[TRI_AHEAD];
-#pragma unroll
-                for (uint32_t k = 0; k < TRI_AHEAD; k++)
-                    if (k0 + k < count) {
-                        const float *src = sc.tri_hot[start + k0 + k].v0;
-                        const float3 a = *reinterpret_cast<const float3 *>(src);
-                        const float3 b = *reinterpret_cast<const float3 *>(src + 4);
-                        const float3 c = *reinterpret_cast<const float3 *>(src + 8);
-                        H[k].v0[0] = a.x; H[k].v0[1] = a.y; H[k].v0[2] = a.z;
-                        H[k].e1[0] = b.x; H[k].e1[1] = b.y; H[k].e1[2] = b.z;
-                        H[k].e2[0] = c.x; H[k].e2[1] = c.y; H[k].e2[2] = c.z;
-                    }
-#pragma unroll
-                for (uint32_t k = 0; k < TRI_AHEAD; k++) {
-                    if (k0 + k >= count) break;
-                    float t = 0.0f, u = 0.0f, v = 0.0f;
-                    if (COUNT) cnt.tri++;
-                    if (tri_test(H[k], T.lr, TMIN, T.tmax, t, u, v)) {
-                        T.found = true; T.tmax = t;
-                        T.hit.t = t; T.hit.inst = T.cur_inst; T.hit.ptype = type; T.hit.slot = start + k0 + k;
-                        T.hit.u = u; T.hit.v = v;
-                    }
-                }
-            }
-        } else {
-            for (uint32_t k = 0; k < count; k++) {
-                const uint32_t slot = start + k;
-                float t = 0.0f, u = 0.0f, v = 0.0f;
-                bool h;
-                if (type == RT_PRIM_SPHERE) {
-                    if (COUNT) cnt.sq++;
-                    h = sphere_test(sc.sph_hot[slot], T.lr, TMIN, T.tmax, t);
-                } else {
-                    if (COUNT) { cnt.sq++; cnt.quad++; }
-                    h = quad_test(sc.quad_hot[slot], T.lr, TMIN, T.tmax, t, u, v);
-                }
-                if (h) {
-                    T.found = true; T.tmax = t;
-                    T.hit.t = t; T.hit.inst = T.cur_inst; T.hit.ptype = type; T.hit.slot = slot; T.hit.u = u; T.hit.v = v;
-                }
-            }
-        }
-        if (!ref_is_marker(T.cur) && !(T.curT < T.tmax)) T.cur = REF_POP;   // re-test the successor
-    }
-    if (T.cur == REF_POP && T.stk.empty()) T.cur = REF_NONE;
-    if (T.cur == REF_NONE) T.tracing = false;
-}
-
-template <bool COUNT>
-__device__ __forceinline__ void lw_round(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt, PhaseCycles &pc,
-                                         uint32_t &steps, bool track) {
-    DIAG_T(t0);
-    for (;;) {
-        if (T.tracing && T.pleaf == REF_NONE && T.cur == REF_NONE) T.tracing = false;   // done, no leaf left
-        if (!__any(T.tracing && T.pleaf == REF_NONE)) break;
-        if (lean_active(T)) {
-            lw_step<COUNT>(T, sc, spill, cnt);
-            if (track) steps++;
-        }
-        if (RT_DIAG) pc.iters++;
-    }
-    DIAG_ADD(pc.interior, t0);
-    DIAG_T(t1);
-    if (T.tracing) {
-        lw_leaf_phase<COUNT>(T, sc, spill, cnt);
-        if (track) steps++;
-    }
-    DIAG_ADD(pc.leaf, t1);
-}
-#endif
 
 template <bool COUNT>
 __device__ __forceinline__ bool trace(const SceneGPU &sc, const f3 &o, const f3 &d, Hit &hit, Trav &T, SEnt *spill,
@@ -1526,8 +1108,8 @@ __device__ __forceinline__ bool map_item(const OutputGPU &out, const CameraGPU &
 }
 
 // Camera ray of sample `sample` of pixel (px, py) (Kernel.cu:119-135), consuming the pixel's RNG.
-// Evaluated without FMA contraction in both kernels, so the primary packet kernel and the persistent
-// kernel regenerate bit-identical camera rays (option "primary").
+// Evaluated without FMA contraction in both builds, so FAST and EXACT start every path from the same
+// camera ray.
 __device__ __forceinline__ void camera_ray(const CameraGPU &cam, uint32_t px, uint32_t py, uint32_t sample, Rng &rng,
                                            f3 &o, f3 &d) {
 #pragma clang fp contract(off)
@@ -1563,17 +1145,12 @@ __device__ __forceinline__ void write_pixel(const OutputGPU &out, uint32_t oi, f
 // the unit it claimed, so a unit's total work is the time it holds a wave; units over the particle
 // cluster hold one for up to ~0.4 ms against ~20 us for a sky unit (C2, measured), and the launch
 // ends with whichever wave claimed the last heavy units.
-// RT_UNIT_COST_DEFER (default): a lane keeps one pending (unit, cost) sum and flushes it with a
-// no-return atomic just before the wave's next claim atomic, whose returned value the wave waits for
-// anyway, so the flush adds no wait of its own (vector memory counters retire in order: a returning
-// atomic's wait also covers the stores and atomics issued before it).  A lane that finishes a pixel of
-// another unit before that flushes its old sum at once.  Measured: per-shade-step atomics (below,
-// RT_UNIT_COST_DEFER=0) made each next node load wait for their memory-side completion (~11 % of C2
-// throughput, profiles/r02_ab_unit_cost.jsonl).
-#ifndef RT_UNIT_COST_DEFER
-#define RT_UNIT_COST_DEFER 1
-#endif
-// Lanes that finished a pixel in this shade step: one atomicAdd per distinct unit.
+// A lane keeps one pending (unit, cost) sum and flushes it with a no-return atomic just before the
+// wave's next claim atomic, whose returned value the wave waits for anyway, so the flush adds no wait of
+// its own (vector memory counters retire in order: a returning atomic's wait also covers the stores and
+// atomics issued before it).  A lane that finishes a pixel of another unit before that flushes its old
+// sum at once.  Measured: per-shade-step atomics made each next node load wait for their memory-side
+// completion (~11 % of C2 throughput, profiles/r02_ab_unit_cost.jsonl).
 __device__ __forceinline__ uint32_t wave_max(uint32_t v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off, 64));
@@ -1585,10 +1162,8 @@ __device__ __forceinline__ void unit_cost_flush(uint32_t *cost, uint32_t unit, u
     if (use_max) atomicMax(cost + unit, c);
     else atomicAdd(cost + unit, c);
 }
+// the pending sums of the lanes in `fin`: one atomic per distinct unit
 __device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t unit, uint32_t c, bool use_max) {
-#ifdef RT_AB_NO_UNIT_COST
-    return;
-#endif
     uint64_t m = __ballot(fin);
     while (m) {
         const uint32_t first = (uint32_t)__builtin_ctzll(m);
@@ -1600,47 +1175,11 @@ __device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t
     }
 }
 
-#ifndef RT_ARGS_LDS
-#define RT_ARGS_LDS 0                   // kernel arguments read from LDS copies (fewer live SGPRs, fewer spills):
-                                        // 1 = the camera, 2 = + the output block, 3 = + the scene block
-#endif
-template <typename A>
-__device__ __forceinline__ void args_to_lds(A &dst, const A &src) {
-    static_assert(sizeof(A) % 4 == 0 && sizeof(A) / 4 <= BLOCK, "argument block copied one dword per thread");
-    if (threadIdx.x < sizeof(A) / 4)
-        reinterpret_cast<uint32_t *>(&dst)[threadIdx.x] = reinterpret_cast<const uint32_t *>(&src)[threadIdx.x];
-}
-template <bool COUNT, bool LEAN, bool WIDE>
-__device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, const CameraGPU &cam_arg,
-                                                       const OutputGPU &out_arg, uint32_t *queue, uint32_t threshold,
-                                                       unsigned long long *counters) {
-#if RT_ARGS_LDS >= 1
-    __shared__ CameraGPU lds_cam;
-    args_to_lds(lds_cam, cam_arg);
-    const CameraGPU &cam = lds_cam;
-#else
-    const CameraGPU &cam = cam_arg;
-#endif
-#if RT_ARGS_LDS >= 2
-    __shared__ OutputGPU lds_out;
-    args_to_lds(lds_out, out_arg);
-    const OutputGPU &out = lds_out;
-#else
-    const OutputGPU &out = out_arg;
-#endif
-#if RT_ARGS_LDS >= 3
-    __shared__ SceneGPU lds_sc;
-    args_to_lds(lds_sc, sc_arg);
-    const SceneGPU &sc = lds_sc;
-#else
-    const SceneGPU &sc = sc_arg;
-#endif
-#if RT_ARGS_LDS >= 1
-    __syncthreads();                              // the argument copies, before the scene fill reads them
-#endif
-    __shared__ unsigned long long lds_stack[LEAN ? LEAN_DEPTH : LDS_DEPTH][BLOCK];
+template <bool COUNT, bool WIDE>
+__device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out,
+                                                       uint32_t *queue, uint32_t threshold, unsigned long long *counters) {
+    __shared__ unsigned long long lds_stack[LDS_DEPTH][BLOCK];
     __shared__ float4 lds_mat[LDS_MATERIALS];     // the scene's materials (shading reads them per hit)
-    __shared__ uint32_t lds_path[RT_PATH_LDS ? PATH_WORDS : 1][BLOCK];
     const int tid = threadIdx.x;
     const int lane = tid & 63;
     const bool mat_lds = sc.material_count <= LDS_MATERIALS;
@@ -1660,36 +1199,12 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, c
     uint32_t rays = 0, pixels = 0;
 
     bool has = false;                  // lane owns a pixel
-    bool heavy = false;                // RT_HEAVY_PRIO: the lane's pixel came from a split (heavy) item
-    bool pool_heavy = false;           // wave-uniform: the current pool is a split item
-    bool prio_up = false;              // wave-uniform: priority currently raised
     uint32_t px_steps = 0;             // traversal steps spent on the lane's pixel (COUNT cost map, reorder)
     uint32_t item = 0, sample = 0, depth = 0;
     Rng rng;
     rng.s = 0;
     f3 acc = mk(0.0f, 0.0f, 0.0f), thr = mk(1.0f, 1.0f, 1.0f);
-    // RT_PATH_LDS: the path state lives in LDS between shade steps, so it holds no VGPRs during traversal
-    const auto save_path = [&]() {
-        if (RT_PATH_LDS) {
-            lds_path[0][tid] = __float_as_uint(acc.x); lds_path[1][tid] = __float_as_uint(acc.y);
-            lds_path[2][tid] = __float_as_uint(acc.z); lds_path[3][tid] = __float_as_uint(thr.x);
-            lds_path[4][tid] = __float_as_uint(thr.y); lds_path[5][tid] = __float_as_uint(thr.z);
-            lds_path[6][tid] = (uint32_t)rng.s; lds_path[7][tid] = (uint32_t)(rng.s >> 32);
-            lds_path[8][tid] = item; lds_path[9][tid] = sample << 16 | depth;
-        }
-    };
-    const auto load_path = [&]() {
-        if (RT_PATH_LDS) {
-            acc = mk(__uint_as_float(lds_path[0][tid]), __uint_as_float(lds_path[1][tid]), __uint_as_float(lds_path[2][tid]));
-            thr = mk(__uint_as_float(lds_path[3][tid]), __uint_as_float(lds_path[4][tid]), __uint_as_float(lds_path[5][tid]));
-            rng.s = (uint64_t)lds_path[6][tid] | ((uint64_t)lds_path[7][tid] << 32);
-            item = lds_path[8][tid];
-            const uint32_t sd = lds_path[9][tid];
-            sample = sd >> 16; depth = sd & 0xFFFFu;
-        }
-    };
     uint32_t pool_next = 0, pool_end = 0;     // wave-uniform
-    uint32_t pool2_next = 0, pool2_end = 0;   // wave-uniform: the second item of a two-item claim
     uint32_t limit = 0, limit_part = ~0u;     // wave-uniform: claim positions in band `limit_part`
     bool exhausted = false;                   // wave-uniform
     const uint32_t S2 = cam.sqrt_s * cam.sqrt_s;
@@ -1700,7 +1215,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, c
     uint32_t part = xcc % parts, tried = 0;
     const uint32_t grab = out.grab;                 // claim size (pixels)
     const bool track = out.unit_cost != nullptr;    // record unit costs for the next launch's order
-    uint32_t pend_unit = 0, pend_cost = 0;          // RT_UNIT_COST_DEFER: the lane's unflushed unit cost
+    uint32_t pend_unit = 0, pend_cost = 0;          // the lane's unflushed unit cost (flushed before a claim)
     unsigned long long t_start = 0, t_exhaust = 0;
     uint32_t n_rounds = 0, n_shades = 0, n_grabs = 0;      // wave-uniform (timeline)
     PhaseCycles pc = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1710,16 +1225,10 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, c
         // ---- refill idle lanes from the wave's pool / the global queue
         DIAG_T(t_refill);
         uint64_t need = __ballot(!has);
-        bool first_claim = true;            // wave-uniform ("mix"): this refill has not claimed yet
         while (need && !exhausted) {
             if (RT_DIAG) pc.refill_iters++;
             const uint32_t n_need = __popcll(need);
-            if (pool_next >= pool_end && pool2_next < pool2_end) {      // the claim's second item
-                pool_next = pool2_next;
-                pool_end = pool2_end;
-                pool2_next = pool2_end;
-                pool_heavy = false;
-            } else if (pool_next >= pool_end) {
+            if (pool_next >= pool_end) {
                 // bands: whole unit rows in frame mode (so a band can be walked in supertiles)
                 const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
                 const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
@@ -1727,31 +1236,19 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, c
                 const uint32_t p_end = (rows * (part + 1) / parts) * upr * 64u;
                 // ordered walk (schedule.hip): one item per claim, a whole unit or a 1/2, 1/4 of a heavy
                 // one; the band's item count sits next to its head.  Screen walk: `grab` pixels per claim.
-                const uint32_t step = out.order ? (out.claim_items > 1u ? 2u : 1u) : grab;
+                const uint32_t step = out.order ? 1u : grab;
                 if (part != limit_part) {          // the band's item count: read once per band, off the head's line
                     limit_part = part;
                     limit = out.order ? __builtin_amdgcn_readfirstlane(queue[(QUEUE_MAX_PARTS + part) * QUEUE_STRIDE])
                                       : p_end - p_begin;
                 }
-                if (RT_UNIT_COST_DEFER && track) {   // completes under the claim's wait
+                if (track) {                         // completes under the claim's wait
                     unit_cost_add(out.unit_cost, pend_cost != 0, pend_unit, pend_cost, out.cost_max != 0);
                     pend_cost = 0;
                 }
                 uint32_t b = 0;
-                if (out.order && out.mix) {
-                    // {front, back} in one 64-bit head: a front claim takes item f, a back claim item
-                    // limit - 1 - k; both are free exactly while f + k < limit at the atomic
-                    const bool back = !first_claim;
-                    unsigned long long old = 0;
-                    if (lane == 0) old = atomicAdd(reinterpret_cast<unsigned long long *>(queue + part * QUEUE_STRIDE),
-                                                   back ? (1ull << 32) : 1ull);
-                    const uint32_t f = __builtin_amdgcn_readfirstlane(__shfl((uint32_t)old, 0, 64));
-                    const uint32_t k = __builtin_amdgcn_readfirstlane(__shfl((uint32_t)(old >> 32), 0, 64));
-                    b = f + k >= limit ? limit : (back ? limit - 1u - k : f);
-                } else {
-                    if (lane == 0) b = atomicAdd(queue + part * QUEUE_STRIDE, step);
-                    b = __builtin_amdgcn_readfirstlane(__shfl(b, 0, 64));
-                }
+                if (lane == 0) b = atomicAdd(queue + part * QUEUE_STRIDE, step);
+                b = __builtin_amdgcn_readfirstlane(__shfl(b, 0, 64));
                 n_grabs++;
                 if (b >= limit) {
                     // the band is dry: try the next one.  `tried` counts failures over the wave's life, so a
@@ -1766,27 +1263,15 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, c
                     part = part + 1 == parts ? 0 : part + 1;
                     continue;
                 }
-                first_claim = false;
                 if (out.order) {
-                    // claim_items 2: two consecutive order items per atomic, both entries read in one
-                    // round trip (the claim atomic + its dependent order read are ~2 us under load)
-                    const uint32_t *ob = out.order + 4u * (p_begin >> 6) + b;
-                    const uint32_t it = ob[0];
-                    const uint32_t it2 = step > 1u && !out.mix && b + 1u < limit ? ob[1] : ~0u;
+                    const uint32_t it = out.order[4u * (p_begin >> 6) + b];
                     // log2 pieces 3: two adjacent light units (schedule option "merge"), 128 pixels
                     const uint32_t ls = it & 3u, len = ls == 3u ? 128u : 64u >> ls;
                     pool_next = (it >> 4) * 64u + (ls == 3u ? 0u : ((it >> 2) & 3u) * len);
-                    pool_heavy = ls == 1u || ls == 2u;
                     pool_end = pool_next + len;
-                    if (it2 != ~0u) {
-                        const uint32_t ls2 = it2 & 3u, len2 = ls2 == 3u ? 128u : 64u >> ls2;
-                        pool2_next = (it2 >> 4) * 64u + (ls2 == 3u ? 0u : ((it2 >> 2) & 3u) * len2);
-                        pool2_end = pool2_next + len2;
-                    }
                 } else {
                     b += p_begin;
                     pool_next = b;
-                    pool_heavy = false;
                     pool_end = min(b + grab, p_end);
                 }
                 if (!out.order && out.supertile && out.tile_count == 0 && grab == 64u) {
@@ -1814,7 +1299,6 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, c
                 item = pool_next + rank;
                 if (map_item(out, cam, item, px, py, oi)) {
                     has = true;
-                    heavy = pool_heavy;
                     const uint32_t pixel = cam.pitch * py + px;                    // Kernel.cu:109
                     rng.init((uint64_t)pixel ^ cam.frame_seed, pixel);              // Kernel.cu:114
                     acc = mk(0.0f, 0.0f, 0.0f);
@@ -1823,21 +1307,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, c
                     px_steps = 0;
                     f3 o, d;
                     camera_ray(cam, px, py, 0, rng, o, d);
-#if !RT_EXACT
-                    const uint4 rec = out.prim_rec ? reinterpret_cast<const uint4 *>(out.prim_rec)[item]
-                                                   : make_uint4(0u, PREC_TRACE, 0u, 0u);
-                    if (rec.y != PREC_TRACE) {          // option "primary": the packet kernel's closest hit
-                        T.wr.o = o; T.wr.d = d;
-                        T.tracing = false;
-                        T.found = rec.y != PREC_MISS;
-                        T.tmax = __uint_as_float(rec.x);
-                        T.hit.t = T.tmax; T.hit.inst = rec.y; T.hit.ptype = rec.z >> 28; T.hit.slot = rec.z & 0x0FFFFFFFu;
-                        T.hit.u = __uint_as_float(rec.w); T.hit.v = out.prim_v[item];
-                        T.stk.sp = 0; T.stk.spilled = 0; T.pleaf = REF_NONE; T.cur = REF_NONE; T.in_blas = false;
-                    } else
-#endif
                     trav_init(T, root, o, d);
-                    save_path();
                     pixels++;
                 }
             }
@@ -1850,31 +1320,13 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, c
             if (exhausted) break;
             continue;
         }
-        if (RT_HEAVY_PRIO && out.order) {    // raised issue priority while the wave holds a heavy pixel
-            const bool want = __any(has && heavy);
-            if (want != prio_up) {
-                if (want) __builtin_amdgcn_s_setprio(2);
-                else __builtin_amdgcn_s_setprio(0);
-                prio_up = want;
-            }
-        }
         // ---- traverse while enough lanes are busy
-        // option "drain": with the queue dry no idle lane can be refilled, and fewer paths than `threshold`
-        // may be left: a lane whose segment ended shades once 1/drain of the remaining paths wait
-        const uint32_t shade_at = exhausted && out.drain
-                                 ? max(1u, min(threshold, (uint32_t)__popcll(__ballot(has)) / out.drain))
-                                 : threshold;
         for (;;) {
             const uint64_t tr = __ballot(T.tracing);
             if (tr == 0) break;
             const uint64_t want = __ballot(!T.tracing && (has || !exhausted));
-            if ((uint32_t)__popcll(want) >= shade_at) break;
-#if !RT_EXACT
-            if constexpr (LEAN) lean_round<COUNT>(T, sc, cnt, pc, px_steps, COUNT || track);
-            else if constexpr (WIDE && RT_LEAN_WIDE) lw_round<COUNT>(T, sc, spill, cnt, pc, px_steps, COUNT || track);
-            else
-#endif
-                spec_round<COUNT, WIDE>(T, sc, spill, cnt, pc, px_steps, COUNT || track);
+            if ((uint32_t)__popcll(want) >= threshold) break;
+            spec_round<COUNT, WIDE>(T, sc, spill, cnt, pc, px_steps, COUNT || track);
             n_rounds++;
         }
         // ---- shade lanes whose segment finished (rayColor body, Kernel.cu:64-100)
@@ -1882,7 +1334,6 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, c
         DIAG_T(t_shade);
         bool fin = false;                    // lane wrote its pixel in this step
         if (has && !T.tracing) {
-            load_path();
             rays++;
             bool path_done;
             f3 no = T.wr.o, nd = T.wr.d;                                     // next segment
@@ -1935,29 +1386,21 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, c
                     fin = true;
                 }
             }
-            if (has) {
-                trav_init(T, root, no, nd);
-                save_path();
-            }
+            if (has) trav_init(T, root, no, nd);
         }
-        if (RT_UNIT_COST_DEFER) {
-            if (track && fin) {
-                const uint32_t u = item >> 6;
-                if (u != pend_unit) {
-                    if (pend_cost) unit_cost_flush(out.unit_cost, pend_unit, pend_cost, out.cost_max != 0);
-                    pend_unit = u;
-                    pend_cost = 0;
-                }
-                pend_cost = out.cost_max ? max(pend_cost, (px_steps + 1u) * 64u) : pend_cost + px_steps + 1u;
+        if (track && fin) {
+            const uint32_t u = item >> 6;
+            if (u != pend_unit) {
+                if (pend_cost) unit_cost_flush(out.unit_cost, pend_unit, pend_cost, out.cost_max != 0);
+                pend_unit = u;
+                pend_cost = 0;
             }
-        } else if (track) {
-            unit_cost_add(out.unit_cost, fin, item >> 6, out.cost_max ? (px_steps + 1u) * 64u : px_steps + 1u,
-                          out.cost_max != 0);
+            pend_cost = out.cost_max ? max(pend_cost, (px_steps + 1u) * 64u) : pend_cost + px_steps + 1u;
         }
         DIAG_ADD(pc.shade, t_shade);
     }
 
-    if (RT_UNIT_COST_DEFER && track && pend_cost) unit_cost_flush(out.unit_cost, pend_unit, pend_cost, out.cost_max != 0);
+    if (track && pend_cost) unit_cost_flush(out.unit_cost, pend_unit, pend_cost, out.cost_max != 0);
     const uint32_t wr = wave_sum(rays);
     const uint32_t wp = wave_sum(pixels);
     if (COUNT) {
@@ -1999,11 +1442,11 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc_arg, c
 }
 
 // Register budget variants: WPE = minimum waves per SIMD the compiler must allow (0 = its choice).
-template <bool COUNT, int WPE, bool LEAN, bool WIDE = false>
+template <bool COUNT, int WPE, bool WIDE = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
 void render_persistent_kernel(SceneGPU sc, CameraGPU cam, OutputGPU out, uint32_t *queue, uint32_t threshold,
                               unsigned long long *counters) {
-    render_persistent_body<COUNT, LEAN, WIDE>(sc, cam, out, queue, threshold, counters);
+    render_persistent_body<COUNT, WIDE>(sc, cam, out, queue, threshold, counters);
 }
 
 __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const float *rays, uint32_t n, rt_hit *hits) {
@@ -2035,212 +1478,6 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const fl
     hits[i] = r;
 }
 
-#if !RT_EXACT
-// ---- primary packets (option "primary", FAST kernel on quad trees) ----------------------------
-// The first camera ray of every pixel is the same for every frame's path and the 64 of one 8x8 unit
-// are coherent (measured, C2: depth-1 launches alone took 0.233 of the 0.358 ms frame,
-// scripts/depth_probe.py), so they are traced before the persistent launch by one wave per unit that
-// walks the union of its rays' paths together: the node, instance and primitive records are
-// wave-uniform loads, the stack holds one node ref per entry (LDS) plus each lane's entry t (lanes
-// whose entry t >= their tmax sit the node out), the walk order is by the first hitting lane's entry t
-// (FAST tolerance: only ties within the 1e-6 window can resolve differently).  Every slab and
-// primitive test is the per-lane traversal's own function, so each ray's closest hit is the one the
-// persistent kernel would find.  Only sample 0 is traced here: later samples' camera jitter depends
-// on how many RNG draws the earlier paths took.  The persistent kernel shades the record (regenerating
-// the same camera ray, camera_ray is evaluated without contraction), or traces the pixel itself when
-// the wave's stack filled up (PREC_TRACE).  Measured (C2, rocprofv3): 0.22 ms for the 2.07 M primary
-// rays — each node visit is one dependent scalar-load round trip for the whole wave (~35 per packet),
-// against ~0.08 ms of primary traversal inside the persistent kernel — so the option is off by default.
-constexpr int PSTACK = 32;
-
-__device__ __forceinline__ uint32_t uni(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
-
-// sort 4 children by a wave-uniform key; the per-lane entry t / hit flags move with them
-__device__ __forceinline__ void cswap_pk(float &ka, uint32_t &ra, float &ta, bool &ha, float &kb, uint32_t &rb, float &tb,
-                                         bool &hb) {
-    if (kb < ka) {                       // uniform condition
-        float k = ka; ka = kb; kb = k;
-        uint32_t r = ra; ra = rb; rb = r;
-        float t = ta; ta = tb; tb = t;
-        bool h = ha; ha = hb; hb = h;
-    }
-}
-
-template <bool COUNT>
-__global__ __launch_bounds__(64) void primary_packet_kernel(SceneGPU sc, CameraGPU cam, OutputGPU out,
-                                                            unsigned long long *counters) {
-    __shared__ float tstk[PSTACK][64];       // per-lane entry t of each pushed node
-    __shared__ uint32_t rstk[PSTACK];        // the pushed node refs (wave-uniform)
-    const uint32_t lane = threadIdx.x;
-    const uint32_t item = blockIdx.x * 64u + lane;
-    uint32_t px, py, oi;
-    const bool alive = map_item(out, cam, item, px, py, oi);
-    LaneCount cnt = {0, 0, 0, 0, 0, 0, 0};
-    f3 o = mk(0.0f, 0.0f, 0.0f), d = mk(0.0f, 0.0f, 1.0f);
-    if (alive) {
-        const uint32_t pixel = cam.pitch * py + px;
-        Rng rng;
-        rng.init((uint64_t)pixel ^ cam.frame_seed, pixel);                      // Kernel.cu:114
-        camera_ray(cam, px, py, 0, rng, o, d);
-    }
-    RayP wr;
-    wr.o = o; wr.d = d;
-    prep(wr);
-    RayP lr = wr;
-    float tmax = __builtin_huge_valf();
-    uint32_t h_inst = PREC_MISS, h_pslot = 0;
-    float h_u = 0.0f, h_v = 0.0f;
-    const TreeRoot root = uniform_root<true>(sc);
-    float te = __builtin_huge_valf();
-    if (alive) {
-        float t0 = 0.0f;
-        if (slab(root.box, wr, TMIN, tmax, t0)) te = t0;
-    }
-    uint32_t cur = root.ref;              // wave-uniform walk state
-    uint32_t cur_inst = 0;
-    int sp = 0;
-    bool in_blas = false, overflow = false;
-    bool have = __ballot(te < tmax) != 0;
-    while (have) {
-        const bool act = te < tmax;
-        bool pop = true;
-        if (!(cur & REF_LEAF)) {
-            // interior quad: 4 slab tests per lane against the uniform node
-            const NodeQuad *base = (cur & REF_BLAS) ? sc.blas_quads : sc.tlas_quads;
-            const float4 *Q = reinterpret_cast<const float4 *>(base + (cur & REF_INDEX_MASK));
-            const float4 lx = Q[0], hx = Q[1], ly = Q[2], hy = Q[3], lz = Q[4], hz = Q[5];
-            const uint4 R = reinterpret_cast<const uint4 *>(Q)[6];
-            const RayP &r = in_blas ? lr : wr;
-            float t[4];
-            bool h[4];
-            if (!r.tiny) {
-                float4 tn = make_float4(TMIN, TMIN, TMIN, TMIN), tf = make_float4(tmax, tmax, tmax, tmax);
-                slab4(lx, hx, r.inv.x, r.oinv.x, tn, tf);
-                slab4(ly, hy, r.inv.y, r.oinv.y, tn, tf);
-                slab4(lz, hz, r.inv.z, r.oinv.z, tn, tf);
-                t[0] = tn.x; t[1] = tn.y; t[2] = tn.z; t[3] = tn.w;
-                h[0] = tn.x < tf.x; h[1] = tn.y < tf.y; h[2] = tn.z < tf.z; h[3] = tn.w < tf.w;
-            } else {
-                const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
-                const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
-                const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
-#pragma unroll
-                for (int k = 0; k < 4; k++) {
-                    const float b[6] = {LX[k], HX[k], LY[k], HY[k], LZ[k], HZ[k]};
-                    t[k] = 0.0f;
-                    h[k] = slab_ref(b, r.o, r.d, TMIN, tmax, t[k]);
-                }
-            }
-            if (COUNT && act) cnt.pairs += 2;
-            float key[4];
-            uint32_t ref[4] = {R.x, R.y, R.z, R.w};
-            uint32_t nh = 0;
-#pragma unroll
-            for (int k = 0; k < 4; k++) {
-                h[k] = h[k] && act;
-                const uint64_t m = __ballot(h[k]);
-                key[k] = m ? __int_as_float(__builtin_amdgcn_readlane(__float_as_int(t[k]), (int)__builtin_ctzll(m)))
-                           : __builtin_huge_valf();
-                nh += m ? 1u : 0u;
-                if (!h[k]) t[k] = __builtin_huge_valf();
-            }
-            if (nh) {
-                cswap_pk(key[0], ref[0], t[0], h[0], key[1], ref[1], t[1], h[1]);
-                cswap_pk(key[2], ref[2], t[2], h[2], key[3], ref[3], t[3], h[3]);
-                cswap_pk(key[0], ref[0], t[0], h[0], key[2], ref[2], t[2], h[2]);
-                cswap_pk(key[1], ref[1], t[1], h[1], key[3], ref[3], t[3], h[3]);
-                cswap_pk(key[1], ref[1], t[1], h[1], key[2], ref[2], t[2], h[2]);
-                if (sp + (int)nh - 1 > PSTACK) { overflow = true; break; }
-#pragma unroll
-                for (int k = 3; k >= 1; k--)                  // farthest first: popped nearest first
-                    if ((uint32_t)k < nh) {
-                        tstk[sp][lane] = t[k];
-                        rstk[sp] = ref[k];
-                        sp++;
-                    }
-                cur = uni(ref[0]);
-                te = t[0];
-                pop = false;
-            }
-        } else if (!(cur & REF_BLAS)) {
-            // TLAS leaf: its remaining instances wait on the stack with the leaf's entry t; enter the first
-            const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur);
-            if (count > 1) {
-                if (sp == PSTACK) { overflow = true; break; }
-                tstk[sp][lane] = te;
-                rstk[sp] = make_leaf_ref(start + 1, count - 1, 0, false);
-                sp++;
-            }
-            cur_inst = uni(sc.inst_by_slot ? start : sc.tlas_slots[start]);
-            const InstHot &I = sc.inst_hot[cur_inst];
-            if (COUNT && act) cnt.inst++;
-            lr.o = xf_point(I.inv, wr.o);                                  // Instance.cu:26-27
-            lr.d = xf_vector(I.inv, wr.d);
-            prep(lr);
-            float t0 = 0.0f;
-            const bool hb = act && slab(I.root_box, lr, TMIN, tmax, t0);
-            if (__ballot(hb)) {
-                in_blas = true;
-                cur = uni(I.root_ref_wide);
-                te = hb ? t0 : __builtin_huge_valf();
-                pop = false;
-            }
-        } else {
-            // BLAS leaf: its primitives in leaf order against each active lane's instance ray
-            const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur), type = ref_leaf_type(cur);
-            for (uint32_t k = 0; k < count; k++) {
-                const uint32_t slot = start + k;
-                float t = 0.0f, u = 0.0f, v = 0.0f;
-                bool hh = false;
-                if (type == RT_PRIM_TRIANGLE) {
-                    if (COUNT && act) cnt.tri++;
-                    if (act) hh = tri_test(sc.tri_hot[slot], lr, TMIN, tmax, t, u, v);
-                } else if (type == RT_PRIM_SPHERE) {
-                    if (COUNT && act) cnt.sq++;
-                    if (act) hh = sphere_test(sc.sph_hot[slot], lr, TMIN, tmax, t);
-                } else {
-                    if (COUNT && act) { cnt.sq++; cnt.quad++; }
-                    if (act) hh = quad_test(sc.quad_hot[slot], lr, TMIN, tmax, t, u, v);
-                }
-                if (hh) {
-                    tmax = t; h_inst = cur_inst; h_pslot = (type << 28) | slot; h_u = u; h_v = v;
-                }
-            }
-        }
-        if (pop) {
-            have = false;
-            while (sp > 0) {
-                sp--;
-                const float t = tstk[sp][lane];
-                if (__ballot(t < tmax)) {
-                    cur = uni(rstk[sp]);
-                    te = t;
-                    if (!(cur & REF_BLAS)) in_blas = false;      // back in the TLAS: world rays
-                    have = true;
-                    break;
-                }
-            }
-        }
-    }
-    if (item < out.units * 64u) {
-        const uint32_t inst = overflow ? PREC_TRACE : h_inst;
-        reinterpret_cast<uint4 *>(out.prim_rec)[item] = make_uint4(__float_as_uint(tmax), inst, h_pslot, __float_as_uint(h_u));
-        out.prim_v[item] = h_v;
-    }
-    if (COUNT) {
-        const uint32_t a = wave_sum(cnt.pairs), b = wave_sum(cnt.tri), c = wave_sum(cnt.sq), e = wave_sum(cnt.inst),
-                       f = wave_sum(cnt.quad);
-        if (lane == 0) {
-            atomicAdd(&counters[CNT_PAIRS], (unsigned long long)a);
-            atomicAdd(&counters[CNT_TRI], (unsigned long long)b);
-            atomicAdd(&counters[CNT_SPHQUAD], (unsigned long long)c);
-            atomicAdd(&counters[CNT_INST], (unsigned long long)e);
-            atomicAdd(&counters[CNT_QUAD], (unsigned long long)f);
-        }
-    }
-}
-#endif
-
 }  // namespace dev
 
 hipError_t RT_SUFFIX(launch_render)(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
@@ -2255,7 +1492,7 @@ hipError_t RT_SUFFIX(launch_render)(const SceneGPU &sc, const CameraGPU &cam, co
 }
 
 namespace {
-template <int WPE, bool LEAN, bool WIDE = false>
+template <int WPE, bool WIDE = false>
 hipError_t launch_persistent_wpe(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
                                  unsigned long long *counters, uint32_t *queue, uint32_t blocks_per_cu_cus,
                                  uint32_t threshold, hipStream_t stream) {
@@ -2263,62 +1500,46 @@ hipError_t launch_persistent_wpe(const SceneGPU &sc, const CameraGPU &cam, const
     const uint32_t need = (out.units + (BLOCK / 64) - 1) / (BLOCK / 64);
     const dim3 grid(blocks_per_cu_cus < need ? blocks_per_cu_cus : need);
     if (count)
-        hipLaunchKernelGGL((render_persistent_kernel<true, WPE, LEAN, WIDE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
+        hipLaunchKernelGGL((render_persistent_kernel<true, WPE, WIDE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
     else
-        hipLaunchKernelGGL((render_persistent_kernel<false, WPE, LEAN, WIDE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
+        hipLaunchKernelGGL((render_persistent_kernel<false, WPE, WIDE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
     return hipGetLastError();
 }
-template <int WPE, bool LEAN, bool WIDE = false>
+template <int WPE, bool WIDE = false>
 uint32_t blocks_per_cu_wpe() {
     using namespace RT_SUFFIX(dev);
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false, WPE, LEAN, WIDE>, BLOCK, 0) != hipSuccess) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false, WPE, WIDE>, BLOCK, 0) != hipSuccess) return 1;
     return n > 0 ? (uint32_t)n : 1u;
 }
 #if RT_EXACT
-constexpr bool HAS_LEAN = false;
 constexpr bool HAS_WIDE = false;      // EXACT keeps the reference's binary trees and visit order
 #else
-constexpr bool HAS_LEAN = true;
 constexpr bool HAS_WIDE = true;
 #endif
 }  // namespace
 
-// variant: 0 = compiler's register budget (quad trees: at least 3 waves per SIMD), 4 / 5 = at least 4 / 5 waves per SIMD.
-// lean: LDS-only-stack traversal (FAST kernel; the caller checks the tree heights).
+// variant: 0 = compiler's register budget (quad trees: at least 3 waves per SIMD), 4 = at least 4 waves per SIMD.
 hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
                                                unsigned long long *counters, uint32_t *queue, uint32_t blocks,
-                                               uint32_t threshold, uint32_t variant, bool lean, bool reset_queue,
-                                               hipStream_t stream) {
+                                               uint32_t threshold, uint32_t variant, bool reset_queue, hipStream_t stream) {
     if (out.units == 0) return hipSuccess;
     if (reset_queue) {       // else the schedule kernel (schedule.hip) just reset the heads
         const hipError_t e = hipMemsetAsync(queue, 0, QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
     }
-    if (lean && HAS_LEAN) {
-        if (variant == 4) return launch_persistent_wpe<4, HAS_LEAN>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-        if (variant == 5) return launch_persistent_wpe<5, HAS_LEAN>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-        return launch_persistent_wpe<3, HAS_LEAN>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-    }
     if (sc.wide && HAS_WIDE) {
-        if (variant == 4) return launch_persistent_wpe<4, false, HAS_WIDE>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-        return launch_persistent_wpe<3, false, HAS_WIDE>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+        if (variant == 4) return launch_persistent_wpe<4, HAS_WIDE>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+        return launch_persistent_wpe<3, HAS_WIDE>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     }
-    if (variant == 4) return launch_persistent_wpe<4, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-    if (variant == 5) return launch_persistent_wpe<5, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-    return launch_persistent_wpe<0, false>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+    if (variant == 4) return launch_persistent_wpe<4>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+    return launch_persistent_wpe<0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
 }
 
-uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, bool lean, bool wide) {
-    if (lean && HAS_LEAN) {
-        if (variant == 4) return blocks_per_cu_wpe<4, HAS_LEAN>();
-        if (variant == 5) return blocks_per_cu_wpe<5, HAS_LEAN>();
-        return blocks_per_cu_wpe<3, HAS_LEAN>();
-    }
-    if (wide && HAS_WIDE) return variant == 4 ? blocks_per_cu_wpe<4, false, HAS_WIDE>() : blocks_per_cu_wpe<3, false, HAS_WIDE>();
-    if (variant == 4) return blocks_per_cu_wpe<4, false>();
-    if (variant == 5) return blocks_per_cu_wpe<5, false>();
-    return blocks_per_cu_wpe<0, false>();
+uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, bool wide) {
+    if (wide && HAS_WIDE) return variant == 4 ? blocks_per_cu_wpe<4, HAS_WIDE>() : blocks_per_cu_wpe<3, HAS_WIDE>();
+    if (variant == 4) return blocks_per_cu_wpe<4>();
+    return blocks_per_cu_wpe<0>();
 }
 
 hipError_t RT_SUFFIX(launch_trace_rays)(const SceneGPU &sc, const float *rays, uint32_t n, rt_hit *hits,
@@ -2328,18 +1549,5 @@ hipError_t RT_SUFFIX(launch_trace_rays)(const SceneGPU &sc, const float *rays, u
     hipLaunchKernelGGL(trace_rays_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, stream, sc, rays, n, hits);
     return hipGetLastError();
 }
-
-#if !RT_EXACT
-// One wave per 8x8 unit; out.prim_rec / prim_v hold out.units * 64 records.
-hipError_t launch_primary_fast(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
-                               unsigned long long *counters, hipStream_t stream) {
-    using namespace dev_fast;
-    if (out.units == 0) return hipSuccess;
-    if (!out.prim_rec || !out.prim_v || !sc.wide) return hipErrorInvalidValue;
-    if (count) hipLaunchKernelGGL(primary_packet_kernel<true>, dim3(out.units), dim3(64), 0, stream, sc, cam, out, counters);
-    else hipLaunchKernelGGL(primary_packet_kernel<false>, dim3(out.units), dim3(64), 0, stream, sc, cam, out, counters);
-    return hipGetLastError();
-}
-#endif
 
 }  // namespace rtamd

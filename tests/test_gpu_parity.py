@@ -406,13 +406,12 @@ def test_reorder_period_byte_identical(gpu_lib, period, lanes):
         assert np.array_equal(bufs[f].cpu().numpy().reshape(H, W, 4), ref[f]), f
 
 
-@pytest.mark.parametrize("opts", [{"mix": 1}, {"claim_items": 2}, {"mix": 1, "claim_items": 2}, {"grid_pct": 30},
-                                  {"merge": 8}, {"merge": 16}, {"merge": 8, "claim_items": 2},
-                                  {"drain": 1}, {"drain": 4}, {"drain": 64}, {"lds_blas": 0}])
+@pytest.mark.parametrize("opts", [{"grid_pct": 30}, {"merge": 8}, {"merge": 16}, {"merge": 0}, {"split": 0xFFFF},
+                                  {"split": 4 | 8 << 8}, {"cost_max": 1}, {"lds_blas": 0}])
 def test_claim_options_byte_identical(gpu_lib, opts):
-    """Claim-order options of the persistent kernel ("mix": heaviest item from a band's front, light fill
-    from its back; "claim_items" 2; a 30 % grid): which wave traces a pixel changes, the pixel's result
-    does not.  Frames on three overlapped lanes equal the screen-order walk byte for byte, across the
+    """Claim-order options of the persistent kernel (light units merged into 128-pixel items, heavy units
+    split in halves / quarters, costs as the longest path, a 30 % grid): which wave traces a pixel changes,
+    the pixel's result does not.  Frames on three overlapped lanes equal the screen-order walk byte for byte, across the
     launches that record costs and the ones that claim in the recorded order, and the work counters
     equal the serial frames'."""
     import torch
