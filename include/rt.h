@@ -170,8 +170,12 @@ typedef enum rt_render_flags {
     RT_RENDER_EXACT = 1u << 0,        /* bit-faithful arithmetic (IEEE division, no FMA) */
     RT_RENDER_COUNT_WORK = 1u << 1,   /* fill rt_stats work counters (slower)              */
     RT_RENDER_NO_SYNC = 1u << 2,      /* return after enqueue (device outputs only)        */
-    RT_RENDER_SKIP_UPDATE = 1u << 3,  /* do not run the instance update / TLAS rebuild     */
-    RT_RENDER_KEEP_COUNTERS = 1u << 4 /* accumulate device counters (see rt_scene_collect) */
+    RT_RENDER_SKIP_UPDATE = 1u << 3,  /* do not run the instance update / TLAS rebuild (with
+                                         "overlap": the frame waits for the whole launch that
+                                         uploaded its frame block, i.e. it serialises with it) */
+    RT_RENDER_KEEP_COUNTERS = 1u << 4 /* accumulate device counters (see rt_scene_collect); a
+                                         synchronous frame with "overlap" then waits for every lane
+                                         and reports the totals over all lanes                 */
 } rt_render_flags;
 
 /* Per-call options for rt_render.  Zero-initialise, then set what you need. */
@@ -397,6 +401,68 @@ rt_status rt_synchronize(rt_scene *scene);
 
 /* Renderer::cleanup (src/Global/Renderer.cu:368-391). */
 void rt_scene_destroy(rt_scene *scene);
+
+/* --- interactive loop without a window -------------------------------------------
+ * The reference's frame loop (src/Global/Renderer.cu:232-338) reads SDL key / mouse events, moves the
+ * camera (SDL_OpenGLWindow::calculateNewPosition, src/Global/SDL_OpenGLWindow.cu:182-256), recomputes the
+ * camera (RenderPin.cu:73-95), steps the move speed on the mouse wheel and caps the frame rate at 120 fps.
+ * These calls restate that host logic on caller-supplied input, so a scripted or remote input stream drives
+ * the same camera path; the window, the GL surface and SDL itself stay out (presentation).  Host-only. */
+
+/* OperateArgs (include/Global/SDL_OpenGLWindow.cuh:34-45, filled by getOperateArgs :63-74) plus the loop's
+ * relative-mouse-mode state (Renderer.cu:230, toggled by a click :239-241). */
+typedef struct rt_camera_control {
+    float mouse_sensitivity;       /* radians per mouse count */
+    float pitch_limit;             /* as getOperateArgs stores it: PI / degreeToRadian(pitch_limit_degree) */
+    float move_speed;              /* world units per frame; the wheel steps it */
+    float move_speed_change_step;
+    float fps_limit;               /* INFINITY: no cap */
+    uint32_t restrict_frame_count; /* fps_limit != INFINITY */
+    int64_t target_frame_us;       /* microseconds((int64)(1e6f / fps_limit)) */
+    int64_t sleep_margin_us;       /* 2000 */
+    uint32_t relative_mouse;       /* mouse motion counts only in relative mode (on at loop start) */
+    uint32_t reserved;
+} rt_camera_control;
+
+/* KeyMouseInputArgs (include/Global/SDL_OpenGLWindow.cuh:47-60) for one frame: held keys, the mouse motion
+ * and wheel accumulated since the previous frame (getKeyMouseInput resets them per frame,
+ * SDL_OpenGLWindow.cu:135-141), a click, quit. */
+typedef struct rt_input_state {
+    uint32_t key_w, key_a, key_s, key_d, key_space, key_lshift;
+    int32_t dx, dy;
+    int32_t d_speed;
+    uint32_t mouse_click;
+    uint32_t key_quit;
+} rt_input_state;
+
+/* getOperateArgs(fpsLimit, mouseSensitivity, pitchLimitDegree, moveSpeedNTimesStep, moveSpeedChangeStep); the
+ * reference's loop uses (120, 0.001, 80, 2, 0.05) (Renderer.cu:224-225). */
+rt_status rt_camera_control_init(rt_camera_control *ctl, float fps_limit, float mouse_sensitivity,
+                                 float pitch_limit_degree, uint32_t move_speed_n_steps, float move_speed_change_step);
+
+/* The camera half of one loop iteration (Renderer.cu:236-262): mouse motion (counted in relative mode) turns
+ * the view (yaw about V, then pitch about U, pitch clamp), held keys translate center and target in the
+ * horizontal plane / along up; a click toggles relative mode; the wheel steps ctl->move_speed (after the
+ * move, as the reference does).  `camera` is updated in place (center, target); *moved = 1 when the camera
+ * moved, i.e. when the reference recomputes the camera (the caller then passes it to rt_camera_set with the
+ * framebuffer size; the U / V / W the move used are those rt_camera_set derives from `camera`). */
+rt_status rt_camera_move(rt_camera_input *camera, rt_camera_control *ctl, const rt_input_state *input,
+                         uint32_t *moved);
+
+/* Monotonic clock (steady_clock) in nanoseconds. */
+int64_t rt_clock_ns(void);
+
+/* The frame limiter (Renderer.cu:327-337): when less than ctl->target_frame_us has passed since
+ * frame_start_ns, sleep until sleep_margin_us before the target, then spin until it.  Returns the
+ * nanoseconds spent waiting (0 when the frame took longer). */
+int64_t rt_frame_pace(const rt_camera_control *ctl, int64_t frame_start_ns);
+
+/* Abort a stuck multi-GPU frame instead of blocking: with a timeout set, every wait the library does on a
+ * frame that gathers over RCCL polls ncclCommGetAsyncError; on an asynchronous RCCL error or when the
+ * frame has not completed after `timeout_ms`, the communicators are aborted (ncclCommAbort), the scene is
+ * detached and the call returns RT_ERR_DEVICE.  0 (default) = wait without limit, polling only for
+ * asynchronous errors. */
+rt_status rt_comm_set_timeout(rt_scene *scene, uint32_t timeout_ms);
 
 /* --- introspection (tests / tooling) -------------------------------------------- */
 

@@ -16,7 +16,7 @@ namespace rtamd {
 __global__ __launch_bounds__(256) void assemble_kernel(const uint32_t *__restrict__ gathered, uint32_t slab_tiles,
                                                        uint32_t tile_w, uint32_t tile_h, uint32_t tile_count,
                                                        uint32_t width, uint32_t height, uint32_t *__restrict__ frame,
-                                                       bool frame_aligned) {
+                                                       bool aligned16) {
     const uint32_t g = blockIdx.x;
     const uint32_t rank = g / slab_tiles, k = g - rank * slab_tiles;
     const uint32_t t = rank + k * tile_count;
@@ -25,7 +25,7 @@ __global__ __launch_bounds__(256) void assemble_kernel(const uint32_t *__restric
     const uint32_t x0 = (t % tiles_x) * tile_w, y0 = (t / tiles_x) * tile_h;
     const uint32_t *src = gathered + (size_t)g * tile_w * tile_h;
     const uint32_t per = (tile_w & 3u) == 0 ? 4u : 1u;                    // pixels per thread step (a row piece)
-    const bool vec = per == 4u && (width & 3u) == 0 && frame_aligned;   // 16 B stores need a 16 B-aligned frame
+    const bool vec = per == 4u && (width & 3u) == 0 && aligned16;   // 16 B loads / stores: both buffers 16 B-aligned
     for (uint32_t q = threadIdx.x; q < tile_w * tile_h / per; q += blockDim.x) {
         const uint32_t p = per * q, row = p / tile_w, col = p - row * tile_w;
         const uint32_t y = y0 + row, x = x0 + col;
@@ -44,9 +44,12 @@ hipError_t launch_assemble(const void *gathered, uint32_t slab_tiles, uint32_t t
     const uint64_t blocks = (uint64_t)slab_tiles * tile_count;
     if (blocks == 0 || width == 0 || height == 0) return hipSuccess;
     if (tile_w == 0 || tile_h == 0 || blocks > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    if (((reinterpret_cast<uintptr_t>(frame) | reinterpret_cast<uintptr_t>(gathered)) & 3u) != 0)
+        return hipErrorInvalidValue;                                         // RGBA8 pixels are read as u32
     hipLaunchKernelGGL(assemble_kernel, dim3((uint32_t)blocks), dim3(256), 0, stream,
                        static_cast<const uint32_t *>(gathered), slab_tiles, tile_w, tile_h, tile_count, width, height,
-                       static_cast<uint32_t *>(frame), (reinterpret_cast<uintptr_t>(frame) & 15u) == 0);
+                       static_cast<uint32_t *>(frame),
+                       ((reinterpret_cast<uintptr_t>(frame) | reinterpret_cast<uintptr_t>(gathered)) & 15u) == 0);
     return hipGetLastError();
 }
 

@@ -36,6 +36,7 @@ Rccl load() {
     sym(r.CommSplit, "ncclCommSplit");
     sym(r.CommDestroy, "ncclCommDestroy");
     sym(r.CommAbort, "ncclCommAbort");
+    sym(r.CommGetAsyncError, "ncclCommGetAsyncError");
     sym(r.GroupStart, "ncclGroupStart");
     sym(r.GroupEnd, "ncclGroupEnd");
     sym(r.Send, "ncclSend");

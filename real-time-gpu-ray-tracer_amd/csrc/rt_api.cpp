@@ -23,6 +23,7 @@
 #include "../../include/rt.h"
 #include "bvh_build.hpp"
 #include "comm.hpp"
+#include "comm_wait.hpp"
 #include "host_math.hpp"
 #include "layout.hpp"
 #include "lbvh.hpp"
@@ -63,6 +64,12 @@ rt_status fail(rt_status s, const std::string &msg) {
     g_error = msg;
     return s;
 }
+
+#define RT_TRY(expr)                                                                               \
+    do {                                                                                           \
+        const rt_status st_ = (expr);                                                              \
+        if (st_ != RT_OK) return st_;                                                              \
+    } while (0)
 
 #define HIP_TRY(expr)                                                                              \
     do {                                                                                           \
@@ -118,10 +125,14 @@ struct DevBuf {
 };
 
 // rt_scene_attach_comm: this scene is rank `rank` of a `world`-rank frame.  One communicator
-// per overlap lane (split from the first), so the lanes' gathers on different streams never share one.
+// per overlap lane at attach time (split from the first), so the lanes' gathers on different streams do not
+// share one; lane q uses comm[q % ncomm] if "overlap" is raised after the attach (every rank issues the same
+// lane sequence, so a shared communicator still sees its operations in one order on every rank).
 struct CommState {
     static constexpr int NLANE = 8;
     int rank = 0, world = 1;
+    int ncomm = 1;
+    uint32_t timeout_ms = 0;               // rt_comm_set_timeout: 0 = no deadline (async errors still polled)
     uint32_t tile_w = 64, tile_h = 64;
     ncclComm_t comm[NLANE] = {};
     size_t slab_bytes = 0;                 // one rank's slab (largest tile count), RGBA8
@@ -325,6 +336,7 @@ struct rt_scene {
     bool gpu_tlas() const { return build_mode == RT_BUILD_LBVH || (gpu_tlas_sah && build_mode == RT_BUILD_SAH); }
 
     CommState *comm = nullptr;             // multi-GPU frame (rt_scene_attach_comm)
+    uint32_t comm_timeout_ms = 0;          // rt_comm_set_timeout (kept across attach / detach)
     void release_comm() {
         if (!comm) return;
         for (int q = 0; q < CommState::NLANE; q++) {
@@ -335,9 +347,30 @@ struct rt_scene {
         delete comm;
         comm = nullptr;
     }
+    // A failed frame (peer error or deadline): abort every communicator so the gather kernels in flight
+    // return, and drop the communicator state.  The slabs are not freed: kernels of the aborted frames may
+    // still reference them, and hipFree would wait for those (a bounded leak instead of a hang).
+    void abort_comm() {
+        if (!comm) return;
+        for (int q = 0; q < CommState::NLANE; q++)
+            if (comm->comm[q]) (void)rccl().CommAbort(comm->comm[q]);
+        delete comm;
+        comm = nullptr;
+        for (int q = 0; q < NLANE; q++) r_lane[q] = ev_lane_done[q];
+        r_done = nullptr;
+        for (int b = 0; b < NLANE; b++) { r_copied[b] = ev_copied[b]; r_used[b] = ev_used[b]; }
+    }
 
     ~rt_scene() {
         (void)hipSetDevice(device);
+        if (comm) {                            // a peer may be gone: bounded waits, abort instead of hanging
+            bool ok = true;
+            const auto q_ev = [](hipEvent_t e) { const hipError_t r = hipEventQuery(e); return r == hipSuccess ? 1 : (r == hipErrorNotReady ? 0 : -1); };
+            for (int q = 0; q < NLANE && ok; q++)
+                if (r_lane[q]) ok = poll_wait([&] { return q_ev(r_lane[q]); }, [] { return 0; },
+                                              comm->timeout_ms ? comm->timeout_ms : 10000u) == WaitResult::done;
+            if (!ok) abort_comm();
+        }
         if (stream) (void)hipStreamSynchronize(stream);
         for (int q = 0; q < NLANE; q++)          // launches still running on caller streams
             if (r_lane[q]) (void)hipEventSynchronize(r_lane[q]);
@@ -432,14 +465,53 @@ void store_rows(float *dst, const hm::Mat &m) {   // rows 1..3, cols 1..4
 
 rt_status gpu_build_blas(rt_scene *s);
 
+// Wait for a stream / an event of the scene.  With a communicator attached the wait polls (comm_wait.hpp):
+// an asynchronous RCCL error or the rt_comm_set_timeout deadline aborts the communicators and fails with
+// RT_ERR_DEVICE instead of blocking on a peer that will never send.
+int query_result(hipError_t r) { return r == hipSuccess ? 1 : (r == hipErrorNotReady ? 0 : -1); }
+rt_status comm_poll(rt_scene *s, hipStream_t st, hipEvent_t ev) {
+    CommState *cm = s->comm;
+    const Rccl &R = rccl();
+    int code = 0;
+    const WaitResult w = poll_wait(
+        [&] { return st ? query_result(hipStreamQuery(st)) : query_result(hipEventQuery(ev)); },
+        [&] {
+            return first_async_error(cm->ncomm, [&](int q, int *st) {
+                ncclResult_t a = ncclSuccess;
+                const ncclResult_t r = cm->comm[q] ? R.CommGetAsyncError(cm->comm[q], &a) : ncclSuccess;
+                *st = (int)a;
+                return (int)r;
+            });
+        },
+        cm->timeout_ms, &code);
+    if (w == WaitResult::done) return RT_OK;
+    if (w == WaitResult::failed) {
+        const hipError_t e = st ? hipStreamSynchronize(st) : hipEventSynchronize(ev);
+        return fail(RT_ERR_DEVICE, std::string("multi-GPU frame: ") + hipGetErrorString(e));
+    }
+    const std::string why = w == WaitResult::timeout
+        ? "multi-GPU frame not complete after " + std::to_string(cm->timeout_ms) + " ms (a peer stopped?)"
+        : std::string("RCCL asynchronous error: ") + R.GetErrorString((ncclResult_t)code);
+    s->abort_comm();
+    return fail(RT_ERR_DEVICE, why + "; communicators aborted, scene detached");
+}
+rt_status wait_stream(rt_scene *s, hipStream_t st) {
+    if (s->comm) return comm_poll(s, st, nullptr);
+    const hipError_t e = hipStreamSynchronize(st);
+    return e == hipSuccess ? RT_OK : fail(RT_ERR_DEVICE, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
+}
+rt_status wait_event(rt_scene *s, hipEvent_t ev) {
+    if (s->comm) return comm_poll(s, nullptr, ev);
+    const hipError_t e = hipEventSynchronize(ev);
+    return e == hipSuccess ? RT_OK : fail(RT_ERR_DEVICE, std::string("hipEventSynchronize: ") + hipGetErrorString(e));
+}
 // Wait for every enqueued launch of the scene: its own stream, the last caller stream, every lane.
-hipError_t drain(rt_scene *s) {
-    hipError_t e = hipSuccess;
-    if (s->last_stream) e = hipStreamSynchronize(s->last_stream);
-    if (e == hipSuccess && s->stream) e = hipStreamSynchronize(s->stream);
-    for (int q = 0; q < rt_scene::NLANE && e == hipSuccess; q++)
-        if (s->r_lane[q]) e = hipEventSynchronize(s->r_lane[q]);
-    return e;
+rt_status drain(rt_scene *s) {
+    if (s->last_stream) RT_TRY(wait_stream(s, s->last_stream));
+    if (s->stream) RT_TRY(wait_stream(s, s->stream));
+    for (int q = 0; q < rt_scene::NLANE; q++)
+        if (s->r_lane[q]) RT_TRY(wait_event(s, s->r_lane[q]));
+    return RT_OK;
 }
 
 // Host half of one frame: update callback, instance matrices, TLAS rebuild, staging, upload.
@@ -452,7 +524,7 @@ hipError_t drain(rt_scene *s) {
 rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool defer = false) {
     const int b = s->active < 0 ? 0 : (s->active + 1) % rt_scene::NLANE;
     const auto w0 = std::chrono::steady_clock::now();
-    HIP_TRY(hipEventSynchronize(s->r_copied[b]));      // staging[b] no longer read by a pending copy
+    RT_TRY(wait_event(s, s->r_copied[b]));             // staging[b] no longer read by a pending copy
     s->update_wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     if (s->update) {                                  // Renderer.cu:269
         std::vector<rt_xform> xs(s->inst.size());
@@ -678,7 +750,7 @@ rt_status gpu_build_blas(rt_scene *s) {
         rt_status st;
         if (sp.pairs.n != s->blas_pairs.n || sp.tri_hot.n != s->tri_hot.n || sp.sph_hot.n != s->sph_hot.n ||
             sp.quad_hot.n != s->quad_hot.n || sp.roots.n != s->blas_roots.n) {
-            HIP_TRY(drain(s));
+            RT_TRY(drain(s));
             sp.release();
             if ((st = alloc_buf(sp.pairs, s->blas_pairs.n)) != RT_OK) return st;
             if ((st = alloc_buf(sp.quads, s->blas_quads.n)) != RT_OK) return st;
@@ -763,7 +835,7 @@ rt_status gpu_setup_blas(rt_scene *s, const std::vector<LbvhSeg> &segs, const ui
     // one-time readback for introspection (rt_scene_get_info)
     uint32_t pairs = 0;
     std::vector<TreeRoot> roots(segs.size());
-    HIP_TRY(drain(s));
+    RT_TRY(drain(s));
     HIP_TRY(hipMemcpy(&pairs, s->gpu_counts.p, sizeof pairs, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(roots.data(), s->blas_roots.p, roots.size() * sizeof(TreeRoot), hipMemcpyDeviceToHost));
     s->blas_pair_count = pairs;
@@ -838,7 +910,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     if (mode != RT_BUILD_COMPAT_MEDIAN && mode != RT_BUILD_SAH && mode != RT_BUILD_LBVH)
         return fail(RT_ERR_UNSUPPORTED, "unsupported build mode");
     HIP_TRY(hipSetDevice(s->device));
-    if (s->built) HIP_TRY(drain(s));              // a rebuild frees buffers earlier frames may still read
+    if (s->built) RT_TRY(drain(s));              // a rebuild frees buffers earlier frames may still read
     s->build_seed = seed;
     s->build_mode = mode;
     s->inst.clear();
@@ -1238,15 +1310,17 @@ rt_status rt_scene_attach_comm(rt_scene *s, const rt_comm_id *id, int rank, int 
     const Rccl &R = rccl();
     if (!R.ok) return fail(RT_ERR_UNSUPPORTED, R.error);
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(drain(s));
+    RT_TRY(drain(s));
     s->release_comm();
     auto *cm = new (std::nothrow) CommState();
     if (!cm) return fail(RT_ERR_OUT_OF_MEMORY, "host allocation failed");
     cm->rank = rank; cm->world = world; cm->tile_w = tw; cm->tile_h = th;
+    cm->ncomm = (int)std::max<uint32_t>(1u, s->overlap ? s->lanes : 1u);   // one per lane in use
+    cm->timeout_ms = s->comm_timeout_ms;
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
     ncclResult_t e = R.CommInitRank(&cm->comm[0], world, u, rank);
-    for (int q = 1; q < CommState::NLANE && e == ncclSuccess; q++) e = R.CommSplit(cm->comm[0], 0, rank, &cm->comm[q], nullptr);
+    for (int q = 1; q < cm->ncomm && e == ncclSuccess; q++) e = R.CommSplit(cm->comm[0], 0, rank, &cm->comm[q], nullptr);
     s->comm = cm;
     if (e != ncclSuccess) {
         const std::string msg = std::string("RCCL communicator: ") + R.GetErrorString(e);
@@ -1256,11 +1330,18 @@ rt_status rt_scene_attach_comm(rt_scene *s, const rt_comm_id *id, int rank, int 
     return RT_OK;
 }
 
+rt_status rt_comm_set_timeout(rt_scene *s, uint32_t timeout_ms) {
+    if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
+    s->comm_timeout_ms = timeout_ms;
+    if (s->comm) s->comm->timeout_ms = timeout_ms;
+    return RT_OK;
+}
+
 rt_status rt_scene_detach_comm(rt_scene *s) {
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
     if (!s->comm) return RT_OK;
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(drain(s));
+    RT_TRY(drain(s));
     s->release_comm();
     return RT_OK;
 }
@@ -1328,7 +1409,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         const size_t slab_bytes = (size_t)slab_tile_count(W, H, cm->tile_w, cm->tile_h, (uint32_t)cm->world) * cm->tile_w *
                                   cm->tile_h * 4;
         if (slab_bytes != cm->slab_bytes) {    // first frame, or the camera size changed: lanes may be in flight
-            HIP_TRY(drain(s));
+            RT_TRY(drain(s));
             for (int l = 0; l < CommState::NLANE; l++) { cm->slab[l].release(); cm->gathered[l].release(); }
             cm->slab_bytes = slab_bytes;
         }
@@ -1521,9 +1602,9 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             ncclResult_t e = R.GroupStart();
             if (cm->rank == 0) {
                 for (int r = 1; r < cm->world && e == ncclSuccess; r++)
-                    e = R.Recv(cm->gathered[q].p + (size_t)r * sb, sb, ncclUint8, r, cm->comm[q], stream);
+                    e = R.Recv(cm->gathered[q].p + (size_t)r * sb, sb, ncclUint8, r, cm->comm[q % cm->ncomm], stream);
             } else if (e == ncclSuccess) {
-                e = R.Send(cm->slab[q].p, sb, ncclUint8, 0, cm->comm[q], stream);
+                e = R.Send(cm->slab[q].p, sb, ncclUint8, 0, cm->comm[q % cm->ncomm], stream);
             }
             const ncclResult_t e2 = R.GroupEnd();
             if (e != ncclSuccess || e2 != ncclSuccess)
@@ -1544,8 +1625,22 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; stats->update_wait_ms = s->update_wait_ms; }
         return RT_OK;
     }
-    HIP_TRY(hipMemcpyAsync(s->counters_host, lane_counters, CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
-    HIP_TRY(hipStreamSynchronize(stream));
+    // counters: this lane's block; with "overlap" + RT_RENDER_KEEP_COUNTERS the accumulated totals of every lane
+    // in the current epoch (as rt_scene_collect sums them), after every lane's launches finished
+    const bool sum_lanes = s->overlap && (o.flags & RT_RENDER_KEEP_COUNTERS);
+    if (!sum_lanes)
+        HIP_TRY(hipMemcpyAsync(s->counters_host, lane_counters, CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost, stream));
+    RT_TRY(wait_stream(s, stream));
+    if (sum_lanes) {
+        RT_TRY(drain(s));
+        HIP_TRY(hipMemcpy(s->counters_host, s->counters, rt_scene::NLANE * CNT_NUM * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost));
+        for (int l = 1; l < rt_scene::NLANE; l++)          // lane blocks of the current epoch, summed into block 0
+            for (uint32_t k = 0; k < CNT_NUM; k++) {
+                if (l == 1 && s->lane_epoch[0] != s->cnt_epoch) s->counters_host[k] = 0;
+                if (s->lane_epoch[l] == s->cnt_epoch) s->counters_host[k] += s->counters_host[(size_t)l * CNT_NUM + k];
+            }
+    }
     s->ring_pending = 0;
     if (rgba_host && cm && cm->rank == 0) HIP_TRY(hipMemcpy(rgba_host, frame_out, (size_t)W * H * 4, hipMemcpyDeviceToHost));
     else if (rgba_host && !cm) HIP_TRY(hipMemcpy(rgba_host, out.rgba, npix * 4, hipMemcpyDeviceToHost));
@@ -1569,6 +1664,7 @@ rt_status rt_assemble_tiles(rt_scene *s, const void *gathered, uint32_t slab_til
     if (!s || !gathered || !frame) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
     if (!s->cam_ok) return fail(RT_ERR_STATE, "rt_camera_set has not been called");
     if (tw == 0 || th == 0 || tile_count == 0) return fail(RT_ERR_INVALID_ARGUMENT, "bad tile geometry");
+    if (((uintptr_t)gathered | (uintptr_t)frame) & 3u) return fail(RT_ERR_INVALID_ARGUMENT, "RGBA8 buffers must be 4-byte aligned");
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : s->stream;
     HIP_TRY(launch_assemble(gathered, slab_tiles, tw, th, tile_count, s->width, s->height, frame, st));
@@ -1683,11 +1779,11 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         s->tlas_leaf = (uint32_t)value;          // next frame's TLAS
     } else if (k == "inst_by_slot") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "inst_by_slot must be 0 or 1");
-        HIP_TRY(drain(s));
+        RT_TRY(drain(s));
         s->inst_by_slot = value == 1;            // takes effect with the next frame's staging
     } else if (k == "overlap") {
         if (value < 0 || value > rt_scene::NLANE) return fail(RT_ERR_INVALID_ARGUMENT, "overlap must be 0..8 lanes");
-        HIP_TRY(drain(s));
+        RT_TRY(drain(s));
         s->lanes = value < 1 ? 1u : (uint32_t)value;
         s->overlap = s->lanes > 1;
         s->lane = 0;
@@ -1725,7 +1821,7 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
         // 45 floats each: inverse, forward, inverse-transpose rows 1-3 (12 each), transformed box, centroid
         if (!s->built || !s->gpu_tlas()) return fail(RT_ERR_UNSUPPORTED, "instance records are computed on the GPU for RT_BUILD_LBVH only");
         HIP_TRY(hipSetDevice(s->device));
-        HIP_TRY(drain(s));
+        RT_TRY(drain(s));
         const size_t n = s->inst.size();
         *bytes = n * 45 * sizeof(float);
         if (capacity) {
@@ -1753,7 +1849,7 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
         // RT_BUILD_LBVH: the forest as built on the GPU (NodePair / NodeQuad / TreeRoot records, layout.hpp)
         if (!s->built || !s->gpu_tlas()) return fail(RT_ERR_UNSUPPORTED, "raw BLAS records are exported for RT_BUILD_LBVH only");
         HIP_TRY(hipSetDevice(s->device));
-        HIP_TRY(drain(s));
+        RT_TRY(drain(s));
         const void *from = k == "blas_pairs" ? (const void *)s->blas_pairs.p
                                              : (k == "blas_quads" ? (const void *)s->blas_quads.p : (const void *)s->blas_roots.p);
         *bytes = k == "blas_roots" ? s->blas.size() * sizeof(TreeRoot)
@@ -1764,7 +1860,7 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
         // caller triangle index of every leaf-ordered triangle slot (TriCold::orig_index): BLAS b owns
         // the slots [slot_base, slot_base + count) of its primitives, in leaf order
         HIP_TRY(hipSetDevice(s->device));
-        HIP_TRY(drain(s));
+        RT_TRY(drain(s));
         const size_t n = s->tri_cold.n;
         *bytes = n * sizeof(uint32_t);
         if (capacity && n) {
@@ -1783,7 +1879,7 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
     }
     if (!src || size == 0) return fail(RT_ERR_STATE, "debug buffer " + k + " not recorded (set the option first)");
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(drain(s));
+    RT_TRY(drain(s));
     if (capacity) HIP_TRY(hipMemcpy(dst, src, capacity < size ? capacity : size, hipMemcpyDeviceToHost));
     *bytes = size;
     return RT_OK;
@@ -1805,7 +1901,7 @@ rt_status rt_scene_collect(rt_scene *s, rt_stats *acc, float *kernel_ms, uint32_
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
     if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(drain(s));
+    RT_TRY(drain(s));
     HIP_TRY(hipMemcpy(s->counters_host, s->counters, rt_scene::NLANE * CNT_NUM * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     unsigned long long sum[CNT_NUM] = {};
     for (int l = 0; l < rt_scene::NLANE; l++)          // lanes whose block belongs to the current epoch
@@ -1839,7 +1935,7 @@ rt_status rt_scene_update_triangles(rt_scene *s, size_t first, size_t count, con
     for (size_t k = 0; k < count; k++) material_slot(s, tris[k].material_type, tris[k].material_index, ok);
     if (!ok) return fail(RT_ERR_INVALID_ARGUMENT, "triangle references a material out of range");
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(drain(s));        // a pending BLAS build may still read the raw array
+    RT_TRY(drain(s));        // a pending BLAS build may still read the raw array
     std::memcpy(s->tris.data() + first, tris, count * sizeof(rt_triangle));
     HIP_TRY(hipMemcpy(s->raw_tris.p + first, tris, count * sizeof(rt_triangle), hipMemcpyHostToDevice));
     // instance boxes derived from the triangles (RenderPin.cu:124-139); VTK-style bounds stay as given
@@ -1896,8 +1992,8 @@ rt_status rt_scene_update_instances(rt_scene *s, size_t first, size_t count, con
 rt_status rt_synchronize(rt_scene *s) {
     if (!s) return fail(RT_ERR_INVALID_ARGUMENT, "null scene");
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(drain(s));
-    if (s->r_done) HIP_TRY(hipEventSynchronize(s->r_done));
+    RT_TRY(drain(s));
+    if (s->r_done) RT_TRY(wait_event(s, s->r_done));
     return RT_OK;
 }
 

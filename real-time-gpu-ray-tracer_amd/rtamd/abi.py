@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-RT_ABI_VERSION = 1
+RT_ABI_VERSION = 2
 
 RT_OK = 0
 RT_STATUS_NAMES = {
@@ -132,6 +132,21 @@ class CommId(C.Structure):
     _fields_ = [("internal", C.c_char * 128)]
 
 
+class CameraControl(C.Structure):
+    """rt_camera_control: OperateArgs (SDL_OpenGLWindow.cuh:34-45) + the loop's relative-mouse state."""
+    _fields_ = [("mouse_sensitivity", C.c_float), ("pitch_limit", C.c_float), ("move_speed", C.c_float),
+                ("move_speed_change_step", C.c_float), ("fps_limit", C.c_float), ("restrict_frame_count", C.c_uint32),
+                ("target_frame_us", C.c_int64), ("sleep_margin_us", C.c_int64), ("relative_mouse", C.c_uint32),
+                ("reserved", C.c_uint32)]
+
+
+class InputState(C.Structure):
+    """rt_input_state: KeyMouseInputArgs (SDL_OpenGLWindow.cuh:47-60) for one frame."""
+    _fields_ = [("key_w", C.c_uint32), ("key_a", C.c_uint32), ("key_s", C.c_uint32), ("key_d", C.c_uint32),
+                ("key_space", C.c_uint32), ("key_lshift", C.c_uint32), ("dx", C.c_int32), ("dy", C.c_int32),
+                ("d_speed", C.c_int32), ("mouse_click", C.c_uint32), ("key_quit", C.c_uint32)]
+
+
 class VtkInfo(C.Structure):
     _fields_ = [("point_count", C.c_uint64), ("particle_count", C.c_uint64),
                 ("strip_vertex_count", C.c_uint64), ("triangle_count", C.c_uint64)]
@@ -152,6 +167,7 @@ EXPORTED_SYMBOLS = (
     "rt_vtk_read", "rt_vtk_free", "rt_vtk_get_info", "rt_vtk_particles", "rt_vtk_vertices", "rt_vtk_convert",
     "rt_vtk_series_read", "rt_vtk_series_count", "rt_vtk_series_entry", "rt_vtk_series_free",
     "rt_comm_unique_id", "rt_scene_attach_comm", "rt_scene_detach_comm", "rt_slab_tiles", "rt_tile_pixels",
+    "rt_comm_set_timeout", "rt_camera_control_init", "rt_camera_move", "rt_clock_ns", "rt_frame_pace",
 )
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -223,6 +239,15 @@ def _declare(lib):
     lib.rt_tile_pixels.argtypes = [C.c_uint32] * 6 + [C.c_uint64, C.c_uint64, C.c_void_p]
     for name in ("rt_comm_unique_id", "rt_scene_attach_comm", "rt_scene_detach_comm", "rt_tile_pixels"):
         getattr(lib, name).restype = C.c_int
+    lib.rt_comm_set_timeout.argtypes = [C.c_void_p, C.c_uint32]
+    lib.rt_comm_set_timeout.restype = C.c_int
+    lib.rt_camera_control_init.argtypes = [P(CameraControl), C.c_float, C.c_float, C.c_float, C.c_uint32, C.c_float]
+    lib.rt_camera_control_init.restype = C.c_int
+    lib.rt_camera_move.argtypes = [P(CameraInput), P(CameraControl), P(InputState), P(C.c_uint32)]
+    lib.rt_camera_move.restype = C.c_int
+    lib.rt_clock_ns.restype = C.c_int64
+    lib.rt_frame_pace.argtypes = [P(CameraControl), C.c_int64]
+    lib.rt_frame_pace.restype = C.c_int64
     lib.rt_demo_update.argtypes = [C.c_void_p, P(Xform), C.c_size_t, C.c_uint64]
     lib.rt_demo_update.restype = None
     return lib

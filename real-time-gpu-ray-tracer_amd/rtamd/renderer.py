@@ -52,6 +52,19 @@ class Renderer:
         ci = self.scene.camera_input(**camera)
         abi.check(self.lib, self.lib.rt_camera_set(self.h, C.byref(ci), width, height))
         self.width, self.height = width, height
+        self.camera = ci
+        return self
+
+    def set_camera(self, camera_input: abi.CameraInput):
+        """Renderer::configureCamera with an explicit CameraInput (the interactive loop's moved camera,
+        Renderer.cu:247-251 -> RenderPin.cu:73-95), same framebuffer size."""
+        abi.check(self.lib, self.lib.rt_camera_set(self.h, C.byref(camera_input), self.width, self.height))
+        self.camera = camera_input
+        return self
+
+    def set_comm_timeout(self, timeout_ms: int):
+        """rt_comm_set_timeout: bounded waits on multi-GPU frames (0 = unbounded, async errors still polled)."""
+        abi.check(self.lib, self.lib.rt_comm_set_timeout(self.h, int(timeout_ms)))
         return self
 
     def set_option(self, key: str, value: int):

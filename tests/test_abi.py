@@ -19,6 +19,7 @@ STRUCTS = {
     "rt_instance_desc": abi.InstanceDesc, "rt_scene_desc": abi.SceneDesc, "rt_camera_input": abi.CameraInput,
     "rt_render_opts": abi.RenderOpts, "rt_stats": abi.Stats, "rt_hit": abi.Hit, "rt_scene_info": abi.SceneInfo,
     "rt_vtk_info": abi.VtkInfo, "rt_vtk_particle": abi.VtkParticle,
+    "rt_camera_control": abi.CameraControl, "rt_input_state": abi.InputState,
 }
 
 
@@ -29,6 +30,9 @@ def _c_layout(tmp_path):
         lines.append(f'printf("{cname} %zu\\n", sizeof({cname}));')
         for fname, _ in py._fields_:
             lines.append(f'printf("{cname}.{fname} %zu\\n", offsetof({cname}, {fname}));')
+    # the layout RT_ABI_VERSION 2 promises (rt.h): a caller whose rt_stats differs is built against another ABI
+    lines.append('_Static_assert(sizeof(rt_stats) == 96, "rt_stats layout of ABI 2");')
+    lines.append(f'_Static_assert(RT_ABI_VERSION == {abi.RT_ABI_VERSION}u, "rt.h and the ctypes mirror disagree");')
     lines.append('return 0;}')
     src = tmp_path / "layout.c"
     src.write_text("\n".join(lines))

@@ -94,3 +94,74 @@ def test_c4_through_the_comm_path(gpu_lib):
     full = r.render(0)[0]
     r.attach_comm(Renderer.comm_unique_id(), 0, 1, 64, 64)
     assert np.array_equal(r.render(0)[0], full)
+
+
+def test_comm_timeout_frames_and_state(gpu_lib):
+    """rt_comm_set_timeout: every wait on a multi-GPU frame polls (completion, ncclCommGetAsyncError, the
+    deadline); frames that complete are unaffected, and the setting survives a re-attach."""
+    s = scenes.demo_with_particles(4)
+    W, H = 256, 144
+    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(W, H, ray_trace_depth=2)
+    ref = [r.render(f)[0] for f in range(3)]
+    r.set_comm_timeout(5000)
+    r.attach_comm(Renderer.comm_unique_id(), 0, 1, 32, 32)
+    for f in range(3):
+        assert np.array_equal(r.render(f)[0], ref[f])
+    r.set_comm_timeout(0)
+    r.synchronize()
+    r.detach_comm().attach_comm(Renderer.comm_unique_id(), 0, 1, 64, 32)
+    assert np.array_equal(r.render(2)[0], ref[2])
+    r.cleanup()
+
+
+def _two_gpu_rank(rank, world, id_path, out_path):
+    import os
+    import sys
+    import time
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [repo, os.path.join(repo, "real-time-gpu-ray-tracer_amd")]
+    import torch
+    from rtamd import Renderer as R, scenes as S
+    torch.cuda.set_device(rank)
+    s = S.demo_with_particles(10)
+    W, H = 480, 272
+    r = R(s, device=rank).build_acceleration_structure(0, mode="sah").configure_camera(W, H, ray_trace_depth=2)
+    ref = [r.render(f)[0] for f in range(6)] if rank == 0 else None
+    if rank == 0:
+        with open(id_path + ".tmp", "wb") as f:
+            f.write(R.comm_unique_id())
+        os.replace(id_path + ".tmp", id_path)
+    while not os.path.exists(id_path):
+        time.sleep(0.01)
+    cid = open(id_path, "rb").read()
+    r.set_comm_timeout(60000)
+    r.attach_comm(cid, rank, world, 32, 32)
+    ok = True
+    for f in range(3):                                     # synchronous frames
+        rgba = r.render(f)[0]
+        if rank == 0:
+            ok &= bool(np.array_equal(rgba, ref[f]))
+    r.set_option("overlap", 3)                            # lanes beyond the attach-time communicators
+    lanes = [torch.cuda.Stream() for _ in range(3)]
+    bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(6)]
+    for f in range(6):
+        r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=lanes[f % 3].cuda_stream, sync=False)
+    r.synchronize()
+    torch.cuda.synchronize()
+    if rank == 0:
+        for f in range(6):
+            ok &= bool(np.array_equal(bufs[f].cpu().numpy().reshape(H, W, 4), ref[f]))
+        np.save(out_path, np.array([ok]))
+    r.cleanup()
+
+
+def test_two_gpus_gather_equals_single_launch(gpu_lib, tmp_path):
+    """World 2 on two GPUs (skipped on a one-GPU box): the RCCL Send / Recv branch of rt_render, synchronous
+    and on three overlapped lanes; rank 0's assembled frames equal its own single-launch frames."""
+    import torch
+    import torch.multiprocessing as mp
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two GPUs (RCCL rejects two ranks on one device)")
+    out = str(tmp_path / "ok.npy")
+    mp.spawn(_two_gpu_rank, args=(2, str(tmp_path / "id.bin"), out), nprocs=2, join=True)
+    assert bool(np.load(out)[0])

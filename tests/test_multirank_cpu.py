@@ -1,9 +1,12 @@
 """World-size-2 gloo test of the multi-GPU frame protocol on CPU.
 
-Each rank renders only its interleaved screen tiles (here with the oracle, per tile region),
-packs them into a padded tile-compact slab, the slabs are gathered to rank 0 exactly as
-bench.py does with RCCL, and rank 0 assembles the frame.  The result must be byte-identical to
-a single-rank full-frame render: the RNG is keyed by the global padded pixel index.
+Each rank fills only its interleaved screen tiles, packed into a padded tile-compact slab through the
+library's own slab -> frame mapping (rt_slab_tiles / rt_tile_pixels, csrc/layout.hpp tile_pixel — the
+function the trace kernel's tile map and the assemble kernel use); the slabs are gathered to rank 0 as the
+library's RCCL chain does, and rank 0 assembles the frame with the same mapping.  A pixel's content is a
+function of its frame position and the frame number only (as a traced pixel is: the RNG is keyed by the
+global padded pixel index), so the assembled frame must equal that function over the whole frame for any
+world size.  No renderer runs here: the GPU chain itself is tested in tests/test_gpu_multigpu.py.
 """
 import os
 import socket
@@ -14,7 +17,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-from rtamd import scenes, tiles
+from rtamd import tiles
 
 W, H, TW, TH = 200, 120, 64, 32
 
@@ -27,14 +30,21 @@ def _free_port():
     return port
 
 
-def _render_slab(o, rank, count):
-    """The rank's tiles traced by the oracle (the checker stands in for the GPU here), packed into the
-    padded slab with the library's slab -> frame mapping (rt_tile_pixels, the assemble kernel's)."""
-    canvas = np.zeros((H, W, 4), np.uint8)
+def pixel_values(frame):
+    """(H, W, 4) uint8: a pixel's content as a function of (x, y, frame) only, distinct for every pixel."""
+    y, x = np.mgrid[0:H, 0:W]
+    return np.stack([x & 255, y & 255, ((x >> 8) | ((y >> 8) << 4)) ^ (frame & 15),
+                     np.full_like(x, 255 - (frame & 127))], axis=-1).astype(np.uint8)
+
+
+def _render_slab(frame, rank, count):
+    """The rank's slab: only its own tiles' pixels are taken (through rt_tile_pixels); the rest of the
+    canvas is poisoned, so a pixel landing in another rank's tile shows up in the assembled frame."""
+    mine = np.zeros((H, W), bool)
     for t in tiles.rank_tiles(W, H, TW, TH, rank, count):
         x0, y0 = tiles.tile_origin(t, W, TW, TH)
-        w, h = min(TW, W - x0), min(TH, H - y0)
-        canvas[y0:y0 + h, x0:x0 + w] = o.render(region=(x0, y0, w, h), threads=2, want_rgb=False)[1]
+        mine[y0:y0 + TH, x0:x0 + TW] = True
+    canvas = np.where(mine[..., None], pixel_values(frame), np.uint8(0xAB))
     return tiles.pack(lambda: canvas, W, H, TW, TH, rank, count)
 
 
@@ -42,20 +52,15 @@ def _worker(rank, world, port, result_path):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [repo, os.path.join(repo, "real-time-gpu-ray-tracer_amd")]
-    from oracle.oracle import OracleScene
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    o = OracleScene(scenes.demo_with_particles(4), build_seed=2)
-    o.camera(W, H, ray_trace_depth=2)
-    o.update(5)
-    slab = torch.from_numpy(_render_slab(o, rank, world))
+    slab = torch.from_numpy(_render_slab(5, rank, world))
     gather = [torch.zeros_like(slab) for _ in range(world)] if rank == 0 else None
     dist.gather(slab, gather, dst=0)
     if rank == 0:
         g = torch.stack(gather).numpy()
         frame = tiles.assemble(g, W, H, TW, TH, world)
-        _, full, _ = o.render(threads=2, want_rgb=False)
-        np.save(result_path, np.stack([frame, full]))
+        np.save(result_path, np.stack([frame, pixel_values(5)]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -66,11 +71,8 @@ def _pipelined_worker(rank, world, port, result_path):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [repo, os.path.join(repo, "real-time-gpu-ray-tracer_amd")]
-    from oracle.oracle import OracleScene
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    o = OracleScene(scenes.demo_with_particles(4), build_seed=2)
-    o.camera(W, H, ray_trace_depth=1)
     st = tiles.slab_tiles(W, H, TW, TH, world)
     slabs = [torch.zeros(st * TW * TH, 4, dtype=torch.uint8) for _ in range(2)]
     gathered = [[torch.zeros_like(slabs[0]) for _ in range(world)] if rank == 0 else None for _ in range(2)]
@@ -85,8 +87,7 @@ def _pipelined_worker(rank, world, port, result_path):
 
     for f in range(3):
         b = f % 2
-        o.update(f)
-        slabs[b].copy_(torch.from_numpy(_render_slab(o, rank, world)))
+        slabs[b].copy_(torch.from_numpy(_render_slab(f, rank, world)))
         work = dist.gather(slabs[b], gathered[b], dst=0, async_op=True)
         finish()
         pending.append((work, gathered[b], f))
@@ -94,8 +95,7 @@ def _pipelined_worker(rank, world, port, result_path):
     if rank == 0:
         out = []
         for f, frame in frames:
-            o.update(f)
-            out.append(np.stack([frame, o.render(threads=2, want_rgb=False)[1]]))
+            out.append(np.stack([frame, pixel_values(f)]))
         np.save(result_path, np.stack(out))
     dist.barrier()
     dist.destroy_process_group()
@@ -108,11 +108,8 @@ def _lanes_worker(rank, world, port, result_path, nl=3):
     import sys
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [repo, os.path.join(repo, "real-time-gpu-ray-tracer_amd")]
-    from oracle.oracle import OracleScene
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    o = OracleScene(scenes.demo_with_particles(4), build_seed=2)
-    o.camera(W, H, ray_trace_depth=1)
     st = tiles.slab_tiles(W, H, TW, TH, world)
     slabs = [torch.zeros(st * TW * TH, 4, dtype=torch.uint8) for _ in range(nl)]
     gathered = [[torch.zeros_like(slabs[0]) for _ in range(world)] if rank == 0 else None for _ in range(nl)]
@@ -120,13 +117,12 @@ def _lanes_worker(rank, world, port, result_path, nl=3):
     out = []
     for f in range(2 * nl):
         b = f % nl
-        o.update(f)
-        slabs[b].copy_(torch.from_numpy(_render_slab(o, rank, world)))
+        slabs[b].copy_(torch.from_numpy(_render_slab(f, rank, world)))
         dist.gather(slabs[b], gathered[b], dst=0, async_op=True).wait()
         if rank == 0:
             frame_bufs[b][:] = tiles.assemble(torch.stack(gathered[b]).numpy(), W, H, TW, TH, world)
             if f >= nl:       # lane b's previous frame has been replaced by frame f
-                out.append(np.stack([frame_bufs[b].copy(), o.render(threads=2, want_rgb=False)[1]]))
+                out.append(np.stack([frame_bufs[b].copy(), pixel_values(f)]))
     if rank == 0:
         np.save(result_path, np.stack(out))
     dist.barrier()
@@ -151,7 +147,7 @@ def test_pipelined_gather_gloo(tmp_path):
         assert np.array_equal(frame, full)
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_tile_gather_assemble_gloo(tmp_path, world):
     out = str(tmp_path / "res.npy")
     mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
