@@ -17,6 +17,7 @@ Rank 0 prints one JSON line (see DESIGN.md §4 for every field's definition).
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -37,6 +38,7 @@ A_AABB, A_TRI, A_SQ, A_INST, A_RAY, A_PIXEL = 32, 36, 32, 48, 32, 4
 B_PAIR, B_TRI, B_SPH, B_QUAD, B_INST, B_HIT, B_PIXEL = 64, 48, 16, 80, 80, 208, 4
 # measured HBM fraction below which the kernel is reported latency-bound
 LATENCY_BOUND_FRAC = 0.25
+PMC_DIR = os.path.join(REPO, "profiles", "pmc")
 
 
 def parse():
@@ -65,6 +67,7 @@ def parse():
                    help="N = 1: run the multi-GPU frame path anyway (a world-1 RCCL communicator: tiles + assemble)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--print-pmc-tag", action="store_true", help="print this run's PMC tag as JSON and exit (no GPU)")
     return p.parse_args()
 
 
@@ -132,23 +135,48 @@ def cpu_baseline(scene, cfg, budget_s):
             "trees": "compat (reference random-axis median split)"}
 
 
-def load_traffic(kname):
-    """HBM bytes per launch of this kernel from the committed rocprofv3 PMC summary of the default
-    bench command (profiles/pmc_latest.json, written by scripts/pmc_passes.sh); None if absent."""
-    path = os.path.join(REPO, "profiles", "pmc_latest.json")
-    want = ("dev_exact::" if "<exact>" in kname else "dev_fast::") + kname.split("<")[0] + "<"
+def lib_sha16():
+    """Identity of the trace library this run loads (the PMC summaries are tagged with it)."""
+    from rtamd import abi
+    path = os.environ.get("RTAMD_LIB") or abi.LIB_PATH
+    with open(path, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def pmc_tag(args):
+    """What a PMC summary must have been measured on to price this run's launches: the same config, BVH
+    builder, per-frame rebuild, kernel (EXACT / FAST, persistent / grid), scene options and library build."""
+    return {"config": args.config, "build": args.build, "rebuild": bool(args.rebuild), "exact": bool(args.exact),
+            "kernel": int(args.kernel), "options": sorted(args.pre_opt + args.opt), "lib_sha16": lib_sha16()}
+
+
+def pmc_path(tag):
+    return os.path.join(PMC_DIR, f"{tag['config']}_{tag['build']}{'_rebuild' if tag['rebuild'] else ''}"
+                                 f"{'_exact' if tag['exact'] else ''}{'' if tag['kernel'] else '_grid'}.json")
+
+
+def load_traffic(tag):
+    """HBM bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, MI355X_MICROARCH.md's gfx950 correction) of the trace
+    kernel from the committed rocprofv3 PMC summary of this exact workload (scripts/pmc_tagged.sh writes
+    profiles/pmc/<config>_<build>....json): only if every tag field, the library hash included, matches.
+    Returns (bytes or None, summary path or None, why)."""
+    path = pmc_path(tag)
     try:
         with open(path) as f:
             d = json.load(f)
-        if want in d.get("kernel", ""):
-            return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        pass
-    return None
+        return None, None, f"no PMC summary {os.path.relpath(path, REPO)}"
+    diff = [k for k, v in tag.items() if d.get("tag", {}).get(k) != v]
+    if diff:
+        return None, None, f"{os.path.relpath(path, REPO)} measured another workload or build ({', '.join(diff)} differ)"
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO), "tagged PMC summary"
 
 
 def main():
     args = parse()
+    if args.print_pmc_tag:
+        print(json.dumps(pmc_tag(args)))
+        return
     if not 1 <= args.steps <= 256:
         raise SystemExit("--steps must be in 1..256 (the library's per-frame kernel-time ring)")
     global TILE
@@ -223,9 +251,6 @@ def main():
     frame_bufs = ([frame_buf] + [torch.zeros_like(frame_buf) if overlap else frame_buf for _ in range(L - 1)]
                   if rank == 0 else [None] * L)
 
-    def finish_gather():
-        """(kept for the call sites: the gather is stream-ordered inside rt_render)"""
-
     host_update = []                                       # (update_ms, part of it waiting on the GPU) per call
 
     def step(frame, sync=True, keep=False):
@@ -251,7 +276,6 @@ def main():
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(args.warmup + k, sync=False, keep=True)      # counters were zeroed by collect()
-    finish_gather()
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()
@@ -278,7 +302,6 @@ def main():
     for k in range(20):
         t1 = time.perf_counter()
         step(args.warmup + args.steps + k, sync=False)    # enqueue, then wait for the whole device
-        finish_gather()
         torch.cuda.synchronize()
         lat.append((time.perf_counter() - t1) * 1e3)
     _, serial_ms = r.collect()
@@ -298,9 +321,11 @@ def main():
         bytes_launch = algorithmic_bytes(cst)
         achieved = bytes_launch / (serial_kernel_ms * 1e-3) / 1e9
         kname = ("render_persistent_kernel" if args.kernel else "render_kernel") + ("<exact>" if args.exact else "<fast>")
-        traffic = load_traffic(kname)
+        tag = pmc_tag(args)
+        traffic, traffic_src, traffic_why = load_traffic(tag)
         hbm_frac = traffic / (serial_kernel_ms * 1e-3) / (HBM_PEAK_GBS * 1e9) if traffic else None
-        bound = ("latency" if hbm_frac < LATENCY_BOUND_FRAC else "hbm") if hbm_frac is not None else "hbm"
+        # what the counters say limits the kernel (null without a PMC summary of this exact workload)
+        limiter = ("latency" if hbm_frac < LATENCY_BOUND_FRAC else "hbm") if hbm_frac is not None else None
         value = rays / elapsed / 1e6
         out = {
             "metric": METRIC,
@@ -351,7 +376,8 @@ def main():
             "kernel_ms": round(serial_kernel_ms, 4),
             "kernel_ms_overlapped": round(avg_kernel_ms, 4),
             "roofline": {
-                "bound": bound,
+                "bound": "hbm",                                   # the roof `achieved` is priced against
+                "limiter": limiter,
                 "achieved": round(achieved, 2),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -360,6 +386,9 @@ def main():
                 "frac_throughput": (round(bytes_launch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
                                     if n == 1 and not shard else None),
                 "traffic": traffic,
+                "traffic_source": traffic_src,
+                "traffic_note": traffic_why,
+                "lib_sha16": tag["lib_sha16"],
                 "hbm_frac_measured": round(hbm_frac, 5) if hbm_frac is not None else None,
                 "kernel": kname,
                 "timing": "mean HIP-event duration of 20 serialised launches (kernel_ms)",

@@ -369,7 +369,8 @@ rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
  *               last launch used (band b's items start at 4 x its first unit: unit << 4 | piece << 2 | log2 pieces);
  *   "instances": RT_BUILD_LBVH or "gpu_tlas": 45 floats per instance, the records the GPU computed for the current frame
  *               (instances.hip): inverse, forward and inverse-transpose rows 1-3 (12 each), transformed box
- *               {xmin,xmax,ymin,ymax,zmin,zmax}, transformed centroid;
+ *               {xmin,xmax,ymin,ymax,zmin,zmax} (all +inf for a record kept out of the TLAS: a member of an
+ *               intact instance group, option "group"), transformed centroid;
  *   "blas_pairs", "blas_quads", "blas_roots": RT_BUILD_LBVH: the GPU-built forest as NodePair / NodeQuad /
  *               TreeRoot records (csrc/layout.hpp; quad q is the 4-wide node rooted at pair q);
  *   "leaf_prims": 1 u32 per leaf-ordered triangle slot: the caller's triangle index stored there (each

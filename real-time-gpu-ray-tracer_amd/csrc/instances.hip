@@ -53,8 +53,15 @@ __global__ __launch_bounds__(256) void instance_update_kernel(const InstParams *
     // the local box exactly as the host holds it (already volume-expanded): from_points would not move it
     hm::Box lb;
     for (int a = 0; a < 3; a++) lb.r[a] = hm::Range{P.box[2 * a], P.box[2 * a + 1]};
-    hm::transform_box(lb, fwd).store(tbox + 6 * (size_t)i);
     const hm::V3 tc = hm::apply_point(fwd, hm::V3{P.centroid[0], P.centroid[1], P.centroid[2]});
+    if (P.pad[0] != 0.0f) {       // inactive record (an intact group's member, a broken group): kept out of the TLAS
+        const float inf = __builtin_huge_valf();
+#pragma unroll
+        for (int k = 0; k < 6; k++) tbox[6 * (size_t)i + k] = inf;
+        tcent[i] = make_float4(tc.x, tc.y, tc.z, 1.0f);
+        return;
+    }
+    hm::transform_box(lb, fwd).store(tbox + 6 * (size_t)i);
     tcent[i] = make_float4(tc.x, tc.y, tc.z, 0.0f);
 }
 

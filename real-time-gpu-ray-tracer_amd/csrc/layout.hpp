@@ -126,7 +126,7 @@ struct alignas(16) InstParams {     // 96 B
     float shift[3], cos[3], sin[3], scale[3];   // Instance::updateTransformArguments arguments (cos / sin: host libm)
     float box[6];                   // local box {xmin,xmax,ymin,ymax,zmin,zmax} (volume-expanded, as the host holds it)
     float centroid[3];              // local centroid
-    float pad[3];
+    float pad[3];                   // pad[0] != 0: inactive record (kept out of the GPU TLAS, option "group")
 };
 static_assert(sizeof(InstParams) == 96, "InstParams must be 96 B");
 struct alignas(16) InstDelta {      // 112 B

@@ -152,7 +152,8 @@ __global__ void prep_blas_kernel(const LbvhSeg *segs, const uint32_t *seg_of, ui
 }
 
 // Centroid bounds per segment: a wave whose 64 items share one segment reduces in registers and
-// issues 6 atomics; mixed waves (segment boundaries) fall back to per-lane atomics.
+// issues 6 atomics; mixed waves (segment boundaries) fall back to per-lane atomics.  Inactive TLAS items
+// (centroid w != 0, set_items) are left out.
 __global__ void bounds_kernel(const uint32_t *seg_of, const float4 *cent, uint32_t n, uint32_t *bounds) {
     const uint32_t it = blockIdx.x * BLOCK + threadIdx.x;
     const bool valid = it < n;
@@ -160,9 +161,12 @@ __global__ void bounds_kernel(const uint32_t *seg_of, const float4 *cent, uint32
     float4 c = valid ? cent[it] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const uint32_t seg0 = __builtin_amdgcn_readfirstlane(seg);
     const bool uniform = __all(seg == seg0);
+    const bool live = valid && c.w == 0.0f;
     if (uniform) {
-        if (seg0 == NONE) return;
-        float lo[3] = {c.x, c.y, c.z}, hi[3] = {c.x, c.y, c.z};
+        if (seg0 == NONE || !__any(live)) return;
+        const float inf = __builtin_huge_valf();
+        float lo[3] = {live ? c.x : inf, live ? c.y : inf, live ? c.z : inf};
+        float hi[3] = {live ? c.x : -inf, live ? c.y : -inf, live ? c.z : -inf};
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
 #pragma unroll
@@ -180,7 +184,7 @@ __global__ void bounds_kernel(const uint32_t *seg_of, const float4 *cent, uint32
         }
         return;
     }
-    if (!valid) return;
+    if (!live) return;
     const float v[3] = {c.x, c.y, c.z};
 #pragma unroll
     for (int a = 0; a < 3; a++) {
@@ -200,6 +204,11 @@ __global__ void morton_kernel(const uint32_t *seg_of, const float4 *cent, uint32
     if (it >= n) return;
     const uint32_t seg = seg_of[it];
     const float4 c = cent[it];
+    if (c.w != 0.0f) {                           // inactive item: behind every active one (no class bits reach ~0)
+        keys[it] = ((unsigned long long)seg << 32) | 0xFFFFFFFFull;
+        vals[it] = it;
+        return;
+    }
     const uint32_t *B = bounds + 6 * seg;
     const uint32_t x = quant10(c.x, o2f(B[0]), o2f(B[1]));
     const uint32_t y = quant10(c.y, o2f(B[2]), o2f(B[3]));
@@ -449,7 +458,7 @@ __device__ __forceinline__ uint32_t material_slot(uint32_t type, uint32_t index,
 }
 
 __global__ void gather_blas_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals, uint32_t n,
-                                   RawPrimsGPU raw, PrimOutGPU out) {
+                                   RawPrimsGPU raw, PrimOutGPU out, const uint32_t *members) {
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
     if (p >= n) return;
     const LbvhSeg S = segs[seg_of_sorted(keys, p)];
@@ -473,6 +482,15 @@ __global__ void gather_blas_kernel(const LbvhSeg *segs, const unsigned long long
         C.material = material_slot(t.material_type, t.material_index, raw.rough_count);
         C.orig_index = prim;
         C.pad = 0;
+        if (S.member_count) {             // a group's BLAS: the member instance holding `prim`, + 1
+            const uint32_t *M = members + 2 * (size_t)S.member_base;
+            uint32_t lo = 0, hi = S.member_count;          // last member whose first primitive <= prim
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) / 2;
+                if (M[2 * mid] <= prim) lo = mid; else hi = mid;
+            }
+            C.pad = M[2 * lo + 1] + 1u;
+        }
         out.tri_hot[slot] = H;
         out.tri_cold[slot] = C;
     } else if (S.ptype == RT_PRIM_SPHERE) {
@@ -617,7 +635,7 @@ static void dfree(T *&p) {
 }
 
 void LbvhBuilder::release() {
-    dfree(segs_); dfree(seg_of_); dfree(own_box_); dfree(own_cent_); dfree(bounds_);
+    dfree(segs_); dfree(seg_of_); dfree(members_); dfree(own_box_); dfree(own_cent_); dfree(bounds_);
     dfree(k0_); dfree(k1_); dfree(v0_); dfree(v1_); dfree(child_); dfree(parent_); dfree(parent_leaf_);
     dfree(range_); dfree(flag_); dfree(height_); dfree(nbox_); dfree(kept_); dfree(pidx_); dfree(front_);
     if (tmp_) (void)hipFree(tmp_);
@@ -676,6 +694,14 @@ hipError_t LbvhBuilder::prep_blas_items(const RawPrimsGPU &raw, hipStream_t stre
     return hipGetLastError();
 }
 
+hipError_t LbvhBuilder::set_members(const std::vector<uint32_t> &pairs, hipStream_t stream) {
+    dfree(members_);
+    if (pairs.empty()) return hipSuccess;
+    LB_TRY(dalloc(members_, pairs.size()));
+    LB_TRY(hipMemcpyAsync(members_, pairs.data(), pairs.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+    return hipStreamSynchronize(stream);            // `pairs` (host) must outlive the copy
+}
+
 hipError_t LbvhBuilder::set_items(const float *boxes, const float4 *centroids) {
     box_ = const_cast<float *>(boxes);
     cent_ = const_cast<float4 *>(centroids);
@@ -715,7 +741,7 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
 
 hipError_t LbvhBuilder::gather_blas(const RawPrimsGPU &raw, const PrimOutGPU &out, hipStream_t stream) {
     hipLaunchKernelGGL(gather_blas_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, n_items_,
-                       raw, out);
+                       raw, out, members_);
     return hipGetLastError();
 }
 

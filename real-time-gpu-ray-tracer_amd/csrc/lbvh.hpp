@@ -36,6 +36,9 @@ struct LbvhSeg {            // one tree of the forest
     uint32_t node_base;     // first Karras interior node = item_base - segment index
     uint32_t leaf_cap;      // subtrees of <= leaf_cap items become one leaf (<= 4)
     uint32_t blas;          // 1: BLAS-level refs
+    // an instance group's merged BLAS (option "group"): its members' entries in the builder's member table
+    // ({first caller primitive, caller instance}, ascending), so a leaf slot records the instance it came from
+    uint32_t member_base, member_count;
 };
 
 // Raw caller primitives in HBM (the builder recomputes boxes, centroids and the leaf-ordered hot /
@@ -70,8 +73,13 @@ public:
 
     // BLAS items: boxes / centroids of the segments' primitives (reference box semantics).
     hipError_t prep_blas_items(const RawPrimsGPU &raw, hipStream_t stream);
-    // TLAS items: caller-provided boxes (6 floats per item) and centroids (4 floats per item).
+    // TLAS items: caller-provided boxes (6 floats per item) and centroids (4 floats per item).  An item whose
+    // centroid has w != 0 is inactive (an instance group's member while the group is one item, or a broken
+    // group): it is kept out of the centroid bounds and sorted behind every active item (its box must be all
+    // +inf, which no slab test accepts), so the active items form the tree's first subtree.
     hipError_t set_items(const float *boxes, const float4 *centroids);
+    // Member tables of group segments (LbvhSeg::member_base / member_count): {first primitive, instance} pairs.
+    hipError_t set_members(const std::vector<uint32_t> &pairs, hipStream_t stream);
 
     // Builds every segment: pairs written from index 0 of `pairs` (capacity max_pairs()),
     // roots[s] receives segment s's root; `pair_count` (device, may be null) the pairs written.
@@ -90,6 +98,7 @@ private:
     uint32_t n_items_ = 0, n_segs_ = 0, seg_bits_ = 0, max_count_ = 0;
     LbvhSeg *segs_ = nullptr;
     uint32_t *seg_of_ = nullptr;          // item -> segment
+    uint32_t *members_ = nullptr;         // group segments: {first primitive, instance} pairs
     float *box_ = nullptr;                // 6 floats per item (owned or caller's)
 public:
     bool size_classes_ = false;           // TLAS: size class above the Morton code (morton_kernel)

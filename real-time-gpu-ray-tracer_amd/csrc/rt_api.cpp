@@ -307,8 +307,15 @@ struct rt_scene {
     DevBuf<rt_triangle> raw_tris;
     DevBuf<rt_sphere> raw_sph;
     DevBuf<rt_parallelogram> raw_quad;
-    DevBuf<TreeRoot> blas_roots;        // per unique BLAS
-    DevBuf<uint32_t> inst_blas;         // instance -> BLAS
+    DevBuf<TreeRoot> blas_roots;        // per segment the builder holds (seg_of_blas)
+    DevBuf<uint32_t> inst_blas;         // instance record (instances, then groups) -> segment
+    // RT_BUILD_LBVH + option "group": every unique BLAS's segment (index = BLAS index; the groups' merged BLASes
+    // follow the own ones), BLAS -> segment the builder currently holds (NONE: not built), and per group whether
+    // it was intact at that setup.  A group's BLAS and its members' BLASes share one leaf-slot range, and only
+    // one of them is built: the group's while it is intact, the members' once it breaks (lbvh_segments)
+    std::vector<LbvhSeg> lbvh_segs;
+    std::vector<uint32_t> seg_of_blas;
+    std::vector<uint8_t> lbvh_intact;
     DevBuf<uint32_t> gpu_counts;        // [0] BLAS pairs written, [1] TLAS pairs written (last frame)
     bool rebuild_blas = false;          // option "rebuild": rebuild every BLAS each frame
     bool blas_dirty = false;            // rt_scene_update_triangles since the last BLAS build
@@ -464,6 +471,9 @@ void store_rows(float *dst, const hm::Mat &m) {   // rows 1..3, cols 1..4
 }
 
 rt_status gpu_build_blas(rt_scene *s);
+bool record_inactive(const rt_scene *s, size_t i);
+const InstState &record_state(const rt_scene *s, size_t i);
+rt_status lbvh_sync_groups(rt_scene *s);
 
 // Wait for a stream / an event of the scene.  With a communicator attached the wait polls (comm_wait.hpp):
 // an asynchronous RCCL error or the rt_comm_set_timeout deadline aborts the communicators and fails with
@@ -542,14 +552,17 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
     InstHot *hot = reinterpret_cast<InstHot *>(st + s->off_hot);
     InstCold *cold = reinterpret_cast<InstCold *>(st + s->off_cold);
     if (s->gpu_tlas()) {
+        RT_TRY(lbvh_sync_groups(s));                  // option "group": which records are TLAS items
         s->block_by_slot[b] = false;                  // until the slot-order copy below
-        // only the changed instances cross PCIe: (index, shift, cos / sin of the angles, scale, local box)
+        // records: the instances, then (LBVH, option "group") the groups as instances of their merged BLAS
+        const size_t nrec = s->inst.size() + s->groups.size();
+        // only the changed records cross PCIe: (index, shift, cos / sin of the angles, scale, local box, inactive)
         InstDelta *dl = reinterpret_cast<InstDelta *>(st + s->off_delta);
         uint32_t nd = 0;
-        for (size_t i = 0; i < s->inst.size(); i++) {
+        for (size_t i = 0; i < nrec; i++) {
             if (!s->inst_dirty[i]) continue;
             s->inst_dirty[i] = 0;
-            const InstState &in = s->inst[i];
+            const InstState &in = record_state(s, i);
             InstDelta &d = dl[nd++];
             std::memset(&d, 0, sizeof d);
             d.index = (uint32_t)i;
@@ -562,6 +575,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
                 d.p.centroid[a] = in.centroid[a];
             }
             in.box.store(d.p.box);
+            d.p.pad[0] = record_inactive(s, i) ? 1.0f : 0.0f;
         }
         uint8_t *fd = s->frame_dev[b];
         HIP_TRY(hipStreamWaitEvent(s->stream, s->r_used[b], 0));
@@ -570,14 +584,14 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
                                           s->stream));
         // Instance::updateTransformArguments for every instance, on the GPU (instances.hip)
         HIP_TRY(launch_instance_update(reinterpret_cast<const InstDelta *>(fd + s->off_delta), nd, s->inst_params.p,
-                                       (uint32_t)s->inst.size(), reinterpret_cast<InstHot *>(fd + s->off_hot),
+                                       (uint32_t)nrec, reinterpret_cast<InstHot *>(fd + s->off_hot),
                                        reinterpret_cast<InstCold *>(fd + s->off_cold), reinterpret_cast<float *>(fd + s->off_tbox),
                                        reinterpret_cast<float4 *>(fd + s->off_tcent), s->stream));
         if (s->blas_builder && (s->rebuild_blas || s->blas_dirty)) {    // GPU-built BLASes only
             const rt_status bs = gpu_build_blas(s);
             if (bs != RT_OK) return bs;
         }
-        const uint32_t n = (uint32_t)s->inst.size();
+        const uint32_t n = (uint32_t)nrec;
         HIP_TRY(launch_patch_inst_roots(reinterpret_cast<InstHot *>(fd + s->off_hot), s->inst_blas.p, s->blas_roots.p,
                                         s->blas_wide_refs.p, n,
                                         s->stream));
@@ -686,7 +700,7 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.sph_hot = s->sph_hot.p; g.sph_cold = s->sph_cold.p;
     g.quad_hot = s->quad_hot.p; g.quad_cold = s->quad_cold.p;
     g.materials = s->materials.p;
-    g.instance_count = s->gpu_tlas() ? (uint32_t)s->inst.size() : s->frame_items[b];   // instance records
+    g.instance_count = s->gpu_tlas() ? (uint32_t)(s->inst.size() + s->groups.size()) : s->frame_items[b];   // records
     g.rough_count = (uint32_t)s->roughs.size();
     g.material_count = (uint32_t)(s->materials.n / 4);
     // option "lds_scene": the quads the frame's TLAS refs can index (host-built: this frame's quad count;
@@ -739,6 +753,95 @@ rt_status alloc_buf(DevBuf<T> &buf, size_t n) {
     HIP_TRY(hipMalloc(&buf.p, (n ? n : 1) * sizeof(T)));
     buf.n = n;
     return RT_OK;
+}
+
+// RT_BUILD_LBVH + option "group": record i (instances, then groups) kept out of the GPU TLAS — a member of an
+// intact group (the group is the TLAS item) or a broken group (its members are)
+bool record_inactive(const rt_scene *s, size_t i) {
+    if (s->build_mode != RT_BUILD_LBVH || s->groups.empty()) return false;
+    if (i < s->inst.size()) return s->group_of[i] && s->lbvh_intact[s->group_of[i] - 1];
+    return !s->lbvh_intact[i - s->inst.size()];
+}
+const InstState &record_state(const rt_scene *s, size_t i) {
+    return i < s->inst.size() ? s->inst[i] : s->groups[i - s->inst.size()].st;
+}
+// a group is one TLAS item while it is valid (no rt_scene_update_instances on a member) and every member still
+// has the group's transform (SAH: frame_update; LBVH: lbvh_sync_groups)
+bool group_intact(const rt_scene *s, size_t g) {
+    const InstGroup &G = s->groups[g];
+    bool ok = G.valid;
+    for (size_t k = 0; ok && k < G.members.size(); k++)
+        ok = std::memcmp(&s->inst[G.members[k]].x, &G.st.x, sizeof(rt_xform)) == 0;
+    return ok;
+}
+
+// RT_BUILD_LBVH: (re)configure the builder's segments for the current group states: the segments of the BLASes
+// in use (item ranges re-tiled in BLAS order), the group member tables, the BLAS arrays sized for them, the
+// record -> segment map.  Called at the build and when a group breaks or re-forms (the device is drained).
+rt_status lbvh_segments(rt_scene *s) {
+    constexpr uint32_t NONE = 0xFFFFFFFFu;
+    std::vector<uint8_t> use(s->blas.size(), 1);
+    for (size_t g = 0; g < s->groups.size(); g++) {
+        if (s->lbvh_intact[g]) for (uint32_t m : s->groups[g].members) use[s->inst[m].blas] = 0;
+        else use[s->groups[g].st.blas] = 0;
+    }
+    std::vector<LbvhSeg> segs;
+    std::vector<uint32_t> members;
+    s->seg_of_blas.assign(s->blas.size(), NONE);
+    uint32_t item = 0;
+    for (size_t b = 0; b < s->blas.size(); b++) {
+        if (!use[b]) continue;
+        LbvhSeg sg = s->lbvh_segs[b];
+        sg.item_base = item;
+        sg.node_base = item - (uint32_t)segs.size();
+        if (!s->blas[b].members.empty()) {
+            sg.member_base = (uint32_t)(members.size() / 2);
+            sg.member_count = (uint32_t)s->blas[b].members.size();
+            for (const auto &m : s->blas[b].members) { members.push_back(m[0]); members.push_back(m[2]); }
+        }
+        s->seg_of_blas[b] = (uint32_t)segs.size();
+        segs.push_back(sg);
+        item += sg.count;
+    }
+    if (!s->blas_builder) s->blas_builder = new LbvhBuilder();
+    HIP_TRY(s->blas_builder->init(segs, s->stream));
+    HIP_TRY(s->blas_builder->set_members(members, s->stream));
+    rt_status st;
+    if ((st = alloc_buf(s->blas_pairs, s->blas_builder->max_pairs())) != RT_OK) return st;
+    if ((st = alloc_buf(s->blas_quads, s->blas_builder->max_pairs())) != RT_OK) return st;   // quad q = rooted at pair q
+    if ((st = alloc_buf(s->blas_roots, segs.size())) != RT_OK) return st;
+    const size_t n = s->inst.size() + s->groups.size();
+    std::vector<uint32_t> ib(n);
+    for (size_t i = 0; i < n; i++) {
+        uint32_t sg = s->seg_of_blas[record_state(s, i).blas];
+        if (sg == NONE && i < s->inst.size() && s->group_of[i]) sg = s->seg_of_blas[s->groups[s->group_of[i] - 1].st.blas];
+        ib[i] = sg == NONE ? 0u : sg;                      // an inactive record's root is never entered
+    }
+    if ((st = upload(s->inst_blas, ib)) != RT_OK) return st;
+    s->blas_dirty = true;
+    return RT_OK;
+}
+
+// RT_BUILD_LBVH, per frame: a group that broke (a member moved, rt_scene_update_instances) or re-formed switches
+// the BLASes built and the records in the TLAS (their inactive flags travel with the next instance deltas)
+rt_status lbvh_sync_groups(rt_scene *s) {
+    if (s->build_mode != RT_BUILD_LBVH || s->groups.empty()) return RT_OK;
+    bool changed = false;
+    std::vector<uint8_t> now(s->groups.size());
+    for (size_t g = 0; g < s->groups.size(); g++) {
+        now[g] = group_intact(s, g) ? 1 : 0;
+        changed = changed || now[g] != s->lbvh_intact[g];
+    }
+    if (!changed) return RT_OK;
+    RT_TRY(drain(s));
+    for (size_t g = 0; g < s->groups.size(); g++) {
+        if (now[g] == s->lbvh_intact[g]) continue;
+        for (uint32_t m : s->groups[g].members) s->inst_dirty[m] = 1;
+        s->inst_dirty[s->inst.size() + g] = 1;
+    }
+    s->lbvh_intact = now;
+    s->spare.release();                                   // re-sized with the next double-buffered build
+    return lbvh_segments(s);
 }
 
 // RT_BUILD_LBVH: rebuild every BLAS on the GPU (prep -> Morton -> sort -> Karras -> boxes -> pairs ->
@@ -794,7 +897,8 @@ rt_status gpu_build_blas(rt_scene *s) {
 }
 
 // RT_BUILD_LBVH: upload the raw primitives, allocate the leaf-ordered arrays, build every BLAS once.
-rt_status gpu_setup_blas(rt_scene *s, const std::vector<LbvhSeg> &segs, const uint32_t *slot_count) {
+rt_status gpu_setup_blas(rt_scene *s, const uint32_t *slot_count) {
+    const std::vector<LbvhSeg> &segs = s->lbvh_segs;
     bool ok = true;                                  // the host builds check the same materials
     for (const LbvhSeg &g : segs)
         for (uint32_t k = 0; k < g.count; k++) {
@@ -815,15 +919,11 @@ rt_status gpu_setup_blas(rt_scene *s, const std::vector<LbvhSeg> &segs, const ui
     if ((st = alloc_buf(s->quad_hot, slot_count[RT_PRIM_PARALLELOGRAM])) != RT_OK) return st;
     if ((st = alloc_buf(s->quad_cold, slot_count[RT_PRIM_PARALLELOGRAM])) != RT_OK) return st;
     delete s->blas_builder;
-    s->blas_builder = new LbvhBuilder();
-    HIP_TRY(s->blas_builder->init(segs, s->stream));
-    if ((st = alloc_buf(s->blas_pairs, s->blas_builder->max_pairs())) != RT_OK) return st;
-    if ((st = alloc_buf(s->blas_quads, s->blas_builder->max_pairs())) != RT_OK) return st;   // quad q = rooted at pair q
-    if ((st = alloc_buf(s->blas_roots, segs.size())) != RT_OK) return st;
+    s->blas_builder = nullptr;
+    s->lbvh_intact.assign(s->groups.size(), 1);       // members start with the group's transform (frame 0 re-checks)
+    s->spare.release();
+    if ((st = lbvh_segments(s)) != RT_OK) return st;
     if ((st = alloc_buf(s->gpu_counts, 2)) != RT_OK) return st;
-    std::vector<uint32_t> ib(s->inst.size());
-    for (size_t i = 0; i < ib.size(); i++) ib[i] = s->inst[i].blas;
-    if ((st = upload(s->inst_blas, ib)) != RT_OK) return st;
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
     if (!s->r_done) s->r_done = s->ev_render_done;
     for (int q = 0; q < rt_scene::NLANE; q++) {       // "blas_double": every trace records its lane's event from now on
@@ -834,12 +934,12 @@ rt_status gpu_setup_blas(rt_scene *s, const std::vector<LbvhSeg> &segs, const ui
     if ((st = gpu_build_blas(s)) != RT_OK) return st;
     // one-time readback for introspection (rt_scene_get_info)
     uint32_t pairs = 0;
-    std::vector<TreeRoot> roots(segs.size());
+    std::vector<TreeRoot> roots(s->blas_roots.n);
     RT_TRY(drain(s));
     HIP_TRY(hipMemcpy(&pairs, s->gpu_counts.p, sizeof pairs, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(roots.data(), s->blas_roots.p, roots.size() * sizeof(TreeRoot), hipMemcpyDeviceToHost));
     s->blas_pair_count = pairs;
-    s->blas_leaf_count = pairs + segs.size();        // binary trees: leaves = interior nodes + 1
+    s->blas_leaf_count = pairs + roots.size();       // binary trees: leaves = interior nodes + 1
     for (const TreeRoot &r : roots) s->max_blas_height = std::max(s->max_blas_height, r.height);
     return RT_OK;
 }
@@ -924,7 +1024,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     // The reference's map stores the instance index instead of the BLAS index (RenderPin.cu:151);
     // the BLAS index is stored here (identical whenever the reference's demo order is used).
     std::vector<std::pair<uint64_t, uint32_t>> seen;
-    std::vector<LbvhSeg> segs;                  // RT_BUILD_LBVH: one tree per unique BLAS
+    std::vector<LbvhSeg> &segs = s->lbvh_segs;  // RT_BUILD_LBVH: one tree per unique BLAS
+    segs.clear();
     uint64_t item_total = 0;
     uint32_t pair_base = 0, quad_base = 0;
     uint32_t slot_base[3] = {0, 0, 0};
@@ -994,7 +1095,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     }
     s->blas_own = s->blas.size();
     s->group_of.assign(s->inst.size(), 0u);
-    if (mode == RT_BUILD_SAH && s->group_inst && !s->gpu_tlas()) {
+    if (s->group_inst && ((mode == RT_BUILD_SAH && !s->gpu_tlas()) || mode == RT_BUILD_LBVH)) {
         // option "group": triangle instances with bit-identical transforms and a BLAS of their own
         std::vector<uint32_t> users(s->blas.size(), 0u);
         for (const InstState &in : s->inst) users[in.blas]++;
@@ -1015,6 +1116,14 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             bool disjoint = true;          // every triangle of the group belongs to exactly one member
             for (size_t k = 1; k < ranges.size(); k++)
                 disjoint = disjoint && ranges[k][0] >= ranges[k - 1][0] + ranges[k - 1][1];
+            if (mode == RT_BUILD_LBVH) {
+                // the group's LBVH segment is one contiguous primitive range and reuses its members' leaf slots:
+                // their triangles back to back, their slot ranges too (the reference's VTK particles, C5)
+                for (size_t k = 1; k < ranges.size() && disjoint; k++) {
+                    const BlasHost &a = s->blas[s->inst[ranges[k - 1][2]].blas], &c = s->blas[s->inst[ranges[k][2]].blas];
+                    disjoint = ranges[k][0] == ranges[k - 1][0] + ranges[k - 1][1] && c.slot_base == a.slot_base + ranges[k - 1][1];
+                }
+            }
             if (!disjoint) continue;
             const uint32_t gi = (uint32_t)s->groups.size();
             uint64_t total = 0;
@@ -1029,7 +1138,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
                 bh.members.push_back({m.pindex, m.pcount, g.members[k]});
                 s->group_of[g.members[k]] = gi + 1;
             }
-            if ((uint64_t)slot_base[RT_PRIM_TRIANGLE] + total >= MAX_LEAF_SLOTS)
+            if (mode != RT_BUILD_LBVH && (uint64_t)slot_base[RT_PRIM_TRIANGLE] + total >= MAX_LEAF_SLOTS)
                 return fail(RT_ERR_UNSUPPORTED, "too many primitives of one type (2^26 leaf slots)");
             g.st.ptype = RT_PRIM_TRIANGLE;
             g.st.pindex = 0;
@@ -1037,6 +1146,19 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             g.st.centroid = hm::v3((float)(c[0] / g.members.size()), (float)(c[1] / g.members.size()),
                                    (float)(c[2] / g.members.size()));
             g.st.x = s->inst_desc[g.members[0]].xform;
+            if (mode == RT_BUILD_LBVH) {
+                // one more segment over the members' triangles, in their leaf slots (lbvh_segments builds either
+                // it or the members' own segments); item / node bases are assigned there
+                bh.slot_base = s->blas[s->inst[ranges[0][2]].blas].slot_base;
+                bh.pair_base = 0;
+                segs.push_back(LbvhSeg{0u, (uint32_t)total, bh.slot_base, ranges[0][0], RT_PRIM_TRIANGLE, 0u,
+                                       LBVH_BLAS_LEAF_CAP, 1u, 0u, 0u});
+                std::sort(bh.members.begin(), bh.members.end());
+                g.st.blas = (uint32_t)s->blas.size();
+                s->blas.push_back(std::move(bh));
+                s->groups.push_back(std::move(g));
+                continue;
+            }
             std::vector<BuildItem> items;
             items.reserve(total);
             for (const auto &mr : bh.members)
@@ -1068,7 +1190,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     if (!s->r_done) s->r_done = s->ev_render_done;
     for (bool &v : s->sched_valid) v = false;
     if (mode == RT_BUILD_LBVH) {
-        if ((st = gpu_setup_blas(s, segs, slot_base)) != RT_OK) return st;
+        if ((st = gpu_setup_blas(s, slot_base)) != RT_OK) return st;
     } else {
     // leaf-ordered primitive arrays + node pairs
     std::vector<NodePair> pairs;
@@ -1852,7 +1974,7 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
         RT_TRY(drain(s));
         const void *from = k == "blas_pairs" ? (const void *)s->blas_pairs.p
                                              : (k == "blas_quads" ? (const void *)s->blas_quads.p : (const void *)s->blas_roots.p);
-        *bytes = k == "blas_roots" ? s->blas.size() * sizeof(TreeRoot)
+        *bytes = k == "blas_roots" ? s->blas_roots.n * sizeof(TreeRoot)
                                    : s->blas_pair_count * (k == "blas_pairs" ? sizeof(NodePair) : sizeof(NodeQuad));
         if (capacity && *bytes) HIP_TRY(hipMemcpy(dst, from, std::min(capacity, *bytes), hipMemcpyDeviceToHost));
         return RT_OK;
@@ -1956,6 +2078,17 @@ rt_status rt_scene_update_triangles(rt_scene *s, size_t first, size_t count, con
                                      : hm::v3((float)(c[0] / in.pcount), (float)(c[1] / in.pcount), (float)(c[2] / in.pcount));
         instance_update(in, in.x);
         if (s->gpu_tlas()) s->inst_dirty[i] = 1;     // the GPU copy of its local box
+    }
+    for (size_t g = 0; g < s->groups.size(); g++) {   // option "group" (LBVH): the union of the members' boxes
+        InstGroup &G = s->groups[g];
+        double c[3] = {0, 0, 0};
+        for (size_t k = 0; k < G.members.size(); k++) {
+            const InstState &m = s->inst[G.members[k]];
+            G.st.box = k ? hm::Box::merge(G.st.box, m.box) : m.box;
+            for (int a = 0; a < 3; a++) c[a] += m.centroid[a];
+        }
+        G.st.centroid = hm::v3((float)(c[0] / G.members.size()), (float)(c[1] / G.members.size()), (float)(c[2] / G.members.size()));
+        if (s->gpu_tlas()) s->inst_dirty[s->inst.size() + g] = 1;
     }
     s->blas_dirty = true;
     return RT_OK;
@@ -2084,8 +2217,10 @@ rt_status rt_scene_export_blas(const rt_scene *s, uint32_t b, float *boxes, uint
         HIP_TRY(hipStreamSynchronize(s->stream));
         std::vector<NodePair> pairs;
         std::vector<TreeRoot> roots;
+        if (s->seg_of_blas[b] == 0xFFFFFFFFu)
+            return fail(RT_ERR_STATE, "this BLAS is not built: its instance group is one BLAS (option \"group\")");
         HIP_TRY(read_back(pairs, s->blas_pairs.p, s->blas_pair_count));
-        HIP_TRY(read_back(roots, s->blas_roots.p, s->blas.size()));
+        HIP_TRY(read_back(roots, s->blas_roots.p, s->blas_roots.n));
         const uint32_t type = s->blas[b].type;
         std::vector<uint32_t> orig;
         if (type == RT_PRIM_TRIANGLE) {
@@ -2098,7 +2233,7 @@ rt_status rt_scene_export_blas(const rt_scene *s, uint32_t b, float *boxes, uint
                               type == RT_PRIM_SPHERE ? s->sph_cold.n : s->quad_cold.n));
             for (const PrimCold &x : c) orig.push_back(x.orig_index);
         }
-        gpu_tree = tree_from_pairs(roots[b], pairs, 0, orig);
+        gpu_tree = tree_from_pairs(roots[s->seg_of_blas[b]], pairs, 0, orig);
     }
     const Tree &t = s->build_mode == RT_BUILD_LBVH ? gpu_tree : s->blas[b].tree;
     if (n_nodes) *n_nodes = (uint32_t)t.nodes.size();
@@ -2121,8 +2256,9 @@ rt_status rt_scene_export_tlas(const rt_scene *s, float *boxes, uint32_t *ci, ui
         std::vector<NodePair> pairs;
         std::vector<uint32_t> slots;
         HIP_TRY(hipMemcpy(&root, fd + s->off_root, sizeof root, hipMemcpyDeviceToHost));
-        HIP_TRY(read_back(pairs, reinterpret_cast<const NodePair *>(fd + s->off_pairs), s->inst.size()));
-        HIP_TRY(read_back(slots, reinterpret_cast<const uint32_t *>(fd + s->off_slots), s->inst.size()));
+        const size_t nrec = s->inst.size() + s->groups.size();
+        HIP_TRY(read_back(pairs, reinterpret_cast<const NodePair *>(fd + s->off_pairs), nrec));
+        HIP_TRY(read_back(slots, reinterpret_cast<const uint32_t *>(fd + s->off_slots), nrec));
         gpu_tree = tree_from_pairs(root, pairs, 0, slots);
     }
     const Tree &t = s->gpu_tlas() ? gpu_tree : s->tlas;

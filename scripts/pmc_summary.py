@@ -34,10 +34,25 @@ def load(dirs, kernel_sub):
 
 
 def main():
-    out, kernel_sub, dirs = sys.argv[1], sys.argv[2], sys.argv[3:]
+    argv = sys.argv[1:]
+    tag = cmd = None
+    if "--tag" in argv:
+        i = argv.index("--tag")
+        with open(argv[i + 1]) as f:
+            tag = json.load(f)                    # bench.py --print-pmc-tag: the workload these counters price
+        del argv[i:i + 2]
+    if "--cmd" in argv:
+        i = argv.index("--cmd")
+        cmd = argv[i + 1]
+        del argv[i:i + 2]
+    out, kernel_sub, dirs = argv[0], argv[1], argv[2:]
     avg, ndisp, names = load(dirs, kernel_sub)
     res = {"kernel": names[0] if names else kernel_sub, "kernels_matched": names, "counters_avg_per_dispatch": avg,
            "dispatches": ndisp, "source_dirs": dirs}
+    if tag is not None:
+        res["tag"] = tag
+    if cmd is not None:
+        res["command"] = cmd
     if "FETCH_SIZE" in avg and "WRITE_SIZE" in avg:
         res["fetch_bytes_per_launch_corrected"] = 2.0 * avg["FETCH_SIZE"] * 1024.0
         res["write_bytes_per_launch"] = avg["WRITE_SIZE"] * 1024.0

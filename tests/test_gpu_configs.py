@@ -124,14 +124,13 @@ def test_c5_lbvh_per_frame_rebuild(gpu_lib):
     info = r.info()
     assert info["sqrt_sample_count"] == 2                                # 8 requested -> 4 traced (RenderPin.cu:93)
     assert info["blas_count"] == 4 + P                                   # 2 spheres, quad, demo triangle + particles
-    # every triangle in exactly one leaf slot, inside its own BLAS's slot range: the demo triangle's
-    # BLAS comes first in instance order (slot 0), then one 1024-slot range per particle
+    # every triangle in exactly one leaf slot, inside its BLAS's slot range: the demo triangle's BLAS comes
+    # first in instance order (slot 0), then the particles' slots, which (option "group": all particles share
+    # the VTK transform) hold one LBVH over all their triangles
     orig = r.debug_read("leaf_prims").view(np.uint32)
     assert orig.shape == (n_tris,)
     assert orig[0] == n_tris - 1
-    per = orig[1:].reshape(P, 1024).astype(np.int64)
-    per.sort(axis=1)
-    assert np.array_equal(per, np.arange(P * 1024, dtype=np.int64).reshape(P, 1024))
+    assert np.array_equal(np.sort(orig[1:].astype(np.int64)), np.arange(P * 1024, dtype=np.int64))
     f0, _, _ = r.render(0)                                               # rebuild + trace
     f0b, _, _ = r.render(0)                                              # rebuilt again: same bytes
     assert np.array_equal(f0, f0b)

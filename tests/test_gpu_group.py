@@ -93,3 +93,86 @@ def test_broken_group_equals_ungrouped_scene(gpu_lib):
         assert np.array_equal(rg.render(frame)[0], r0.render(frame)[0]), frame
     for exact in (False, True):
         assert np.array_equal(rg.render(6, exact=exact)[0], r0.render(6, exact=exact)[0]), exact
+
+
+# ---- option "group" with the GPU builder (RT_BUILD_LBVH): one LBVH segment over the members' triangles, in
+# their leaf slots; members and the group are TLAS records, the inactive ones kept out of the GPU TLAS ----
+
+def _lbvh(s, group=1, **cam):
+    r = Renderer(s).set_option("group", group).build_acceleration_structure(0, mode="lbvh")
+    return r.configure_camera(cam.pop("W", 320), cam.pop("H", 180), **cam)
+
+
+def test_lbvh_group_tree_equals_restatement(gpu_lib):
+    """The group's BLAS is the LBVH of the members' triangles taken as one contiguous range: equal bit for bit to
+    the numpy restatement over the same primitives; a member's own BLAS is not built while the group holds."""
+    from lbvh_ref import lbvh_tree
+    from test_gpu_lbvh import prim_items
+    from rtamd import abi
+    P = 12
+    s = scenes.demo_with_particles(P)
+    r = _lbvh(s, W=64, H=64)
+    nb_own = r.info()["blas_count"]
+    assert nb_own == 4 + P
+    boxes, cents = prim_items(s, abi.TRIANGLE, 0, P * 1024)
+    nb, ci, refs = r.export_blas(nb_own)                  # the group's BLAS follows the own ones
+    wb, wci, wrefs = lbvh_tree(boxes, cents, 4)
+    assert np.array_equal(ci, wci) and np.array_equal(refs, wrefs) and np.array_equal(nb, wb)
+    with pytest.raises(abi.RtError):
+        r.export_blas(4)                                   # particle 0's own BLAS: not built
+    _, _, trefs = r.export_tlas()                         # every record is a TLAS leaf (inactive ones in a subtree
+    assert sorted(trefs.tolist()) == list(range(len(s.instances) + 1))   # no ray enters); the group is record n
+
+
+def test_lbvh_group_images_and_hits_match_oracle(gpu_lib):
+    from oracle.oracle import OracleScene
+    s = scenes.demo_with_particles(24)
+    r = _lbvh(s, ray_trace_depth=2)
+    o = OracleScene(s, build_seed=0)
+    o.camera(320, 180, ray_trace_depth=2)
+    for frame in (0, 7):
+        o.update(frame)
+        _, orgba, ocnt = o.render(threads=THREADS)
+        for exact in (False, True):
+            rgba, _, st = r.render(frame, exact=exact, count_work=True)
+            f, mx = frac_within(rgba, orgba)
+            assert f >= 0.999, (frame, exact, f, mx)
+            assert abs(st["rays"] - ocnt["rays"]) <= 0.001 * ocnt["rays"]
+    rays = _rays(20000, 6)
+    oh, _ = o.trace(rays)
+    h = r.trace_rays(rays)
+    same = (h["instance"] == oh["instance"]) & (h["pindex"] == oh["pindex"])
+    assert same.mean() >= 0.999, same.mean()
+
+
+@pytest.mark.parametrize("rebuild", [0, 1])
+def test_lbvh_broken_group_switches_to_members(gpu_lib, rebuild):
+    """A member moved by rt_scene_update_instances breaks the group for good: the builder switches to the
+    members' own BLASes (exportable again) and the frame matches a scene built without groups within the
+    FAST tolerance, with equal hits on >= 99.9 % of rays."""
+    from rtamd import abi
+    P = 16
+    s = scenes.demo_with_particles(P)
+    r = _lbvh(s, ray_trace_depth=2)
+    r0 = _lbvh(s, group=0, ray_trace_depth=2)
+    for x in (r, r0):
+        x.set_option("rebuild", rebuild)
+    first = len(s.instances) - P
+    moved = dict(s.instances[first + 3])
+    moved["shift"] = (0.3, 4.2, -0.1)
+    for x in (r, r0):
+        x.render(0)
+        x.update_instances(first + 3, [moved])
+    for frame in (1, 2):
+        a, _, sa = r.render(frame, count_work=True)
+        b, _, sb = r0.render(frame, count_work=True)
+        f, mx = frac_within(a, b)
+        assert f >= 0.9995, (frame, f, mx)
+        assert abs(sa["instance_visits"] - sb["instance_visits"]) <= 0.01 * sb["instance_visits"]
+    nb_own = r.info()["blas_count"]
+    r.export_blas(first)                                   # a member's own BLAS is built now
+    with pytest.raises(abi.RtError):
+        r.export_blas(nb_own)                              # the group's is not
+    rays = _rays(8000, 7)
+    ha, hb = r.trace_rays(rays), r0.trace_rays(rays)
+    assert ((ha["instance"] == hb["instance"]) & (ha["pindex"] == hb["pindex"])).mean() >= 0.999

@@ -65,7 +65,7 @@ def unique_blas(scene):
 
 def test_blas_trees_equal_restatement(gpu_lib):
     s = scenes.demo_with_particles(5)
-    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(64, 64)
+    r = Renderer(s).set_option("group", 0).build_acceleration_structure(0, mode="lbvh").configure_camera(64, 64)
     blas = unique_blas(s)
     assert r.info()["blas_count"] == len(blas)
     for b, (ptype, first, count) in enumerate(blas):
@@ -80,7 +80,7 @@ def test_blas_trees_equal_restatement(gpu_lib):
 
 def test_tlas_valid_every_frame(gpu_lib):
     s = scenes.demo_with_particles(12)
-    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(64, 64)
+    r = Renderer(s).set_option("group", 0).build_acceleration_structure(0, mode="lbvh").configure_camera(64, 64)
     n = len(s.instances)
     for frame in (0, 5, 37):
         r.update(frame)
@@ -187,7 +187,8 @@ def test_large_forest_c5_shape(gpu_lib):
     from oracle.oracle import OracleScene
     P = 1000
     s = scenes.demo_with_particles(P)
-    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(192, 108, ray_trace_depth=2)
+    r = Renderer(s).set_option("group", 0).build_acceleration_structure(0, mode="lbvh").configure_camera(
+        192, 108, ray_trace_depth=2)
     info = r.info()
     assert info["blas_count"] == 5 - 1 + P
     assert info["blas_leaves"] == info["blas_node_pairs"] + info["blas_count"]
