@@ -67,6 +67,8 @@ def parse():
                    help="N = 1: run the multi-GPU frame path anyway (a world-1 RCCL communicator: tiles + assemble)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--clock-warmup", type=float, default=0.5,
+                   help="seconds of untimed frames before the W warm-up steps (the GPU's clocks ramp up under load)")
     p.add_argument("--print-pmc-tag", action="store_true", help="print this run's PMC tag as JSON and exit (no GPU)")
     return p.parse_args()
 
@@ -253,17 +255,33 @@ def main():
 
     host_update = []                                       # (update_ms, part of it waiting on the GPU) per call
 
-    def step(frame, sync=True, keep=False):
+    def step(frame, sync=True, keep=False, one_stream=False):
         """One frame; sync=False pipelines it (host TLAS build of the next frame overlaps the GPU).
-        With "overlap", frame k runs on lanes[k % L] (its own trace -> gather -> assemble chain)."""
+        With "overlap", frame k runs on lanes[k % L] (its own trace -> gather -> assemble chain);
+        one_stream: every frame on the first lane's stream (launches serialised back to back)."""
         b = frame % L if overlap else 0
-        st = lanes[b].cuda_stream if overlap else stream
+        st = lanes[0 if one_stream else b].cuda_stream if overlap else stream
         fb = frame_bufs[b]
         t_call = time.perf_counter()
         _, _, sts = r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=fb.data_ptr() if fb is not None else None,
                              stream=st, sync=sync, keep_counters=keep, tiles=tiles)
         host_update.append((sts["update_ms"], sts["update_wait_ms"], (time.perf_counter() - t_call) * 1e3))
 
+    # clock warm-up: the GPU's clocks ramp up over the first ~0.1-0.5 s of load (measured: serialised C2 launches
+    # 395 -> ~265 us, C3 2.8 -> 1.6 ms over the first launches, profiles/r03_*); a real-time renderer runs in
+    # the steady state, so untimed frames are rendered for --clock-warmup seconds before the warm-up steps
+    t_cw = time.perf_counter()
+    k = 0
+    while args.clock_warmup > 0:
+        for _ in range(16):                                # chunks of 16 frames; ranks stop together (rank 0 decides)
+            step(k % 1000, sync=False)
+            k += 1
+        torch.cuda.synchronize()
+        done = torch.tensor([1.0 if time.perf_counter() - t_cw >= args.clock_warmup else 0.0], device="cuda")
+        if n > 1:
+            dist.broadcast(done, src=0)
+        if done.item() > 0:
+            break
     for f in range(args.warmup):
         step(f)
     torch.cuda.synchronize()
@@ -294,17 +312,28 @@ def main():
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed, rays = float(tmax[0]), int(t[1])
 
+    # the roofline's serialised launches: 20 frames back to back on one stream (no overlap partner, so each
+    # launch has the whole GPU: "grid_pct" 100), the GPU kept busy so its clocks stay where the timed region
+    # ran them; the HIP-event duration of each launch is the kernel's own
+    if overlap:
+        r.set_option("grid_pct", 100)
+    for k in range(20):
+        step(args.warmup + args.steps + k, sync=False, one_stream=True)
+    torch.cuda.synchronize()
+    _, serial_ms = r.collect()
+    if overlap:
+        r.set_option("grid_pct", 0)
+    if n > 1:
+        dist.barrier()
     # SURVEY 8d latency definition: wall time from the call to the framebuffer being ready (rank 0: the
     # assembled frame), synchronous frames, median of 20 after the timed region (untimed for `value`)
-    # these frames are also the roofline's serialised launches: each starts on an idle GPU and has no
-    # overlap partner, so its HIP-event duration is the kernel's own (the timed region's launches overlap)
     lat = []
     for k in range(20):
         t1 = time.perf_counter()
         step(args.warmup + args.steps + k, sync=False)    # enqueue, then wait for the whole device
         torch.cuda.synchronize()
         lat.append((time.perf_counter() - t1) * 1e3)
-    _, serial_ms = r.collect()
+    _, sync_ms = r.collect()
     if n > 1:
         dist.barrier()
 
@@ -316,8 +345,9 @@ def main():
         dist.barrier()
 
     if rank == 0:
-        avg_kernel_ms = float(np.mean(kernel_ms))            # timed region: launches overlap (2 lanes)
-        serial_kernel_ms = float(np.mean(serial_ms))         # the same kernel with no overlap partner
+        avg_kernel_ms = float(np.mean(kernel_ms))            # timed region: launches overlap (L lanes)
+        serial_kernel_ms = float(np.mean(serial_ms))         # the same kernel with no overlap partner, back to back
+        sync_kernel_ms = float(np.mean(sync_ms))             # ... and after a host synchronisation each (latency frames)
         bytes_launch = algorithmic_bytes(cst)
         achieved = bytes_launch / (serial_kernel_ms * 1e-3) / 1e9
         kname = ("render_persistent_kernel" if args.kernel else "render_kernel") + ("<exact>" if args.exact else "<fast>")
@@ -375,6 +405,8 @@ def main():
             "host_busy_ms_median": round(float(np.median(timed_update[:, 2] - timed_update[:, 1])), 4),
             "kernel_ms": round(serial_kernel_ms, 4),
             "kernel_ms_overlapped": round(avg_kernel_ms, 4),
+            "kernel_ms_sync": round(sync_kernel_ms, 4),
+            "clock_warmup_s": args.clock_warmup,
             "roofline": {
                 "bound": "hbm",                                   # the roof `achieved` is priced against
                 "limiter": limiter,
@@ -391,7 +423,7 @@ def main():
                 "lib_sha16": tag["lib_sha16"],
                 "hbm_frac_measured": round(hbm_frac, 5) if hbm_frac is not None else None,
                 "kernel": kname,
-                "timing": "mean HIP-event duration of 20 serialised launches (kernel_ms)",
+                "timing": "mean HIP-event duration of 20 serialised launches, back to back on one stream (kernel_ms)",
                 "bytes_formula": "SURVEY 8(d): 32 aabb + 36 tri + 32 sphere/quad + 48 inst + 32 ray + 4 pixel",
                 "algorithmic_bytes_per_launch": int(bytes_launch),
                 "layout_bytes_per_launch": int(layout_bytes(cst)),

@@ -350,6 +350,9 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 as well, the instance hot records into 19 KB of LDS and reads them there; 2 = also the
  *                 sphere / parallelogram records and the instance cold records, while they fit (default 2;
  *                 0 = all from HBM; results identical)
+ *   "tlas_small": GPU-built frames (RT_BUILD_LBVH, "gpu_tlas"): 1 (default) = a TLAS of at most 512 records is built
+ *                 by one workgroup in one launch; 0 = the multi-kernel builder (results identical up to the tree's
+ *                 shape: inactive records are left out instead of sorted into a subtree no ray enters)
  *   "overlap"   : L = consecutive rt_render calls cycle through L (2..8) internal lanes (work-queue
  *                 heads, unit costs, schedule); a launch waits only for the previous launch of its own
  *                 lane and for its frame block, so a caller that cycles L streams runs frame
@@ -369,8 +372,8 @@ rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
  *               last launch used (band b's items start at 4 x its first unit: unit << 4 | piece << 2 | log2 pieces);
  *   "instances": RT_BUILD_LBVH or "gpu_tlas": 45 floats per instance, the records the GPU computed for the current frame
  *               (instances.hip): inverse, forward and inverse-transpose rows 1-3 (12 each), transformed box
- *               {xmin,xmax,ymin,ymax,zmin,zmax} (all +inf for a record kept out of the TLAS: a member of an
- *               intact instance group, option "group"), transformed centroid;
+ *               {xmin,xmax,ymin,ymax,zmin,zmax} (may be all +inf for a record kept out of the TLAS: a member of
+ *               an intact instance group, option "group"), transformed centroid;
  *   "blas_pairs", "blas_quads", "blas_roots": RT_BUILD_LBVH: the GPU-built forest as NodePair / NodeQuad /
  *               TreeRoot records (csrc/layout.hpp; quad q is the 4-wide node rooted at pair q);
  *   "leaf_prims": 1 u32 per leaf-ordered triangle slot: the caller's triangle index stored there (each

@@ -151,45 +151,76 @@ __global__ void prep_blas_kernel(const LbvhSeg *segs, const uint32_t *seg_of, ui
     cent[it] = make_float4(c.x, c.y, c.z, 0.0f);
 }
 
-// Centroid bounds per segment: a wave whose 64 items share one segment reduces in registers and
-// issues 6 atomics; mixed waves (segment boundaries) fall back to per-lane atomics.  Inactive TLAS items
-// (centroid w != 0, set_items) are left out.
-__global__ void bounds_kernel(const uint32_t *seg_of, const float4 *cent, uint32_t n, uint32_t *bounds) {
-    const uint32_t it = blockIdx.x * BLOCK + threadIdx.x;
-    const bool valid = it < n;
-    const uint32_t seg = valid ? seg_of[it] : NONE;
-    float4 c = valid ? cent[it] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    const uint32_t seg0 = __builtin_amdgcn_readfirstlane(seg);
-    const bool uniform = __all(seg == seg0);
-    const bool live = valid && c.w == 0.0f;
-    if (uniform) {
-        if (seg0 == NONE || !__any(live)) return;
-        const float inf = __builtin_huge_valf();
-        float lo[3] = {live ? c.x : inf, live ? c.y : inf, live ? c.z : inf};
-        float hi[3] = {live ? c.x : -inf, live ? c.y : -inf, live ? c.z : -inf};
+// Centroid bounds per segment.  Each block walks `ipt` consecutive block-wide strides of items; a wave
+// whose 64 items share one segment accumulates per lane across strides and reduces only when the segment
+// changes (or at the end), into the block's LDS slot when the segment is the one the block starts in, else
+// with global atomics; mixed waves (segment boundaries) fall back to per-lane atomics.  One global atomic
+// set per block for the common case: one segment of 10M triangles (C5's group) took 10.6 ms with a set per
+// wave, all on the same six words.  Inactive TLAS items (centroid w != 0, set_items) are left out.
+__device__ __forceinline__ void bounds_flush(uint32_t seg, float (&lo)[3], float (&hi)[3], uint32_t bseg, uint32_t *sb,
+                                             uint32_t *bounds) {
 #pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
+    for (int off = 32; off >= 1; off >>= 1) {
 #pragma unroll
-            for (int a = 0; a < 3; a++) {
-                lo[a] = fminf(lo[a], __shfl_xor(lo[a], off));
-                hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off));
-            }
+        for (int a = 0; a < 3; a++) {
+            lo[a] = fminf(lo[a], __shfl_xor(lo[a], off));
+            hi[a] = fmaxf(hi[a], __shfl_xor(hi[a], off));
         }
-        if ((threadIdx.x & 63) == 0) {
-#pragma unroll
-            for (int a = 0; a < 3; a++) {
-                atomicMin(&bounds[6 * seg0 + 2 * a], f2o(lo[a]));
-                atomicMax(&bounds[6 * seg0 + 2 * a + 1], f2o(hi[a]));
-            }
-        }
-        return;
     }
-    if (!live) return;
-    const float v[3] = {c.x, c.y, c.z};
+    if ((threadIdx.x & 63) == 0 && lo[0] <= hi[0]) {      // at least one live item
+        uint32_t *dst = seg == bseg ? sb : bounds + 6 * seg;
 #pragma unroll
-    for (int a = 0; a < 3; a++) {
-        atomicMin(&bounds[6 * seg + 2 * a], f2o(v[a]));
-        atomicMax(&bounds[6 * seg + 2 * a + 1], f2o(v[a]));
+        for (int a = 0; a < 3; a++) {
+            atomicMin(&dst[2 * a], f2o(lo[a]));
+            atomicMax(&dst[2 * a + 1], f2o(hi[a]));
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK) void bounds_kernel(const uint32_t *seg_of, const float4 *cent, uint32_t n, uint32_t ipt,
+                                                       uint32_t *bounds) {
+    __shared__ uint32_t sb[6];
+    const uint64_t base = (uint64_t)blockIdx.x * BLOCK * ipt;
+    const uint32_t bseg = base < n ? seg_of[base] : NONE;
+    if (threadIdx.x < 6) sb[threadIdx.x] = (threadIdx.x & 1) ? 0u : 0xFFFFFFFFu;
+    __syncthreads();
+    const float inf = __builtin_huge_valf();
+    uint32_t acc = NONE;                                   // wave-uniform: the segment lo/hi accumulate
+    float lo[3] = {inf, inf, inf}, hi[3] = {-inf, -inf, -inf};
+    for (uint32_t j = 0; j < ipt; j++) {
+        const uint64_t it = base + (uint64_t)j * BLOCK + threadIdx.x;
+        const bool valid = it < n;
+        const uint32_t seg = valid ? seg_of[it] : NONE;
+        const float4 c = valid ? cent[it] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const bool live = valid && c.w == 0.0f;
+        const uint32_t seg0 = __builtin_amdgcn_readfirstlane(seg);
+        if (__all(seg == seg0)) {
+            if (seg0 == NONE) break;                       // past the end (uniform across the wave)
+            if (seg0 != acc) {
+                if (acc != NONE) bounds_flush(acc, lo, hi, bseg, sb, bounds);
+                acc = seg0;
+#pragma unroll
+                for (int a = 0; a < 3; a++) { lo[a] = inf; hi[a] = -inf; }
+            }
+            if (live) {
+                lo[0] = fminf(lo[0], c.x); hi[0] = fmaxf(hi[0], c.x);
+                lo[1] = fminf(lo[1], c.y); hi[1] = fmaxf(hi[1], c.y);
+                lo[2] = fminf(lo[2], c.z); hi[2] = fmaxf(hi[2], c.z);
+            }
+        } else if (live) {
+            const float v[3] = {c.x, c.y, c.z};
+#pragma unroll
+            for (int a = 0; a < 3; a++) {
+                atomicMin(&bounds[6 * seg + 2 * a], f2o(v[a]));
+                atomicMax(&bounds[6 * seg + 2 * a + 1], f2o(v[a]));
+            }
+        }
+    }
+    if (acc != NONE) bounds_flush(acc, lo, hi, bseg, sb, bounds);
+    __syncthreads();
+    if (threadIdx.x < 6 && bseg != NONE && sb[0] != 0xFFFFFFFFu) {
+        if (threadIdx.x & 1) atomicMax(&bounds[6 * bseg + threadIdx.x], sb[threadIdx.x]);
+        else atomicMin(&bounds[6 * bseg + threadIdx.x], sb[threadIdx.x]);
     }
 }
 
@@ -613,7 +644,288 @@ __global__ __launch_bounds__(BLOCK) void collapse_wide_kernel(const LbvhSeg *seg
     }
 }
 
+// The same quads for forests with a large tree (an instance group's merged BLAS: C5's 10 M triangles in one
+// tree would keep the per-tree kernel's single workgroup walking level by level for ~60 ms): quad q is a pure
+// function of node pair q (its children, the largest-half-area interior one expanded twice), so every pair gets
+// its quad, one thread each; the quads of pairs absorbed into a parent's quad are written but never reached.
+__global__ void collapse_all_kernel(const NodePair *pairs, const uint32_t *n_pairs, NodeQuad *quads) {
+    const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
+    if (q >= *n_pairs) return;
+    float box[4][6];
+    uint32_t ref[4];
+    const NodePair P = pairs[q];
+#pragma unroll
+    for (int k = 0; k < 6; k++) { box[0][k] = P.c0[k]; box[1][k] = P.c1[k]; }
+    ref[0] = P.ref0; ref[1] = P.ref1;
+    uint32_t nc = 2;
+    while (nc < 4) {
+        int best = -1;
+        float area = -1.0f;
+        for (uint32_t k = 0; k < nc; k++)
+            if (!(ref[k] & REF_LEAF) && half_area(box[k]) > area) { area = half_area(box[k]); best = (int)k; }
+        if (best < 0) break;
+        const NodePair C = pairs[ref[best] & REF_INDEX_MASK];
+        for (int k = 0; k < 6; k++) { box[best][k] = C.c0[k]; box[nc][k] = C.c1[k]; }
+        ref[best] = C.ref0;
+        ref[nc] = C.ref1;
+        nc++;
+    }
+    NodeQuad Q;
+    for (uint32_t k = 0; k < 4; k++) {
+        const bool used = k < nc;
+        const float inf = __builtin_huge_valf();
+        Q.lo_x[k] = used ? box[k][0] : inf; Q.hi_x[k] = used ? box[k][1] : inf;
+        Q.lo_y[k] = used ? box[k][2] : inf; Q.hi_y[k] = used ? box[k][3] : inf;
+        Q.lo_z[k] = used ? box[k][4] : inf; Q.hi_z[k] = used ? box[k][5] : inf;
+        Q.ref[k] = used ? ref[k] : REF_EMPTY;
+        Q.pad[k] = 0;
+    }
+    float4 *dst = reinterpret_cast<float4 *>(quads + q);
+    const float4 *src = reinterpret_cast<const float4 *>(&Q);
+#pragma unroll
+    for (int k = 0; k < 8; k++) dst[k] = src[k];
+}
+
+__global__ void copy_roots_kernel(const TreeRoot *roots, uint32_t n, TreeRoot *roots_wide) {
+    const uint32_t s = blockIdx.x * BLOCK + threadIdx.x;
+    if (s < n) roots_wide[s] = roots[s];                        // quad root ref == pair root ref
+}
+
+// ---- the whole per-frame GPU TLAS in one workgroup (GPU-built frames with few TLAS items) ---------------
+// The multi-kernel chain (instance deltas -> records -> bounds -> Morton -> radix sort -> Karras -> boxes ->
+// scan -> pairs -> roots -> quads -> slots -> slot-ordered records) is ~17 launches on one stream per frame:
+// ~100 us of launch gaps for a C2-size TLAS, which bounded GPU-built C2 frames.  With option "group" a GPU-built
+// scene's TLAS holds a handful of items (C2: 6, C5: 6 of 9,772 records), so one workgroup runs the same build
+// in LDS: the same Morton codes, the stable (key, item) order, Karras' hierarchy, exact box unions, leaf
+// collapse, node pairs, quads and slots — over the active records only (inactive ones are left out instead of
+// being sorted behind them).
+constexpr uint32_t SMALL_BLOCK = 1024;
+
+__global__ __launch_bounds__(SMALL_BLOCK) void tlas_small_kernel(SmallTlasArgs a) {
+    __shared__ unsigned long long skey[SMALL_TLAS_MAX];        // (Morton << 32 | live index), sorted
+    __shared__ float snbox[(SMALL_TLAS_MAX - 1) * 6];
+    __shared__ float sibox[SMALL_TLAS_MAX * 6];               // live item boxes
+    __shared__ uint32_t schild[2 * (SMALL_TLAS_MAX - 1)], sparent[SMALL_TLAS_MAX - 1], srange[2 * (SMALL_TLAS_MAX - 1)];
+    __shared__ uint32_t sparent_leaf[SMALL_TLAS_MAX], sflag[SMALL_TLAS_MAX - 1], sheight[SMALL_TLAS_MAX - 1];
+    __shared__ uint32_t spidx[SMALL_TLAS_MAX], slive[SMALL_TLAS_MAX];
+    __shared__ uint32_t scount[SMALL_BLOCK];
+    __shared__ uint32_t sbound[6];
+    const uint32_t t = threadIdx.x, n = a.n;
+    if (t < 6) sbound[t] = (t & 1) ? 0u : 0xFFFFFFFFu;
+    // 1. the live records (instance_update_kernel computed every record; centroid w != 0 marks an inactive one),
+    // in record order: contiguous chunks per thread
+    const uint32_t chunk = (n + SMALL_BLOCK - 1) / SMALL_BLOCK, i0 = t * chunk, i1 = min(n, i0 + chunk);
+    uint32_t live = 0;
+    for (uint32_t i = i0; i < i1; i++) live += a.tcent[i].w == 0.0f ? 1u : 0u;
+    scount[t] = live;
+    __syncthreads();
+    if (t == 0) {                                            // exclusive scan of the per-thread live counts
+        uint32_t acc = 0;
+        for (uint32_t k = 0; k < SMALL_BLOCK; k++) { const uint32_t v = scount[k]; scount[k] = acc; acc += v; }
+        sflag[0] = acc;                                      // (reused below) m
+    }
+    __syncthreads();
+    const uint32_t m = sflag[0];
+    uint32_t pos = scount[t];
+    for (uint32_t i = i0; i < i1; i++)
+        if (a.tcent[i].w == 0.0f && pos < SMALL_TLAS_MAX) slive[pos++] = i;
+    __syncthreads();
+    if (m == 0 || m > SMALL_TLAS_MAX) {                      // the host checked; nothing to build
+        if (t == 0) { *a.pair_count = 0; }
+        return;
+    }
+    // 2. item boxes / centroid bounds over the live items (bounds_kernel), Morton keys (morton_kernel)
+    for (uint32_t k = t; k < m; k += SMALL_BLOCK) {
+        const uint32_t i = slive[k];
+#pragma unroll
+        for (int q = 0; q < 6; q++) sibox[6 * k + q] = a.tbox[6 * (size_t)i + q];
+        const float4 c = a.tcent[i];
+        atomicMin(&sbound[0], f2o(c.x)); atomicMax(&sbound[1], f2o(c.x));
+        atomicMin(&sbound[2], f2o(c.y)); atomicMax(&sbound[3], f2o(c.y));
+        atomicMin(&sbound[4], f2o(c.z)); atomicMax(&sbound[5], f2o(c.z));
+    }
+    __syncthreads();
+    uint32_t np = 1;
+    while (np < m) np <<= 1;
+    for (uint32_t k = t; k < np; k += SMALL_BLOCK) {
+        unsigned long long key = ~0ull;
+        if (k < m) {
+            const float4 c = a.tcent[slive[k]];
+            const uint32_t x = quant10(c.x, o2f(sbound[0]), o2f(sbound[1]));
+            const uint32_t y = quant10(c.y, o2f(sbound[2]), o2f(sbound[3]));
+            const uint32_t z = quant10(c.z, o2f(sbound[4]), o2f(sbound[5]));
+            key = ((unsigned long long)((expand10(x) << 2) | (expand10(y) << 1) | expand10(z)) << 32) | k;
+        }
+        skey[k] = key;
+    }
+    __syncthreads();
+    // bitonic sort of (code, item): the radix sort's stable order
+    for (uint32_t size = 2; size <= np; size <<= 1)
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (uint32_t k = t; k < np; k += SMALL_BLOCK) {
+                const uint32_t o = k ^ stride;
+                if (o > k) {
+                    const unsigned long long x = skey[k], y = skey[o];
+                    const bool up = (k & size) == 0;
+                    if ((x > y) == up) { skey[k] = y; skey[o] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    // 3. Karras hierarchy over the sorted codes (karras_kernel, one segment)
+    const int mi = (int)m;
+    auto code = [&](int i) { return (uint32_t)(skey[i] >> 32); };
+    auto delta = [&](int x, int y) -> int {
+        if (y < 0 || y >= mi) return -1;
+        const uint32_t kx = code(x), ky = code(y);
+        if (kx != ky) return __clz(kx ^ ky);
+        return 32 + __clz((uint32_t)x ^ (uint32_t)y);
+    };
+    for (int i = (int)t; i < mi - 1; i += SMALL_BLOCK) {
+        const int d = (delta(i, i + 1) - delta(i, i - 1)) >= 0 ? 1 : -1;
+        const int dmin = delta(i, i - d);
+        int lmax = 2;
+        while (delta(i, i + lmax * d) > dmin) lmax <<= 1;
+        int l = 0;
+        for (int q = lmax >> 1; q >= 1; q >>= 1)
+            if (delta(i, i + (l + q) * d) > dmin) l += q;
+        const int j = i + l * d;
+        const int dnode = delta(i, j);
+        int sp = 0, q = l;
+        do {
+            q = (q + 1) >> 1;
+            if (delta(i, i + (sp + q) * d) > dnode) sp += q;
+        } while (q > 1);
+        const int gamma = i + sp * d + (d < 0 ? -1 : 0);
+        const int lo = i < j ? i : j, hi = i < j ? j : i;
+        uint32_t c0, c1;
+        if (lo == gamma) { c0 = LEAF_BIT | (uint32_t)gamma; sparent_leaf[gamma] = (uint32_t)i; }
+        else { c0 = (uint32_t)gamma; sparent[gamma] = (uint32_t)i; }
+        if (hi == gamma + 1) { c1 = LEAF_BIT | (uint32_t)(gamma + 1); sparent_leaf[gamma + 1] = (uint32_t)i; }
+        else { c1 = (uint32_t)gamma + 1; sparent[gamma + 1] = (uint32_t)i; }
+        schild[2 * i] = c0; schild[2 * i + 1] = c1;
+        srange[2 * i] = (uint32_t)lo; srange[2 * i + 1] = (uint32_t)hi;
+        sflag[i] = 0;
+        if (i == 0) sparent[0] = NONE;
+    }
+    if (m == 1 && t == 0) sparent_leaf[0] = NONE;
+    __syncthreads();
+    // 4. exact box unions bottom-up (bottom_up_local_kernel)
+    const uint32_t cap = a.leaf_cap;
+    for (uint32_t li = t; li < m && m > 1; li += SMALL_BLOCK) {
+        uint32_t g = sparent_leaf[li];
+        while (g != NONE) {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (atomicAdd(&sflag[g], 1u) == 0u) break;
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            float b[6];
+            uint32_t h = 0;
+            for (int c = 0; c < 2; c++) {
+                const uint32_t ch = schild[2 * g + c];
+                const float *cb = (ch & LEAF_BIT) ? sibox + 6 * (skey[ch & ~LEAF_BIT] & 0xFFFFFFFFu) : snbox + 6 * ch;
+                const uint32_t chh = (ch & LEAF_BIT) ? 0u : sheight[ch];
+                if (c == 0) {
+                    for (int k = 0; k < 6; k++) b[k] = cb[k];
+                } else {
+                    merge_into(b, cb);
+                }
+                h = chh > h ? chh : h;
+            }
+            const uint32_t size = srange[2 * g + 1] - srange[2 * g] + 1u;
+#pragma unroll
+            for (int k = 0; k < 6; k++) snbox[6 * g + k] = b[k];
+            sheight[g] = size > cap ? h + 1u : 0u;
+            g = sparent[g];
+        }
+    }
+    __syncthreads();
+    // 5. kept interior nodes -> pair index (exclusive scan), pairs, root, slots
+    if (t == 0) {
+        uint32_t acc = 0;
+        for (uint32_t g = 0; g + 1 < m; g++) {
+            spidx[g] = acc;
+            acc += (srange[2 * g + 1] - srange[2 * g] + 1u) > cap ? 1u : 0u;
+        }
+        *a.pair_count = acc;
+    }
+    __syncthreads();
+    auto ref_of = [&](uint32_t ch) -> uint32_t {
+        if (ch & LEAF_BIT) return make_leaf_ref(ch & ~LEAF_BIT, 1u, 0u, false);
+        const uint32_t first = srange[2 * ch], size = srange[2 * ch + 1] - first + 1u;
+        if (size <= cap) return make_leaf_ref(first, size, 0u, false);
+        return make_interior_ref(spidx[ch], false);
+    };
+    for (uint32_t g = t; g + 1 < m; g += SMALL_BLOCK) {
+        if ((srange[2 * g + 1] - srange[2 * g] + 1u) <= cap) continue;
+        const uint32_t c0 = schild[2 * g], c1 = schild[2 * g + 1];
+        const float *b0 = (c0 & LEAF_BIT) ? sibox + 6 * (skey[c0 & ~LEAF_BIT] & 0xFFFFFFFFu) : snbox + 6 * c0;
+        const float *b1 = (c1 & LEAF_BIT) ? sibox + 6 * (skey[c1 & ~LEAF_BIT] & 0xFFFFFFFFu) : snbox + 6 * c1;
+        NodePair P;
+#pragma unroll
+        for (int k = 0; k < 6; k++) { P.c0[k] = b0[k]; P.c1[k] = b1[k]; }
+        P.ref0 = ref_of(c0);
+        P.ref1 = ref_of(c1);
+        P.pad0 = 0; P.pad1 = 0;
+        a.pairs[spidx[g]] = P;
+    }
+    for (uint32_t k = t; k < m; k += SMALL_BLOCK) a.slots[k] = slive[skey[k] & 0xFFFFFFFFu];
+    if (t == 0) {
+        TreeRoot R;
+        const float *b = m == 1 ? sibox : snbox;
+        for (int k = 0; k < 6; k++) R.box[k] = b[k];
+        R.ref = m == 1 ? make_leaf_ref(0, 1u, 0u, false)
+                       : (m <= cap ? make_leaf_ref(0, m, 0u, false) : make_interior_ref(spidx[0], false));
+        R.height = m == 1 ? 0u : sheight[0];
+        *a.root = R;
+        *a.root_wide = R;                                    // quad root ref == pair root ref
+    }
+    __syncthreads();                                         // pairs and records (global, this workgroup) complete
+    // 6. quads (collapse_all_kernel) and the records in leaf-slot order (slot_order_kernel)
+    const uint32_t npairs = *a.pair_count;
+    for (uint32_t q = t; q < npairs; q += SMALL_BLOCK) {
+        float box[4][6];
+        uint32_t ref[4];
+        const NodePair P = a.pairs[q];
+        for (int k = 0; k < 6; k++) { box[0][k] = P.c0[k]; box[1][k] = P.c1[k]; }
+        ref[0] = P.ref0; ref[1] = P.ref1;
+        uint32_t nc = 2;
+        while (nc < 4) {
+            int best = -1;
+            float area = -1.0f;
+            for (uint32_t k = 0; k < nc; k++)
+                if (!(ref[k] & REF_LEAF) && half_area(box[k]) > area) { area = half_area(box[k]); best = (int)k; }
+            if (best < 0) break;
+            const NodePair Cn = a.pairs[ref[best] & REF_INDEX_MASK];
+            for (int k = 0; k < 6; k++) { box[best][k] = Cn.c0[k]; box[nc][k] = Cn.c1[k]; }
+            ref[best] = Cn.ref0;
+            ref[nc] = Cn.ref1;
+            nc++;
+        }
+        NodeQuad Q;
+        for (uint32_t k = 0; k < 4; k++) {
+            const bool used = k < nc;
+            const float inf = __builtin_huge_valf();
+            Q.lo_x[k] = used ? box[k][0] : inf; Q.hi_x[k] = used ? box[k][1] : inf;
+            Q.lo_y[k] = used ? box[k][2] : inf; Q.hi_y[k] = used ? box[k][3] : inf;
+            Q.lo_z[k] = used ? box[k][4] : inf; Q.hi_z[k] = used ? box[k][5] : inf;
+            Q.ref[k] = used ? ref[k] : REF_EMPTY;
+            Q.pad[k] = 0;
+        }
+        a.quads[q] = Q;
+    }
+    for (uint32_t k = t; k < m; k += SMALL_BLOCK) {
+        const uint32_t i = slive[skey[k] & 0xFFFFFFFFu];
+        a.hot_s[k] = a.hot[i];
+        a.cold_s[k] = a.cold[i];
+    }
+}
+
 }  // namespace lbvh
+
+hipError_t launch_tlas_small(const SmallTlasArgs &a, hipStream_t stream) {
+    hipLaunchKernelGGL(lbvh::tlas_small_kernel, dim3(1), dim3(lbvh::SMALL_BLOCK), 0, stream, a);
+    return hipGetLastError();
+}
 
 // ---- host --------------------------------------------------------------------------------------
 using namespace lbvh;
@@ -637,7 +949,8 @@ static void dfree(T *&p) {
 void LbvhBuilder::release() {
     dfree(segs_); dfree(seg_of_); dfree(members_); dfree(own_box_); dfree(own_cent_); dfree(bounds_);
     dfree(k0_); dfree(k1_); dfree(v0_); dfree(v1_); dfree(child_); dfree(parent_); dfree(parent_leaf_);
-    dfree(range_); dfree(flag_); dfree(height_); dfree(nbox_); dfree(kept_); dfree(pidx_); dfree(front_);
+    dfree(range_); dfree(flag_); dfree(height_); dfree(nbox_); dfree(kept_); dfree(pidx_); dfree(front_); dfree(count_);
+    last_count_ = nullptr;
     if (tmp_) (void)hipFree(tmp_);
     tmp_ = nullptr; tmp_bytes_ = 0;
     box_ = nullptr; cent_ = nullptr;
@@ -712,7 +1025,11 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
     if (!box_ || !cent_ || n_items_ == 0) return hipErrorInvalidValue;
     const uint32_t N = n_items_, NI = n_items_ - n_segs_;
     hipLaunchKernelGGL(init_bounds_kernel, dim3(blocks_for(6ull * n_segs_)), dim3(BLOCK), 0, stream, bounds_, n_segs_);
-    hipLaunchKernelGGL(bounds_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, seg_of_, cent_, N, bounds_);
+    {   // ~1024 blocks at most: one LDS-combined atomic set per block (bounds_kernel)
+        const uint32_t ipt = std::max<uint32_t>(1u, (uint32_t)((N + (uint64_t)BLOCK * 1024 - 1) / ((uint64_t)BLOCK * 1024)));
+        const uint32_t nb = (uint32_t)((N + (uint64_t)BLOCK * ipt - 1) / ((uint64_t)BLOCK * ipt));
+        hipLaunchKernelGGL(bounds_kernel, dim3(nb), dim3(BLOCK), 0, stream, seg_of_, cent_, N, ipt, bounds_);
+    }
     hipLaunchKernelGGL(morton_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, seg_of_, cent_, N, bounds_,
                        size_classes_ ? box_ : nullptr, k0_, v0_);
     LB_TRY(hipGetLastError());
@@ -726,6 +1043,11 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
         hipLaunchKernelGGL(bottom_up_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, box_, N, child_,
                            parent_, parent_leaf_, range_, flag_, nbox_, height_, kept_);
     LB_TRY(hipGetLastError());
+    if (!pair_count) {                                // collapse_wide needs the count of this build's pairs
+        if (!count_) LB_TRY(dalloc(count_, 1));
+        pair_count = count_;
+    }
+    last_count_ = pair_count;
     if (NI > 0) {
         bytes = tmp_bytes_;
         LB_TRY(rocprim::exclusive_scan(tmp_, bytes, kept_, pidx_, 0u, NI, rocprim::plus<uint32_t>(), stream));
@@ -747,6 +1069,12 @@ hipError_t LbvhBuilder::gather_blas(const RawPrimsGPU &raw, const PrimOutGPU &ou
 
 hipError_t LbvhBuilder::collapse_wide(const NodePair *pairs, const TreeRoot *roots, NodeQuad *quads, TreeRoot *roots_wide,
                                       hipStream_t stream) {
+    if (max_count_ > COLLAPSE_ALL_MIN && last_count_) {
+        hipLaunchKernelGGL(collapse_all_kernel, dim3(blocks_for(max_pairs())), dim3(BLOCK), 0, stream, pairs, last_count_, quads);
+        if (roots_wide)
+            hipLaunchKernelGGL(copy_roots_kernel, dim3(blocks_for(n_segs_)), dim3(BLOCK), 0, stream, roots, n_segs_, roots_wide);
+        return hipGetLastError();
+    }
     if (max_count_ - 1 > LDS_FRONT && !front_) LB_TRY(dalloc(front_, 2 * (size_t)max_pairs()));
     hipLaunchKernelGGL(collapse_wide_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, roots, pairs, quads, front_,
                        max_pairs(), roots_wide);
@@ -761,30 +1089,3 @@ hipError_t LbvhBuilder::gather_items(uint32_t *slots, hipStream_t stream) {
 
 }  // namespace rtamd
 
-namespace rtamd {
-namespace lbvh {
-// Per-frame: copy each instance's BLAS root {box, ref} into its hot record (the host staging block
-// carries the matrices; the roots of GPU-built BLASes live only in HBM).
-// wide_refs: null for GPU-built BLASes (the quad root of a GPU-built tree has the pair root's ref,
-// collapse_wide_kernel); host-built BLASes under the GPU TLAS pass their quad roots
-__global__ void patch_roots_kernel(InstHot *hot, const uint32_t *inst_blas, const TreeRoot *roots, const uint32_t *wide_refs,
-                                   uint32_t n) {
-    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t b = inst_blas[i];
-    const TreeRoot R = roots[b];
-#pragma unroll
-    for (int k = 0; k < 6; k++) hot[i].root_box[k] = R.box[k];
-    hot[i].root_ref = R.ref;
-    hot[i].root_ref_wide = wide_refs ? wide_refs[b] : R.ref;
-}
-}  // namespace lbvh
-
-hipError_t launch_patch_inst_roots(InstHot *hot, const uint32_t *inst_blas, const TreeRoot *roots, const uint32_t *wide_refs,
-                                   uint32_t n, hipStream_t stream) {
-    if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(lbvh::patch_roots_kernel, dim3(lbvh::blocks_for(n)), dim3(lbvh::BLOCK), 0, stream, hot, inst_blas,
-                       roots, wide_refs, n);
-    return hipGetLastError();
-}
-}  // namespace rtamd

@@ -56,6 +56,20 @@ struct PrimOutGPU {         // leaf-ordered arrays written by the BLAS gather
     QuadHot *quad_hot; PrimCold *quad_cold;
 };
 
+// The per-frame GPU TLAS of a frame with at most SMALL_TLAS_MAX active records, built by one workgroup
+// (tlas_small_kernel) after instance_update_kernel computed the records: the LBVH over the active records,
+// pairs, quads, slots and the slot-ordered records — one launch instead of ~14.
+constexpr uint32_t SMALL_TLAS_MAX = 512;
+struct SmallTlasArgs {
+    uint32_t n;                                     // records (instances, then groups)
+    const InstHot *hot; const InstCold *cold; const float *tbox; const float4 *tcent;   // record order
+    NodePair *pairs; TreeRoot *root; TreeRoot *root_wide; NodeQuad *quads; uint32_t *slots;
+    InstHot *hot_s; InstCold *cold_s;               // leaf-slot order
+    uint32_t *pair_count;
+    uint32_t leaf_cap;
+};
+hipError_t launch_tlas_small(const SmallTlasArgs &a, hipStream_t stream);
+
 class LbvhBuilder {
 public:
     LbvhBuilder() = default;
@@ -118,6 +132,10 @@ private:
     float *nbox_ = nullptr;               // 6 per interior node
     uint32_t *kept_ = nullptr, *pidx_ = nullptr;
     uint32_t *front_ = nullptr;           // collapse_wide frontier of trees too large for LDS
+    uint32_t *count_ = nullptr;           // pairs written by the last build (when the caller passed no counter)
+    uint32_t *last_count_ = nullptr;      // the counter the last build wrote
+    // a forest with a tree of more than this many items is collapsed one pair per thread (collapse_all_kernel)
+    static constexpr uint32_t COLLAPSE_ALL_MIN = 65536;
     void *tmp_ = nullptr;
     size_t tmp_bytes_ = 0;
 };

@@ -42,11 +42,10 @@ hipError_t launch_frame_copy(void *, const void *, size_t, unsigned long long *,
 hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t,
                            uint32_t, uint32_t, void *, const void *, size_t, unsigned long long *, hipStream_t);
 uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool wide);
-hipError_t launch_patch_inst_roots(InstHot *, const uint32_t *, const TreeRoot *, const uint32_t *, uint32_t, hipStream_t);
 hipError_t launch_instance_slot_order(const uint32_t *, const InstHot *, const InstCold *, uint32_t, InstHot *, InstCold *,
                                       hipStream_t);
 hipError_t launch_instance_update(const InstDelta *, uint32_t, InstParams *, uint32_t, InstHot *, InstCold *, float *, float4 *,
-                                  hipStream_t);
+                                  const uint32_t *, const TreeRoot *, const uint32_t *, bool, hipStream_t);
 uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool wide);
 }  // namespace rtamd
 
@@ -338,6 +337,9 @@ struct rt_scene {
     hipEvent_t ev_render_done = nullptr;   // last trace launch finished (BLAS rebuilds wait on it)
     bool tlas_size_classes = false;     // option "tlas_classes": GPU TLAS keys start with an item size class (measured neutral)
     bool gpu_tlas_sah = false;          // option "gpu_tlas" (set before the build): RT_BUILD_SAH BLASes, per-frame TLAS on the GPU
+    // option "tlas_small": GPU-built frames with at most SMALL_TLAS_MAX records in the TLAS build it in one workgroup
+    // (lbvh.hip tlas_small_kernel) instead of the ~17-launch chain
+    bool tlas_small = true;
     DevBuf<uint32_t> blas_wide_refs;    // host-built BLASes under a GPU TLAS: quad root ref per BLAS
     // instance records + TLAS built by kernels each frame: RT_BUILD_LBVH, or RT_BUILD_SAH with "gpu_tlas"
     bool gpu_tlas() const { return build_mode == RT_BUILD_LBVH || (gpu_tlas_sah && build_mode == RT_BUILD_SAH); }
@@ -582,19 +584,38 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         // a blit kernel reading the pinned staging block, not an SDMA copy (see the host-built path below)
         if (nd) HIP_TRY(launch_frame_copy(fd + s->off_delta, s->staging_dev[b] + s->off_delta, nd * sizeof(InstDelta), nullptr, nullptr,
                                           s->stream));
-        // Instance::updateTransformArguments for every instance, on the GPU (instances.hip)
-        HIP_TRY(launch_instance_update(reinterpret_cast<const InstDelta *>(fd + s->off_delta), nd, s->inst_params.p,
-                                       (uint32_t)nrec, reinterpret_cast<InstHot *>(fd + s->off_hot),
-                                       reinterpret_cast<InstCold *>(fd + s->off_cold), reinterpret_cast<float *>(fd + s->off_tbox),
-                                       reinterpret_cast<float4 *>(fd + s->off_tcent), s->stream));
-        if (s->blas_builder && (s->rebuild_blas || s->blas_dirty)) {    // GPU-built BLASes only
-            const rt_status bs = gpu_build_blas(s);
-            if (bs != RT_OK) return bs;
-        }
+        if (s->blas_builder && (s->rebuild_blas || s->blas_dirty)) RT_TRY(gpu_build_blas(s));   // GPU-built BLASes only
+        uint32_t live = 0;                              // records in this frame's TLAS
+        for (size_t i = 0; i < nrec; i++) live += record_inactive(s, i) ? 0u : 1u;
+        const bool small = s->tlas_small && live > 0 && live <= SMALL_TLAS_MAX;
         const uint32_t n = (uint32_t)nrec;
-        HIP_TRY(launch_patch_inst_roots(reinterpret_cast<InstHot *>(fd + s->off_hot), s->inst_blas.p, s->blas_roots.p,
-                                        s->blas_wide_refs.p, n,
-                                        s->stream));
+        // Instance::updateTransformArguments for every record, on the GPU, with its BLAS root (instances.hip)
+        HIP_TRY(launch_instance_update(reinterpret_cast<const InstDelta *>(fd + s->off_delta), nd, s->inst_params.p, n,
+                                       reinterpret_cast<InstHot *>(fd + s->off_hot), reinterpret_cast<InstCold *>(fd + s->off_cold),
+                                       reinterpret_cast<float *>(fd + s->off_tbox), reinterpret_cast<float4 *>(fd + s->off_tcent),
+                                       s->inst_blas.p, s->blas_roots.p, s->blas_wide_refs.p, /*inf_inactive=*/!small, s->stream));
+        if (small) {
+            // one workgroup: the LBVH TLAS over the live records, quads, slots, slot-ordered records (lbvh.hip)
+            SmallTlasArgs a{};
+            a.n = n;
+            a.hot = reinterpret_cast<const InstHot *>(fd + s->off_hot); a.cold = reinterpret_cast<const InstCold *>(fd + s->off_cold);
+            a.tbox = reinterpret_cast<const float *>(fd + s->off_tbox); a.tcent = reinterpret_cast<const float4 *>(fd + s->off_tcent);
+            a.pairs = reinterpret_cast<NodePair *>(fd + s->off_pairs); a.root = reinterpret_cast<TreeRoot *>(fd + s->off_root);
+            a.root_wide = reinterpret_cast<TreeRoot *>(fd + s->off_root_wide);
+            a.quads = reinterpret_cast<NodeQuad *>(fd + s->off_quads); a.slots = reinterpret_cast<uint32_t *>(fd + s->off_slots);
+            a.hot_s = reinterpret_cast<InstHot *>(fd + s->off_hot_s); a.cold_s = reinterpret_cast<InstCold *>(fd + s->off_cold_s);
+            a.pair_count = s->gpu_counts.p + 1;
+            a.leaf_cap = s->tlas_leaf;
+            HIP_TRY(launch_tlas_small(a, s->stream));
+            s->block_by_slot[b] = s->inst_by_slot;
+            s->frame_items[b] = live;
+            HIP_TRY(hipEventRecord(s->ev_copied[b], s->stream));
+            s->r_copied[b] = s->ev_copied[b];
+            s->active = b;
+            s->frame = frame;
+            return RT_OK;
+        }
+        s->frame_items[b] = n;
         HIP_TRY(s->tlas_builder->set_items(reinterpret_cast<const float *>(fd + s->off_tbox),
                                            reinterpret_cast<const float4 *>(fd + s->off_tcent)));
         HIP_TRY(s->tlas_builder->build(reinterpret_cast<NodePair *>(fd + s->off_pairs), reinterpret_cast<TreeRoot *>(fd + s->off_root),
@@ -700,7 +721,7 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.sph_hot = s->sph_hot.p; g.sph_cold = s->sph_cold.p;
     g.quad_hot = s->quad_hot.p; g.quad_cold = s->quad_cold.p;
     g.materials = s->materials.p;
-    g.instance_count = s->gpu_tlas() ? (uint32_t)(s->inst.size() + s->groups.size()) : s->frame_items[b];   // records
+    g.instance_count = s->frame_items[b];   // records the frame's TLAS holds (GPU-built, small path: the live ones)
     g.rough_count = (uint32_t)s->roughs.size();
     g.material_count = (uint32_t)(s->materials.n / 4);
     // option "lds_scene": the quads the frame's TLAS refs can index (host-built: this frame's quad count;
@@ -709,7 +730,7 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.lds_icold = g.lds_sph_hot = g.lds_sph_cold = g.lds_q_hot = g.lds_q_cold = LDS_NONE;
     if (s->lds_scene && g.wide) {
         const uint32_t n = g.instance_count;
-        const uint32_t nq = s->gpu_tlas() ? (n > 1 ? n - 1 : 0) : (uint32_t)s->tlas_wide.quads.size();
+        const uint32_t nq = s->gpu_tlas() ? (n > 1 ? n - 1 : 0) : (uint32_t)s->tlas_wide.quads.size();   // GPU: <= items - 1
         if (nq > 0 && nq * LDS_QUAD_F4 <= LDS_SCENE_F4) {
             g.lds_quads = nq;
             if (nq * LDS_QUAD_F4 + n * LDS_INST_F4 <= LDS_SCENE_F4) g.lds_insts = n;
@@ -1877,6 +1898,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_classes must be 0 or 1");
         s->tlas_size_classes = value == 1;
         if (s->tlas_builder) s->tlas_builder->size_classes_ = s->tlas_size_classes;
+    } else if (k == "tlas_small") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_small must be 0 or 1");
+        s->tlas_small = value == 1;
     } else if (k == "gpu_tlas") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "gpu_tlas must be 0 or 1");
         if (s->built) return fail(RT_ERR_UNSUPPORTED, "gpu_tlas is set before rt_scene_build");

@@ -619,6 +619,10 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
         lx = Q[0]; hx = Q[1]; ly = Q[2]; hy = Q[3]; lz = Q[4]; hz = Q[5];
         R = reinterpret_cast<const uint4 *>(Q)[6];
     }
+    // the child refs are needed only when a child is hit, so the compiler would issue their load after the slab
+    // tests: a second dependent memory round trip per step.  Pinning them here keeps all 7 dwordx4 loads of the
+    // node in one round trip.
+    asm volatile("" ::"v"(R.x), "v"(R.y), "v"(R.z), "v"(R.w));
     if (COUNT) cnt.pairs += 2;                       // 4 child boxes = 2 node-pair equivalents
     const RayP &r = blas ? T.lr : T.wr;
     float t[4];
@@ -741,6 +745,9 @@ __device__ __forceinline__ uint32_t spec_leaf_phase(Trav &T, const SceneGPU &sc,
 #if !RT_EXACT
         if (WIDE) {
             const InstRec I = load_inst<true>(sc, T.cur_inst);
+            // all 5 dwordx4 of the record in one round trip (the root ref is used only when the root box is hit,
+            // so its load would otherwise be issued after the slab test)
+            asm volatile("" ::"v"(I.i2.x), "v"(I.i2.y), "v"(I.i2.z), "v"(I.i2.w), "v"(I.box2ref.w));
             const float inv[12] = {I.i0.x, I.i0.y, I.i0.z, I.i0.w, I.i1.x, I.i1.y, I.i1.z, I.i1.w,
                                    I.i2.x, I.i2.y, I.i2.z, I.i2.w};
             const float box[6] = {I.box01.x, I.box01.y, I.box01.z, I.box01.w, I.box2ref.x, I.box2ref.y};
@@ -772,17 +779,18 @@ __device__ __forceinline__ uint32_t spec_leaf_phase(Trav &T, const SceneGPU &sc,
             // trip per leaf instead of one per triangle (tests still run in leaf order, BLAS.cu:153-176)
             for (uint32_t k0 = 0; k0 < count; k0 += TRI_AHEAD) {
                 TriHot H[TRI_AHEAD];           // 3 x 12 B loads per triangle (the pad words stay unread)
+                // unconditional loads (slots past the leaf's last triangle re-read that one): a load under
+                // `k0 + k < count` would be issued only after the previous triangles' loads were waited for
 #pragma unroll
-                for (uint32_t k = 0; k < TRI_AHEAD; k++)
-                    if (k0 + k < count) {
-                        const float *src = sc.tri_hot[start + k0 + k].v0;
-                        const float3 a = *reinterpret_cast<const float3 *>(src);
-                        const float3 b = *reinterpret_cast<const float3 *>(src + 4);
-                        const float3 c = *reinterpret_cast<const float3 *>(src + 8);
-                        H[k].v0[0] = a.x; H[k].v0[1] = a.y; H[k].v0[2] = a.z;
-                        H[k].e1[0] = b.x; H[k].e1[1] = b.y; H[k].e1[2] = b.z;
-                        H[k].e2[0] = c.x; H[k].e2[1] = c.y; H[k].e2[2] = c.z;
-                    }
+                for (uint32_t k = 0; k < TRI_AHEAD; k++) {
+                    const float *src = sc.tri_hot[start + min(k0 + k, count - 1u)].v0;
+                    const float3 a = *reinterpret_cast<const float3 *>(src);
+                    const float3 b = *reinterpret_cast<const float3 *>(src + 4);
+                    const float3 c = *reinterpret_cast<const float3 *>(src + 8);
+                    H[k].v0[0] = a.x; H[k].v0[1] = a.y; H[k].v0[2] = a.z;
+                    H[k].e1[0] = b.x; H[k].e1[1] = b.y; H[k].e1[2] = b.z;
+                    H[k].e2[0] = c.x; H[k].e2[1] = c.y; H[k].e2[2] = c.z;
+                }
 #pragma unroll
                 for (uint32_t k = 0; k < TRI_AHEAD; k++) {
                     if (k0 + k >= count) break;

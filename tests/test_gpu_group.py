@@ -120,8 +120,13 @@ def test_lbvh_group_tree_equals_restatement(gpu_lib):
     assert np.array_equal(ci, wci) and np.array_equal(refs, wrefs) and np.array_equal(nb, wb)
     with pytest.raises(abi.RtError):
         r.export_blas(4)                                   # particle 0's own BLAS: not built
-    _, _, trefs = r.export_tlas()                         # every record is a TLAS leaf (inactive ones in a subtree
-    assert sorted(trefs.tolist()) == list(range(len(s.instances) + 1))   # no ray enters); the group is record n
+    n = len(s.instances)
+    _, _, trefs = r.export_tlas()                         # the TLAS holds the demo instances and the group (record n)
+    assert sorted(trefs.tolist()) == list(range(n - P)) + [n]
+    r.set_option("tlas_small", 0)                         # the multi-kernel builder: every record is a leaf, the
+    r.render(1)                                           # inactive ones in a subtree no ray enters
+    _, _, trefs = r.export_tlas()
+    assert sorted(trefs.tolist()) == list(range(n + 1))
 
 
 def test_lbvh_group_images_and_hits_match_oracle(gpu_lib):

@@ -289,13 +289,15 @@ def _expected_quads(pairs, root_ref):
     return out
 
 
-@pytest.mark.parametrize("mode", ["particles", "large"])
+@pytest.mark.parametrize("mode", ["particles", "large", "group80"])
 def test_gpu_quad_collapse_equals_restatement(gpu_lib, mode):
     """RT_BUILD_LBVH trees get the 4-wide form on the GPU (collapse_wide_kernel, lbvh.hip): every quad equals
     the host collapse rule applied to the GPU's binary tree (bit for bit, slot order included), and the quad
     traversal renders the binary traversal's frame within the FAST tolerance with the same ray count."""
     if mode == "particles":
         s = scenes.demo_with_particles(12)
+    elif mode == "group80":  # one 81,920-triangle group BLAS (> 65,536 items): collapsed one pair per thread
+        s = scenes.demo_with_particles(80)
     else:   # one BLAS of 65k triangles: its frontier lives in global scratch, not LDS
         tris, inst = scenes.synth_particles(64, 1024, seed=3)
         s = scenes.demo_scene()
@@ -329,3 +331,34 @@ def test_gpu_quad_collapse_equals_restatement(gpu_lib, mode):
     assert f >= 0.999, (f, mx)
     assert abs(out[0][2]["rays"] - out[1][2]["rays"]) <= 0.001 * out[0][2]["rays"]
     assert out[1][2]["aabb_tests"] != out[0][2]["aabb_tests"]          # the quad form really ran
+
+
+@pytest.mark.parametrize("group", [0, 1])
+def test_small_tlas_equals_multi_kernel_tlas(gpu_lib, group):
+    """Option "tlas_small": one workgroup builds the GPU TLAS (deltas, records, Morton, sort, Karras, boxes, pairs,
+    quads, slots) when at most 512 records are in it.  Without instance groups every record is in the TLAS and the
+    tree is the multi-kernel builder's: identical exports and byte-identical frames over animated frames.  With
+    groups the inactive member records are left out of the TLAS altogether: the tree holds the live records only
+    and frames stay within the FAST tolerance of the multi-kernel path (which sorts them into a dead subtree)."""
+    s = scenes.demo_with_particles(12)
+    a = Renderer(s).set_option("group", group).build_acceleration_structure(0, mode="lbvh").configure_camera(
+        256, 144, ray_trace_depth=2)
+    b = Renderer(s).set_option("group", group).build_acceleration_structure(0, mode="lbvh").configure_camera(
+        256, 144, ray_trace_depth=2)
+    b.set_option("tlas_small", 0)
+    n = len(s.instances)
+    for frame in (0, 3, 37):
+        fa, fb = a.render(frame)[0], b.render(frame)[0]
+        ta, tb = a.export_tlas(), b.export_tlas()
+        if group == 0:
+            assert np.array_equal(fa, fb), frame
+            for x, y in zip(ta, tb):
+                assert np.array_equal(x, y), frame
+            assert sorted(ta[2].tolist()) == list(range(n))
+        else:
+            f, mx = frac_within(fa, fb)
+            assert f >= 0.9995, (frame, f, mx)
+            live = sorted(ta[2].tolist())
+            assert live == list(range(n - 12)) + [n], live         # the demo instances and the group record
+    a.cleanup()
+    b.cleanup()
