@@ -198,12 +198,18 @@ struct rt_scene {
     // (the root and the item arrays are used by GPU-built TLASes only)
     size_t frame_block = 0, off_root = 0, off_pairs = 0, off_slots = 0, off_hot = 0, off_cold = 0, off_tbox = 0,
            off_tcent = 0, off_root_wide = 0, off_quads = 0, off_delta = 0, off_hot_s = 0, off_cold_s = 0;
-    // GPU-built frames: per-instance parameters resident in HBM (instances.hip); the host stages a delta
-    // (InstDelta at off_delta) only for instances whose transform or local box changed
-    DevBuf<InstParams> inst_params;
-    std::vector<uint8_t> inst_dirty;
     // frame blocks cycle through NLANE buffers, so "overlap" lanes never wait on each other's block
     static constexpr int NLANE = 8;
+    // GPU-built frames: per-instance parameters resident in HBM (instances.hip), one copy per frame block
+    // (block b's at inst_params.p + b * records), so frames of different lanes update their records
+    // concurrently; the host stages a delta (InstDelta at off_delta) only for the records whose transform
+    // or local box changed since block b was last written: inst_dirty bit b (ALL_BLOCKS: every block)
+    DevBuf<InstParams> inst_params;
+    std::vector<uint8_t> inst_dirty;
+    static constexpr uint8_t ALL_BLOCKS = 0xFF;
+    static_assert(NLANE <= 8, "inst_dirty holds one bit per frame block");
+    hipStream_t chain_stream[NLANE] = {};         // GPU-built frame b's records / TLAS were built on this stream
+    hipEvent_t ev_blas_built = nullptr;           // a GPU BLAS build on the scene stream finished
     uint8_t *staging[NLANE] = {};                 // pinned host
     uint8_t *staging_dev[NLANE] = {};             // the same, as device-visible pointers
     int pending_copy = -1;                        // rt_render: block whose upload the next launch performs
@@ -315,7 +321,7 @@ struct rt_scene {
     std::vector<LbvhSeg> lbvh_segs;
     std::vector<uint32_t> seg_of_blas;
     std::vector<uint8_t> lbvh_intact;
-    DevBuf<uint32_t> gpu_counts;        // [0] BLAS pairs written, [1] TLAS pairs written (last frame)
+    DevBuf<uint32_t> gpu_counts;        // [0] BLAS pairs written, [1] unused, [2 + b] TLAS pairs of frame block b
     bool rebuild_blas = false;          // option "rebuild": rebuild every BLAS each frame
     bool blas_dirty = false;            // rt_scene_update_triangles since the last BLAS build
     // RT_BUILD_LBVH rebuilds (option "blas_double", default on): a rebuild writes a spare BLAS set and swaps it
@@ -399,6 +405,7 @@ struct rt_scene {
             if (spare.ev_lane[q]) (void)hipEventDestroy(spare.ev_lane[q]);
         }
         if (ev_render_done) (void)hipEventDestroy(ev_render_done);
+        if (ev_blas_built) (void)hipEventDestroy(ev_blas_built);
         for (int b = 0; b < NLANE; b++) {
             if (staging[b]) (void)hipHostFree(staging[b]);
             if (frame_dev[b]) (void)hipFree(frame_dev[b]);
@@ -546,7 +553,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         // recomputed (the demo animates 5 of C2's 73 instances) — on the GPU for GPU-built frames
         for (size_t i = 0; i < xs.size(); i++)
             if (std::memcmp(&xs[i], &s->inst[i].x, sizeof(rt_xform)) != 0) {
-                if (s->gpu_tlas()) { s->inst[i].x = xs[i]; s->inst_dirty[i] = 1; }
+                if (s->gpu_tlas()) { s->inst[i].x = xs[i]; s->inst_dirty[i] = rt_scene::ALL_BLOCKS; }
                 else instance_update(s->inst[i], xs[i]);
             }
     }
@@ -561,9 +568,10 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         // only the changed records cross PCIe: (index, shift, cos / sin of the angles, scale, local box, inactive)
         InstDelta *dl = reinterpret_cast<InstDelta *>(st + s->off_delta);
         uint32_t nd = 0;
+        const uint8_t bit = (uint8_t)(1u << b);
         for (size_t i = 0; i < nrec; i++) {
-            if (!s->inst_dirty[i]) continue;
-            s->inst_dirty[i] = 0;
+            if (!(s->inst_dirty[i] & bit)) continue;
+            s->inst_dirty[i] &= (uint8_t)~bit;
             const InstState &in = record_state(s, i);
             InstDelta &d = dl[nd++];
             std::memset(&d, 0, sizeof d);
@@ -580,20 +588,30 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
             d.p.pad[0] = record_inactive(s, i) ? 1.0f : 0.0f;
         }
         uint8_t *fd = s->frame_dev[b];
-        HIP_TRY(hipStreamWaitEvent(s->stream, s->r_used[b], 0));
-        // a blit kernel reading the pinned staging block, not an SDMA copy (see the host-built path below)
-        if (nd) HIP_TRY(launch_frame_copy(fd + s->off_delta, s->staging_dev[b] + s->off_delta, nd * sizeof(InstDelta), nullptr, nullptr,
-                                          s->stream));
-        if (s->blas_builder && (s->rebuild_blas || s->blas_dirty)) RT_TRY(gpu_build_blas(s));   // GPU-built BLASes only
         uint32_t live = 0;                              // records in this frame's TLAS
         for (size_t i = 0; i < nrec; i++) live += record_inactive(s, i) ? 0u : 1u;
         const bool small = s->tlas_small && live > 0 && live <= SMALL_TLAS_MAX;
         const uint32_t n = (uint32_t)nrec;
-        // Instance::updateTransformArguments for every record, on the GPU, with its BLAS root (instances.hip)
-        HIP_TRY(launch_instance_update(reinterpret_cast<const InstDelta *>(fd + s->off_delta), nd, s->inst_params.p, n,
+        // the one-workgroup TLAS path touches only block b's buffers, so it runs on the trace's own stream
+        // (no cross-queue wait before the trace); the multi-kernel builder's scratch is shared: scene stream
+        const hipStream_t cs = small ? upload : s->stream;
+        if (s->blas_builder && (s->rebuild_blas || s->blas_dirty)) {    // GPU-built BLASes only (scene stream)
+            RT_TRY(gpu_build_blas(s));
+            if (cs != s->stream) {
+                if (!s->ev_blas_built) HIP_TRY(hipEventCreateWithFlags(&s->ev_blas_built, hipEventDisableTiming));
+                HIP_TRY(hipEventRecord(s->ev_blas_built, s->stream));
+                HIP_TRY(hipStreamWaitEvent(cs, s->ev_blas_built, 0));
+            }
+        }
+        if (s->r_used[b]) HIP_TRY(hipStreamWaitEvent(cs, s->r_used[b], 0));      // block b no longer read
+        // Instance::updateTransformArguments for every record of block b, on the GPU, with its BLAS root
+        // (instances.hip); the deltas are read from the pinned staging block directly
+        HIP_TRY(launch_instance_update(reinterpret_cast<const InstDelta *>(s->staging_dev[b] + s->off_delta), nd,
+                                       s->inst_params.p + (size_t)b * n, n,
                                        reinterpret_cast<InstHot *>(fd + s->off_hot), reinterpret_cast<InstCold *>(fd + s->off_cold),
                                        reinterpret_cast<float *>(fd + s->off_tbox), reinterpret_cast<float4 *>(fd + s->off_tcent),
-                                       s->inst_blas.p, s->blas_roots.p, s->blas_wide_refs.p, /*inf_inactive=*/!small, s->stream));
+                                       s->inst_blas.p, s->blas_roots.p, s->blas_wide_refs.p, /*inf_inactive=*/!small, cs));
+        s->chain_stream[b] = cs;
         if (small) {
             // one workgroup: the LBVH TLAS over the live records, quads, slots, slot-ordered records (lbvh.hip)
             SmallTlasArgs a{};
@@ -604,12 +622,12 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
             a.root_wide = reinterpret_cast<TreeRoot *>(fd + s->off_root_wide);
             a.quads = reinterpret_cast<NodeQuad *>(fd + s->off_quads); a.slots = reinterpret_cast<uint32_t *>(fd + s->off_slots);
             a.hot_s = reinterpret_cast<InstHot *>(fd + s->off_hot_s); a.cold_s = reinterpret_cast<InstCold *>(fd + s->off_cold_s);
-            a.pair_count = s->gpu_counts.p + 1;
+            a.pair_count = s->gpu_counts.p + 2 + b;
             a.leaf_cap = s->tlas_leaf;
-            HIP_TRY(launch_tlas_small(a, s->stream));
+            HIP_TRY(launch_tlas_small(a, cs));
             s->block_by_slot[b] = s->inst_by_slot;
             s->frame_items[b] = live;
-            HIP_TRY(hipEventRecord(s->ev_copied[b], s->stream));
+            HIP_TRY(hipEventRecord(s->ev_copied[b], cs));
             s->r_copied[b] = s->ev_copied[b];
             s->active = b;
             s->frame = frame;
@@ -619,7 +637,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         HIP_TRY(s->tlas_builder->set_items(reinterpret_cast<const float *>(fd + s->off_tbox),
                                            reinterpret_cast<const float4 *>(fd + s->off_tcent)));
         HIP_TRY(s->tlas_builder->build(reinterpret_cast<NodePair *>(fd + s->off_pairs), reinterpret_cast<TreeRoot *>(fd + s->off_root),
-                                       s->gpu_counts.p + 1, s->stream));
+                                       s->gpu_counts.p + 2 + b, s->stream));
         HIP_TRY(s->tlas_builder->collapse_wide(reinterpret_cast<const NodePair *>(fd + s->off_pairs),
                                                reinterpret_cast<const TreeRoot *>(fd + s->off_root),
                                                reinterpret_cast<NodeQuad *>(fd + s->off_quads),
@@ -857,8 +875,8 @@ rt_status lbvh_sync_groups(rt_scene *s) {
     RT_TRY(drain(s));
     for (size_t g = 0; g < s->groups.size(); g++) {
         if (now[g] == s->lbvh_intact[g]) continue;
-        for (uint32_t m : s->groups[g].members) s->inst_dirty[m] = 1;
-        s->inst_dirty[s->inst.size() + g] = 1;
+        for (uint32_t m : s->groups[g].members) s->inst_dirty[m] = rt_scene::ALL_BLOCKS;
+        s->inst_dirty[s->inst.size() + g] = rt_scene::ALL_BLOCKS;
     }
     s->lbvh_intact = now;
     s->spare.release();                                   // re-sized with the next double-buffered build
@@ -944,7 +962,7 @@ rt_status gpu_setup_blas(rt_scene *s, const uint32_t *slot_count) {
     s->lbvh_intact.assign(s->groups.size(), 1);       // members start with the group's transform (frame 0 re-checks)
     s->spare.release();
     if ((st = lbvh_segments(s)) != RT_OK) return st;
-    if ((st = alloc_buf(s->gpu_counts, 2)) != RT_OK) return st;
+    if ((st = alloc_buf(s->gpu_counts, 2 + rt_scene::NLANE)) != RT_OK) return st;
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
     if (!s->r_done) s->r_done = s->ev_render_done;
     for (int q = 0; q < rt_scene::NLANE; q++) {       // "blas_double": every trace records its lane's event from now on
@@ -1309,11 +1327,11 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         if ((st = upload(s->blas_roots, roots)) != RT_OK) return st;
         if ((st = upload(s->blas_wide_refs, wide_refs)) != RT_OK) return st;
         if ((st = upload(s->inst_blas, ib)) != RT_OK) return st;
-        if ((st = alloc_buf(s->gpu_counts, 2)) != RT_OK) return st;
+        if ((st = alloc_buf(s->gpu_counts, 2 + rt_scene::NLANE)) != RT_OK) return st;
     }
     if (s->gpu_tlas()) {
-        if ((st = alloc_buf(s->inst_params, n)) != RT_OK) return st;
-        s->inst_dirty.assign(n, 1);                                 // frame 0 uploads every instance
+        if ((st = alloc_buf(s->inst_params, n * rt_scene::NLANE)) != RT_OK) return st;   // one copy per frame block
+        s->inst_dirty.assign(n, rt_scene::ALL_BLOCKS);              // each block's first frame uploads every record
         delete s->tlas_builder;
         s->tlas_builder = new LbvhBuilder();
         const std::vector<LbvhSeg> tseg{LbvhSeg{0u, (uint32_t)n, 0u, 0u, 0u, 0u, s->tlas_leaf, 0u}};
@@ -1704,8 +1722,14 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         copied_here = true;
     }
     // the frame block's upload: stream-ordered when this call enqueued it
-    if (!copied_here) HIP_TRY(hipStreamWaitEvent(stream, s->r_copied[s->active], 0));
-    if (zero_lane) HIP_TRY(hipMemsetAsync(lane_counters, 0, CNT_NUM * sizeof(unsigned long long), stream));
+    if (!copied_here && !(s->gpu_tlas() && s->chain_stream[s->active] == stream))   // else built on this stream
+        HIP_TRY(hipStreamWaitEvent(stream, s->r_copied[s->active], 0));
+    if (zero_lane || (reset_queue && s->use_persistent)) {   // GPU-built frames: one small kernel instead of two fills
+        HIP_TRY(launch_frame_copy(nullptr, nullptr, 0, zero_lane ? lane_counters : nullptr,
+                                  reset_queue && s->use_persistent ? s->queue[q] : nullptr, stream));
+        zero_lane = false;
+        if (s->use_persistent) reset_queue = false;
+    }
     const uint32_t slot = s->ring_head;
     s->ring_head = (s->ring_head + 1) % rt_scene::RING;
     if (s->ring_pending < rt_scene::RING) s->ring_pending++;
@@ -2101,7 +2125,7 @@ rt_status rt_scene_update_triangles(rt_scene *s, size_t first, size_t count, con
         in.centroid = in.pcount == 1 ? prim_centroid(s, in.ptype, in.pindex)
                                      : hm::v3((float)(c[0] / in.pcount), (float)(c[1] / in.pcount), (float)(c[2] / in.pcount));
         instance_update(in, in.x);
-        if (s->gpu_tlas()) s->inst_dirty[i] = 1;     // the GPU copy of its local box
+        if (s->gpu_tlas()) s->inst_dirty[i] = rt_scene::ALL_BLOCKS;     // the GPU copies of its local box
     }
     for (size_t g = 0; g < s->groups.size(); g++) {   // option "group" (LBVH): the union of the members' boxes
         InstGroup &G = s->groups[g];
@@ -2112,7 +2136,7 @@ rt_status rt_scene_update_triangles(rt_scene *s, size_t first, size_t count, con
             for (int a = 0; a < 3; a++) c[a] += m.centroid[a];
         }
         G.st.centroid = hm::v3((float)(c[0] / G.members.size()), (float)(c[1] / G.members.size()), (float)(c[2] / G.members.size()));
-        if (s->gpu_tlas()) s->inst_dirty[s->inst.size() + g] = 1;
+        if (s->gpu_tlas()) s->inst_dirty[s->inst.size() + g] = rt_scene::ALL_BLOCKS;
     }
     s->blas_dirty = true;
     return RT_OK;
@@ -2138,7 +2162,7 @@ rt_status rt_scene_update_instances(rt_scene *s, size_t first, size_t count, con
             in.centroid = hm::of(d[k].local_centroid);
         }
         instance_update(in, d[k].xform);
-        if (s->gpu_tlas()) s->inst_dirty[i] = 1;
+        if (s->gpu_tlas()) s->inst_dirty[i] = rt_scene::ALL_BLOCKS;
         // option "group": the group's box and transform were taken at the build; its members go back to
         // their own TLAS items for good
         if (s->group_of[i]) s->groups[s->group_of[i] - 1].valid = false;
@@ -2165,10 +2189,10 @@ rt_status rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
     info->tlas_node_pairs = s->tlas_flat.pairs.size();
     if (s->gpu_tlas() && s->built) {                 // GPU-built TLAS: read the last frame's count / root
         HIP_TRY(hipSetDevice(s->device));
-        HIP_TRY(hipStreamSynchronize(s->stream));
+        HIP_TRY(hipDeviceSynchronize());        // the frame's TLAS may have been built on a lane stream
         uint32_t np = 0;
         TreeRoot root{};
-        HIP_TRY(hipMemcpy(&np, s->gpu_counts.p + 1, sizeof np, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&np, s->gpu_counts.p + 2 + s->active, sizeof np, hipMemcpyDeviceToHost));
         HIP_TRY(hipMemcpy(&root, s->frame_dev[s->active] + s->off_root, sizeof root, hipMemcpyDeviceToHost));
         info->tlas_node_pairs = np;
         info->tlas_height = root.height;
@@ -2274,7 +2298,7 @@ rt_status rt_scene_export_tlas(const rt_scene *s, float *boxes, uint32_t *ci, ui
     Tree gpu_tree;
     if (s->gpu_tlas()) {
         HIP_TRY(hipSetDevice(s->device));
-        HIP_TRY(hipStreamSynchronize(s->stream));
+        HIP_TRY(hipDeviceSynchronize());        // the frame's TLAS may have been built on a lane stream
         const uint8_t *fd = s->frame_dev[s->active];
         TreeRoot root{};
         std::vector<NodePair> pairs;

@@ -1428,7 +1428,9 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
         atomicAdd(&counters[CNT_RAYS], (unsigned long long)wr);
         atomicAdd(&counters[CNT_PIXELS], (unsigned long long)wp);
         if (out.timeline) {
-            unsigned long long *w = out.timeline + (unsigned long long)TIMELINE_WORDS * (blockIdx.x * (BLOCK / 64) + (threadIdx.x >> 6));
+            // the wave's index from its stack window address (threadIdx.x kept live to here was spilled)
+            const uint32_t wv = (uint32_t)((const unsigned long long *)T.stk.lds - &lds_stack[0][0]) >> 6;
+            unsigned long long *w = out.timeline + (unsigned long long)TIMELINE_WORDS * (blockIdx.x * (BLOCK / 64) + wv);
             w[0] = t_start;
             w[1] = __builtin_amdgcn_s_memrealtime();
             w[2] = ((unsigned long long)hw_id() << 32) | xcc;
