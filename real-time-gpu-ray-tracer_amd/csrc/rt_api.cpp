@@ -310,6 +310,11 @@ struct rt_scene {
     // RT_BUILD_LBVH: GPU builders and the raw caller primitives they read
     LbvhBuilder *blas_builder = nullptr, *tlas_builder = nullptr;
     DevBuf<rt_triangle> raw_tris;
+    // rt_scene_update_triangles: the new triangles are staged in pinned memory and copied on the scene stream,
+    // behind the BLAS builds that read raw_tris (the only readers) and without waiting for any trace
+    rt_triangle *raw_stage = nullptr;
+    size_t raw_stage_cap = 0;
+    hipEvent_t ev_raw_staged = nullptr;            // the last staged copy finished (raw_stage reusable)
     DevBuf<rt_sphere> raw_sph;
     DevBuf<rt_parallelogram> raw_quad;
     DevBuf<TreeRoot> blas_roots;        // per segment the builder holds (seg_of_blas)
@@ -406,6 +411,8 @@ struct rt_scene {
         }
         if (ev_render_done) (void)hipEventDestroy(ev_render_done);
         if (ev_blas_built) (void)hipEventDestroy(ev_blas_built);
+        if (ev_raw_staged) (void)hipEventDestroy(ev_raw_staged);
+        if (raw_stage) (void)hipHostFree(raw_stage);
         for (int b = 0; b < NLANE; b++) {
             if (staging[b]) (void)hipHostFree(staging[b]);
             if (frame_dev[b]) (void)hipFree(frame_dev[b]);
@@ -2105,9 +2112,21 @@ rt_status rt_scene_update_triangles(rt_scene *s, size_t first, size_t count, con
     for (size_t k = 0; k < count; k++) material_slot(s, tris[k].material_type, tris[k].material_index, ok);
     if (!ok) return fail(RT_ERR_INVALID_ARGUMENT, "triangle references a material out of range");
     HIP_TRY(hipSetDevice(s->device));
-    RT_TRY(drain(s));        // a pending BLAS build may still read the raw array
+    // no drain: traces never read raw_tris, and the copy is ordered behind the scene stream's pending BLAS
+    // builds (the next build, which the frame update enqueues after it, reads the new triangles)
+    if (s->ev_raw_staged) RT_TRY(wait_event(s, s->ev_raw_staged));      // the previous staged copy is done
+    else HIP_TRY(hipEventCreateWithFlags(&s->ev_raw_staged, hipEventDisableTiming));
+    if (count > s->raw_stage_cap) {
+        if (s->raw_stage) HIP_TRY(hipHostFree(s->raw_stage));
+        s->raw_stage = nullptr;
+        s->raw_stage_cap = 0;
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->raw_stage), count * sizeof(rt_triangle), hipHostMallocDefault));
+        s->raw_stage_cap = count;
+    }
+    std::memcpy(s->raw_stage, tris, count * sizeof(rt_triangle));
     std::memcpy(s->tris.data() + first, tris, count * sizeof(rt_triangle));
-    HIP_TRY(hipMemcpy(s->raw_tris.p + first, tris, count * sizeof(rt_triangle), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(s->raw_tris.p + first, s->raw_stage, count * sizeof(rt_triangle), hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(hipEventRecord(s->ev_raw_staged, s->stream));
     // instance boxes derived from the triangles (RenderPin.cu:124-139); VTK-style bounds stay as given
     for (size_t i = 0; i < s->inst.size(); i++) {
         InstState &in = s->inst[i];

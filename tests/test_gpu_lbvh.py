@@ -172,6 +172,45 @@ def test_update_triangles_rebuilds(gpu_lib):
     assert np.array_equal(after, fresh.render(0, want_rgb=True)[1])
 
 
+@pytest.mark.parametrize("group", [1, 0])
+def test_update_triangles_pipelined_frames(gpu_lib, group):
+    """Deforming geometry without a device drain: each frame moves the particles' triangles and is launched on
+    one of three overlapped lanes without waiting; every frame equals the same sequence rendered synchronously
+    (the staged triangle copy is ordered behind the BLAS builds that read the array, never behind traces)."""
+    import torch
+    s = scenes.demo_with_particles(8)
+    n_p = 8 * 1024
+    W, H, F, L = 256, 144, 9, 3
+
+    def deform(f):
+        t = s.triangles[:n_p].copy()
+        t["vertex"] += np.asarray([0.02 * f, 0.01 * (f % 3), -0.015 * f], np.float32)
+        return t
+
+    ref_r = Renderer(s).set_option("group", group).build_acceleration_structure(0, mode="lbvh").configure_camera(
+        W, H, ray_trace_depth=2)
+    ref = []
+    for f in range(F):
+        ref_r.update_triangles(0, deform(f))
+        ref.append(ref_r.render(f)[0])
+    ref_r.cleanup()
+    assert not np.array_equal(ref[0], ref[F - 1])
+    r = Renderer(s).set_option("group", group).build_acceleration_structure(0, mode="lbvh").configure_camera(
+        W, H, ray_trace_depth=2)
+    r.set_option("overlap", L)
+    lanes = [torch.cuda.Stream() for _ in range(L)]
+    bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(F)]
+    torch.cuda.synchronize()
+    for f in range(F):
+        r.update_triangles(0, deform(f))
+        r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=lanes[f % L].cuda_stream, sync=False)
+    r.synchronize()
+    torch.cuda.synchronize()
+    for f in range(F):
+        assert np.array_equal(bufs[f].cpu().numpy().reshape(H, W, 4), ref[f]), f
+    r.cleanup()
+
+
 def test_update_triangles_needs_lbvh(gpu_lib):
     s = scenes.demo_with_particles(2)
     r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(32, 32)
