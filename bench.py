@@ -70,6 +70,10 @@ def parse():
     p.add_argument("--clock-warmup", type=float, default=0.5,
                    help="seconds of untimed frames before the W warm-up steps (the GPU's clocks ramp up under load)")
     p.add_argument("--print-pmc-tag", action="store_true", help="print this run's PMC tag as JSON and exit (no GPU)")
+    p.add_argument("--skip-update", action="store_true",
+                   help="diagnostic: timed frames reuse the last frame block (no host update / upload); images are stale")
+    p.add_argument("--launch-times", default=None,
+                   help="write the timed launches' (start, stop) ms, relative to the first start, to this .npy (diagnostic)")
     return p.parse_args()
 
 
@@ -197,7 +201,9 @@ def main():
     # ms/frame, C4 0.090 -> 0.054; profiles/r02_sweep_lanes8b.jsonl, r02_sweep_lanes8c.jsonl), while a
     # whole frame on one GPU is best with 3 lanes and the default 4 queues.  Set before HIP initialises.
     share = n > 1 or args.shard is not None
-    if share and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 12:
+    if os.environ.get("RTAMD_HWQ"):                    # A/B studies: an explicit queue count
+        os.environ["GPU_MAX_HW_QUEUES"] = os.environ["RTAMD_HWQ"]
+    elif share and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 12:
         os.environ["GPU_MAX_HW_QUEUES"] = "12"      # (the pool's boxes export 4, HIP's default)
 
     import numpy as np
@@ -255,7 +261,7 @@ def main():
 
     host_update = []                                       # (update_ms, part of it waiting on the GPU) per call
 
-    def step(frame, sync=True, keep=False, one_stream=False):
+    def step(frame, sync=True, keep=False, one_stream=False, skip=False):
         """One frame; sync=False pipelines it (host TLAS build of the next frame overlaps the GPU).
         With "overlap", frame k runs on lanes[k % L] (its own trace -> gather -> assemble chain);
         one_stream: every frame on the first lane's stream (launches serialised back to back)."""
@@ -264,7 +270,7 @@ def main():
         fb = frame_bufs[b]
         t_call = time.perf_counter()
         _, _, sts = r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=fb.data_ptr() if fb is not None else None,
-                             stream=st, sync=sync, keep_counters=keep, tiles=tiles)
+                             stream=st, sync=sync, keep_counters=keep, tiles=tiles, skip_update=skip)
         host_update.append((sts["update_ms"], sts["update_wait_ms"], (time.perf_counter() - t_call) * 1e3))
 
     # clock warm-up: the GPU's clocks ramp up over the first ~0.1-0.5 s of load (measured: serialised C2 launches
@@ -297,13 +303,15 @@ def main():
     host_update.clear()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(args.warmup + k, sync=False, keep=True)      # counters were zeroed by collect()
+        step(args.warmup + k, sync=False, keep=True, skip=args.skip_update)   # counters were zeroed by collect()
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     timed_update = np.asarray(host_update[:args.steps], dtype=np.float64).reshape(-1, 3)
+    if args.launch_times and rank == 0:                    # before collect() empties the library's ring
+        np.save(args.launch_times, r.debug_read("launch_times").view(np.float32).reshape(-1, 2))
     acc, kernel_ms = r.collect()                           # device counters + HIP-event kernel times
     rays = int(acc["rays"])
     assert len(kernel_ms) == args.steps, (len(kernel_ms), args.steps)
@@ -411,6 +419,8 @@ def main():
             # close to ms_per_step the frame rate is bound by the host's per-frame work, not by the GPU
             "host_call_ms_median": round(float(np.median(timed_update[:, 2])), 4),
             "host_busy_ms_median": round(float(np.median(timed_update[:, 2] - timed_update[:, 1])), 4),
+            "host_call_ms_mean": round(float(np.mean(timed_update[:, 2])), 4),
+            "host_update_wait_ms_mean": round(float(np.mean(timed_update[:, 1])), 4),
             "kernel_ms": round(serial_kernel_ms, 4),
             "kernel_ms_overlapped": round(avg_kernel_ms, 4),
             "kernel_ms_sync": round(sync_kernel_ms, 4),

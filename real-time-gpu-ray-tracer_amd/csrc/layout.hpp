@@ -182,8 +182,11 @@ struct SceneGPU {
     uint32_t lds_bq0, lds_bqn, lds_bq_at;
 };
 constexpr uint32_t LDS_NONE = 0xFFFFFFFFu;
-constexpr uint32_t LDS_SCENE_F4 = 1216;    // 19 KB per workgroup: 32 KB stack + 1 KB materials + 19 KB keeps 3
-                                           // workgroups per CU (160 KB)
+#ifndef RT_LDS_SCENE_F4
+#define RT_LDS_SCENE_F4 1216
+#endif
+constexpr uint32_t LDS_SCENE_F4 = RT_LDS_SCENE_F4;   // 19 KB per workgroup: 32 KB stack + 1 KB materials + 19 KB
+                                                     // keeps 3 workgroups per CU (160 KB)
 constexpr uint32_t LDS_QUAD_F4 = 7, LDS_INST_F4 = 5, LDS_ICOLD_F4 = 6, LDS_QPRIM_F4 = 5;
 
 struct CameraGPU {                  // Camera (RendererImpl.cuh:32-61), precomputed on host

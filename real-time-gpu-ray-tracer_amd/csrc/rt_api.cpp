@@ -210,11 +210,18 @@ struct rt_scene {
     static_assert(NLANE <= 8, "inst_dirty holds one bit per frame block");
     hipStream_t chain_stream[NLANE] = {};         // GPU-built frame b's records / TLAS were built on this stream
     hipEvent_t ev_blas_built = nullptr;           // a GPU BLAS build on the scene stream finished
-    uint8_t *staging[NLANE] = {};                 // pinned host
-    uint8_t *staging_dev[NLANE] = {};             // the same, as device-visible pointers
-    int pending_copy = -1;                        // rt_render: block whose upload the next launch performs
+    // pinned host staging, cycled independently of the frame blocks and twice as deep: a frame's staging is
+    // reusable once its upload ran, which rt_render can only tell by the trace's completion event (a record
+    // right after the copy kernel would idle the GPU ~5 us) — with one staging per block, the host waited for
+    // frame k-8's whole trace before it could stage frame k (8 lanes of 1/8-frame shares: 0.12 ms lane gaps)
+    static constexpr int NSTAGE = 2 * NLANE;
+    uint8_t *staging[NSTAGE] = {};
+    uint8_t *staging_dev[NSTAGE] = {};            // the same, as device-visible pointers
+    hipEvent_t r_staged[NSTAGE] = {};             // staging[i] no longer read (null: never used)
+    int stage_next = 0;
+    int pending_copy = -1, pending_stage = -1;    // rt_render: block (and its staging) whose upload the next launch performs
     uint8_t *frame_dev[NLANE] = {};               // HBM
-    hipEvent_t ev_copied[NLANE] = {};             // upload from staging[b] finished
+    hipEvent_t ev_copied[NLANE] = {};             // frame block b uploaded / built
     hipEvent_t ev_used[NLANE] = {};               // last kernel reading frame_dev[b] finished
     // What the waits below use: the event last recorded for each purpose.  A trace launch records one event
     // after it (its ring_stop timing event, or one event after a multi-GPU gather) and points every purpose
@@ -379,6 +386,7 @@ struct rt_scene {
         for (int q = 0; q < NLANE; q++) r_lane[q] = ev_lane_done[q];
         r_done = nullptr;
         for (int b = 0; b < NLANE; b++) { r_copied[b] = ev_copied[b]; r_used[b] = ev_used[b]; }
+        for (hipEvent_t &e : r_staged) e = nullptr;     // drained: every staging buffer is free
     }
 
     ~rt_scene() {
@@ -413,8 +421,9 @@ struct rt_scene {
         if (ev_blas_built) (void)hipEventDestroy(ev_blas_built);
         if (ev_raw_staged) (void)hipEventDestroy(ev_raw_staged);
         if (raw_stage) (void)hipHostFree(raw_stage);
+        for (int i = 0; i < NSTAGE; i++)
+            if (staging[i]) (void)hipHostFree(staging[i]);
         for (int b = 0; b < NLANE; b++) {
-            if (staging[b]) (void)hipHostFree(staging[b]);
             if (frame_dev[b]) (void)hipFree(frame_dev[b]);
             if (ev_copied[b]) (void)hipEventDestroy(ev_copied[b]);
             if (ev_used[b]) (void)hipEventDestroy(ev_used[b]);
@@ -550,7 +559,9 @@ rt_status drain(rt_scene *s) {
 rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool defer = false) {
     const int b = s->active < 0 ? 0 : (s->active + 1) % rt_scene::NLANE;
     const auto w0 = std::chrono::steady_clock::now();
-    RT_TRY(wait_event(s, s->r_copied[b]));             // staging[b] no longer read by a pending copy
+    const int si = s->stage_next;                      // this frame's staging buffer
+    s->stage_next = (si + 1) % rt_scene::NSTAGE;
+    if (s->r_staged[si]) RT_TRY(wait_event(s, s->r_staged[si]));   // no longer read by a pending copy
     s->update_wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     if (s->update) {                                  // Renderer.cu:269
         std::vector<rt_xform> xs(s->inst.size());
@@ -564,7 +575,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
                 else instance_update(s->inst[i], xs[i]);
             }
     }
-    uint8_t *st = s->staging[b];
+    uint8_t *st = s->staging[si];
     InstHot *hot = reinterpret_cast<InstHot *>(st + s->off_hot);
     InstCold *cold = reinterpret_cast<InstCold *>(st + s->off_cold);
     if (s->gpu_tlas()) {
@@ -613,7 +624,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         if (s->r_used[b]) HIP_TRY(hipStreamWaitEvent(cs, s->r_used[b], 0));      // block b no longer read
         // Instance::updateTransformArguments for every record of block b, on the GPU, with its BLAS root
         // (instances.hip); the deltas are read from the pinned staging block directly
-        HIP_TRY(launch_instance_update(reinterpret_cast<const InstDelta *>(s->staging_dev[b] + s->off_delta), nd,
+        HIP_TRY(launch_instance_update(reinterpret_cast<const InstDelta *>(s->staging_dev[si] + s->off_delta), nd,
                                        s->inst_params.p + (size_t)b * n, n,
                                        reinterpret_cast<InstHot *>(fd + s->off_hot), reinterpret_cast<InstCold *>(fd + s->off_cold),
                                        reinterpret_cast<float *>(fd + s->off_tbox), reinterpret_cast<float4 *>(fd + s->off_tcent),
@@ -635,7 +646,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
             s->block_by_slot[b] = s->inst_by_slot;
             s->frame_items[b] = live;
             HIP_TRY(hipEventRecord(s->ev_copied[b], cs));
-            s->r_copied[b] = s->ev_copied[b];
+            s->r_copied[b] = s->r_staged[si] = s->ev_copied[b];
             s->active = b;
             s->frame = frame;
             return RT_OK;
@@ -659,7 +670,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
             s->block_by_slot[b] = true;
         }
         HIP_TRY(hipEventRecord(s->ev_copied[b], s->stream));
-        s->r_copied[b] = s->ev_copied[b];
+        s->r_copied[b] = s->r_staged[si] = s->ev_copied[b];
         s->active = b;
         s->frame = frame;
         return RT_OK;
@@ -717,10 +728,11 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
     HIP_TRY(hipStreamWaitEvent(upload, s->r_used[b], 0));            // frame_dev[b] free on device
     if (defer) {
         s->pending_copy = b;
+        s->pending_stage = si;
     } else {
         HIP_TRY(hipMemcpyAsync(s->frame_dev[b], st, s->frame_block, hipMemcpyHostToDevice, upload));
         HIP_TRY(hipEventRecord(s->ev_copied[b], upload));
-        s->r_copied[b] = s->ev_copied[b];
+        s->r_copied[b] = s->r_staged[si] = s->ev_copied[b];
     }
     s->active = b;
     s->frame = frame;
@@ -1345,11 +1357,15 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         HIP_TRY(s->tlas_builder->init(tseg, s->stream));
         s->tlas_builder->size_classes_ = s->tlas_size_classes;
     }
+    for (int i = 0; i < rt_scene::NSTAGE; i++) {
+        if (s->staging[i]) { (void)hipHostFree(s->staging[i]); s->staging[i] = nullptr; }
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->staging[i]), s->frame_block, hipHostMallocDefault));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s->staging_dev[i]), s->staging[i], 0));
+        s->r_staged[i] = nullptr;
+    }
+    s->stage_next = 0;
     for (int b = 0; b < rt_scene::NLANE; b++) {
-        if (s->staging[b]) { (void)hipHostFree(s->staging[b]); s->staging[b] = nullptr; }
         if (s->frame_dev[b]) { (void)hipFree(s->frame_dev[b]); s->frame_dev[b] = nullptr; }
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->staging[b]), s->frame_block, hipHostMallocDefault));
-        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s->staging_dev[b]), s->staging[b], 0));
         HIP_TRY(hipMalloc(reinterpret_cast<void **>(&s->frame_dev[b]), s->frame_block));
         if (!s->ev_copied[b]) HIP_TRY(hipEventCreateWithFlags(&s->ev_copied[b], hipEventDisableTiming));
         if (!s->ev_used[b]) HIP_TRY(hipEventCreateWithFlags(&s->ev_used[b], hipEventDisableTiming));
@@ -1666,7 +1682,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     // ... of this frame block: no event between the copy and the trace (each event record between two kernels
     // of a stream costs ~4.5 us of GPU idle: copy -> trace gap 10.6 -> 6.1 us, profiles/r02_gaps.txt); its
     // r_copied is the trace's completion event (the host waits on it only before reusing the staging buffer)
-    int copied_block = -1;
+    int copied_block = -1, copied_stage = -1;
     if (s->use_persistent && s->reorder && s->grab == 64u) {
         DevBuf<uint32_t> &unit_cost = s->unit_cost[q], &unit_order = s->unit_order[q];
         if (unit_cost.n < 2 * (size_t)out.units) {        // [recorded costs | costs of the last launch (debug)]
@@ -1703,11 +1719,12 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             HIP_TRY(launch_schedule(unit_cost.p, unit_cost.p + out.units, unit_order.p, s->queue[q], rows, upr, out.queue_parts,
                                     do_order, s->split & 0xFFu, (s->split >> 8) & 0xFFu, s->merge,
                                     pc >= 0 ? s->frame_dev[pc] : nullptr,
-                                    pc >= 0 ? s->staging_dev[pc] : nullptr, pc >= 0 ? s->frame_block : 0,
+                                    pc >= 0 ? s->staging_dev[s->pending_stage] : nullptr, pc >= 0 ? s->frame_block : 0,
                                     zero_lane ? lane_counters : nullptr, stream));
             zero_lane = false;
             copied_here = pc >= 0;
             copied_block = pc;
+            copied_stage = s->pending_stage;
             s->pending_copy = -1;
             if (do_order) s->order_ok[q] = true;
             reset_queue = false;
@@ -1719,10 +1736,11 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         out.cost_max = s->cost_max;
     }
     if (s->pending_copy >= 0) {                // the frame block's upload (and the lane's counter / queue reset)
-        HIP_TRY(launch_frame_copy(s->frame_dev[s->pending_copy], s->staging_dev[s->pending_copy], s->frame_block,
+        HIP_TRY(launch_frame_copy(s->frame_dev[s->pending_copy], s->staging_dev[s->pending_stage], s->frame_block,
                                   zero_lane ? lane_counters : nullptr, reset_queue && s->use_persistent ? s->queue[q] : nullptr,
                                   stream));
         copied_block = s->pending_copy;
+        copied_stage = s->pending_stage;
         s->pending_copy = -1;
         zero_lane = false;
         reset_queue = false;
@@ -1793,7 +1811,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         done = s->ring_post[slot];                              // staging / block waits must see this launch)
     }
     s->r_used[s->active] = s->r_done = s->r_lane[q] = done;
-    if (copied_block >= 0) s->r_copied[copied_block] = done;
+    if (copied_block >= 0) s->r_copied[copied_block] = s->r_staged[copied_stage] = done;
     if (s->ev_blas_lane[q]) HIP_TRY(hipEventRecord(s->ev_blas_lane[q], stream));   // "blas_double": this set's reader
     if (o.flags & RT_RENDER_NO_SYNC) {
         if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; stats->update_wait_ms = s->update_wait_ms; }
@@ -1993,6 +2011,24 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
     } else if (k == "costmap") {
         src = s->costmap.p;
         size = s->costmap_pixels * sizeof(uint32_t);
+    } else if (k == "launch_times") {
+        // the trace launches not yet collected (rt_scene_collect), oldest first: (start, stop) in ms relative to
+        // the first one's start, as float pairs — how lanes' launches interleave (scripts/lane_timeline.py)
+        HIP_TRY(hipSetDevice(s->device));
+        RT_TRY(drain(s));
+        const uint32_t n = s->ring_pending;
+        *bytes = (size_t)n * 2 * sizeof(float);
+        if (capacity) {
+            if (capacity < *bytes) return fail(RT_ERR_INVALID_ARGUMENT, "buffer too small");
+            float *o = static_cast<float *>(dst);
+            const uint32_t first = (s->ring_head + rt_scene::RING - n) % rt_scene::RING;
+            for (uint32_t j = 0; j < n; j++) {
+                const uint32_t slot = (first + j) % rt_scene::RING;
+                HIP_TRY(hipEventElapsedTime(&o[2 * j], s->ring_start[first], s->ring_start[slot]));
+                HIP_TRY(hipEventElapsedTime(&o[2 * j + 1], s->ring_start[first], s->ring_stop[slot]));
+            }
+        }
+        return RT_OK;
     } else if (k == "instances") {
         // GPU-built frames: the instance records the GPU computed for the current frame, in instance order,
         // 45 floats each: inverse, forward, inverse-transpose rows 1-3 (12 each), transformed box, centroid

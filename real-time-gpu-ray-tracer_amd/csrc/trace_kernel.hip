@@ -51,7 +51,7 @@ constexpr int BLOCK = 256;              // 4 waves; each wave owns one 8x8 pixel
 #endif
 constexpr int LDS_DEPTH = RT_LDS_DEPTH;         // per-lane stack entries kept in LDS
 constexpr int LDS_MATERIALS = RT_LDS_MATERIALS; // persistent kernel: material table in LDS up to this many slots
-constexpr int SPILL_DEPTH = 48;         // overflow entries in scratch (max depth 64 = reference)
+constexpr int SPILL_DEPTH = 64 - LDS_DEPTH;   // overflow entries in scratch (max depth 64 = reference)
 #ifndef RT_CHAIN_ROOT_LEAF
 #define RT_CHAIN_ROOT_LEAF 1            // quad trees: an entered instance whose BLAS root is a leaf (a sphere, a
                                         // parallelogram, a small mesh) has it tested in the same leaf round
