@@ -237,6 +237,10 @@ def main():
     overlap = L > 1
     if overlap:
         r.set_option("overlap", L)
+    if share:
+        # the host stages frame k once frame k - depth's trace is done: 64 lets it run 8 frames ahead per lane
+        # (C2 1/8 share 0.0446 -> 0.0432 ms/frame, C4 equal; profiles/r03_session2/stage_depth.jsonl)
+        r.set_option("stage_depth", 64)
     info = r.info()
     stream = torch.cuda.current_stream().cuda_stream
     # "overlap": frame k runs on lanes[k % L]; each lane is a self-contained trace -> gather -> assemble chain

@@ -214,7 +214,9 @@ struct rt_scene {
     // reusable once its upload ran, which rt_render can only tell by the trace's completion event (a record
     // right after the copy kernel would idle the GPU ~5 us) — with one staging per block, the host waited for
     // frame k-8's whole trace before it could stage frame k (8 lanes of 1/8-frame shares: 0.12 ms lane gaps)
-    static constexpr int NSTAGE = 2 * NLANE;
+    // option "stage_depth" (default 2 x NLANE): buffers in the cycle, allocated on first use
+    static constexpr int NSTAGE = 8 * NLANE;
+    int stage_depth = 2 * NLANE;
     uint8_t *staging[NSTAGE] = {};
     uint8_t *staging_dev[NSTAGE] = {};            // the same, as device-visible pointers
     hipEvent_t r_staged[NSTAGE] = {};             // staging[i] no longer read (null: never used)
@@ -559,9 +561,13 @@ rt_status drain(rt_scene *s) {
 rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool defer = false) {
     const int b = s->active < 0 ? 0 : (s->active + 1) % rt_scene::NLANE;
     const auto w0 = std::chrono::steady_clock::now();
-    const int si = s->stage_next;                      // this frame's staging buffer
-    s->stage_next = (si + 1) % rt_scene::NSTAGE;
+    const int si = s->stage_next % s->stage_depth;      // this frame's staging buffer
+    s->stage_next = (si + 1) % s->stage_depth;
     if (s->r_staged[si]) RT_TRY(wait_event(s, s->r_staged[si]));   // no longer read by a pending copy
+    if (!s->staging[si]) {
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->staging[si]), s->frame_block, hipHostMallocDefault));
+        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s->staging_dev[si]), s->staging[si], 0));
+    }
     s->update_wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     if (s->update) {                                  // Renderer.cu:269
         std::vector<rt_xform> xs(s->inst.size());
@@ -1358,9 +1364,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         s->tlas_builder->size_classes_ = s->tlas_size_classes;
     }
     for (int i = 0; i < rt_scene::NSTAGE; i++) {
-        if (s->staging[i]) { (void)hipHostFree(s->staging[i]); s->staging[i] = nullptr; }
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->staging[i]), s->frame_block, hipHostMallocDefault));
-        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s->staging_dev[i]), s->staging[i], 0));
+        if (s->staging[i]) { (void)hipHostFree(s->staging[i]); s->staging[i] = nullptr; }   // frame_update allocates
+        s->staging_dev[i] = nullptr;
         s->r_staged[i] = nullptr;
     }
     s->stage_next = 0;
@@ -1905,6 +1910,12 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "queue_parts") {
         if (value < 1 || value > (int64_t)QUEUE_MAX_PARTS) return fail(RT_ERR_INVALID_ARGUMENT, "queue_parts must be in 1..8");
         s->queue_parts = (uint32_t)value;
+    } else if (k == "stage_depth") {
+        // pinned staging buffers the host cycles through: it stages frame k once frame k - depth's trace is done
+        if (value < 2 || value > rt_scene::NSTAGE) return fail(RT_ERR_INVALID_ARGUMENT, "stage_depth must be in 2..64");
+        RT_TRY(drain(s));
+        s->stage_depth = (int)value;
+        s->stage_next = 0;
     } else if (k == "nt_store") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "nt_store must be 0 or 1");
         s->nt_store = (uint32_t)value;
