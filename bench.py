@@ -284,10 +284,11 @@ def main():
     k = 0
     # --overlap 1: every launch of the run is serialised, and the roofline is priced on all of them (the set a
     # rocprofv3 --stats average of this very command covers); the library's timing ring holds 256 launches
-    pre_ms = []
+    pre_ms, pre_frames = [], []                            # ... with the frame each launch rendered
     while args.clock_warmup > 0:
         for _ in range(16):                                # chunks of 16 frames; ranks stop together (rank 0 decides)
             step(k % 1000, sync=False)
+            pre_frames.append(k % 1000)
             k += 1
         torch.cuda.synchronize()
         pre_ms += list(r.collect()[1])
@@ -296,8 +297,9 @@ def main():
             dist.broadcast(done, src=0)
         if done.item() > 0:
             break
-    for f in range(args.warmup):
-        step(f)
+    for f in range(args.warmup):                           # pipelined like the timed steps (and in the timing ring)
+        step(f, sync=False)
+        pre_frames.append(f)
     torch.cuda.synchronize()
     if n > 1:
         dist.barrier()
@@ -353,10 +355,21 @@ def main():
     if n > 1:
         dist.barrier()
 
-    # untimed work-counting pass (same frame as the first timed step) for the roofline
+    # untimed work-counting passes for the roofline: the animation changes a frame's work (C3's launches vary
+    # 1.3-2.6 ms over the frames of one run), so every priced launch is priced with the work of the frame it
+    # rendered — one counting pass per distinct frame (all ranks run the same passes: a pass gathers too)
+    timed_frames = [args.warmup + k for k in range(args.steps)]
+    serial_frames = [args.warmup + args.steps + k for k in range(20)]
+    all_serial = not overlap                                 # every launch of the run was serialised
+    priced_frames = (pre_frames + timed_frames + serial_frames + serial_frames) if all_serial else serial_frames
+    assert not all_serial or len(priced_frames) == len(pre_ms) + len(kernel_ms) + len(serial_ms) + len(sync_ms), \
+        (len(pre_frames), len(pre_ms), len(kernel_ms), len(serial_ms), len(sync_ms))
+    work = {}
     torch.cuda.synchronize()
-    _, _, cst = r.render(args.warmup, exact=args.exact, want_rgba=False, count_work=True,
-                         rgba8_device=frame_buf.data_ptr() if frame_buf is not None else None, tiles=tiles, stream=stream)
+    for f in sorted(set(priced_frames + timed_frames)):
+        _, _, work[f] = r.render(f, exact=args.exact, want_rgba=False, count_work=True,
+                                 rgba8_device=frame_buf.data_ptr() if frame_buf is not None else None, tiles=tiles,
+                                 stream=stream)
     if n > 1:
         dist.barrier()
 
@@ -364,11 +377,14 @@ def main():
         avg_kernel_ms = float(np.mean(kernel_ms))            # timed region: launches overlap (L lanes)
         serial_kernel_ms = float(np.mean(serial_ms))         # the same kernel with no overlap partner, back to back
         sync_kernel_ms = float(np.mean(sync_ms))             # ... and after a host synchronisation each (latency frames)
-        all_serial = not overlap                             # every launch of the run was serialised
         if all_serial:
             every = list(pre_ms) + list(kernel_ms) + list(serial_ms) + list(sync_ms)
             serial_kernel_ms = float(np.mean(every))
-        bytes_launch = algorithmic_bytes(cst)
+        # mean over the priced launches of their frames' counted work
+        keys = ("rays", "pixels", "aabb_tests", "triangle_tests", "sphere_quad_tests", "quad_tests", "instance_visits", "hits")
+        cst = {k: float(np.mean([work[f][k] for f in priced_frames])) for k in keys}
+        bytes_launch = float(np.mean([algorithmic_bytes(work[f]) for f in priced_frames]))
+        bytes_timed = float(np.mean([algorithmic_bytes(work[f]) for f in timed_frames]))
         achieved = bytes_launch / (serial_kernel_ms * 1e-3) / 1e9
         kname = ("render_persistent_kernel" if args.kernel else "render_kernel") + ("<exact>" if args.exact else "<fast>")
         tag = pmc_tag(args)
@@ -437,7 +453,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 # the same bytes over the pipelined frame time (frames overlapped: ms_per_step), N = 1 only
-                "frac_throughput": (round(bytes_launch / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
+                "frac_throughput": (round(bytes_timed / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 4)
                                     if n == 1 and not shard else None),
                 "traffic": traffic,
                 "traffic_source": traffic_src,
@@ -452,8 +468,9 @@ def main():
                 "bytes_formula": "SURVEY 8(d): 32 aabb + 36 tri + 32 sphere/quad + 48 inst + 32 ray + 4 pixel",
                 "algorithmic_bytes_per_launch": int(bytes_launch),
                 "layout_bytes_per_launch": int(layout_bytes(cst)),
-                "work_per_launch": {k: int(cst[k]) for k in ("rays", "pixels", "aabb_tests", "triangle_tests",
-                                                             "sphere_quad_tests", "quad_tests", "instance_visits", "hits")},
+                "work_per_launch": {k: int(round(cst[k])) for k in keys},
+                "work_source": (f"RT_RENDER_COUNT_WORK pass of each priced launch's frame ({len(set(priced_frames))} "
+                                f"distinct frames, mean over the {len(priced_frames)} priced launches)"),
             },
             "cpu_baseline": None,
         }
