@@ -391,15 +391,21 @@ __global__ __launch_bounds__(BLOCK) void bottom_up_local_kernel(const LbvhSeg *s
     }
 }
 
-__global__ void bottom_up_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals,
-                                 const float *item_box, uint32_t n, const uint32_t *child, const uint32_t *parent,
-                                 const uint32_t *parent_leaf, const uint32_t *range, uint32_t *flag, float *nbox,
-                                 uint32_t *height, uint32_t *kept) {
-    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
-    if (p >= n) return;
-    const LbvhSeg S = segs[seg_of_sorted(keys, p)];
-    if (S.count <= LOCAL_MAX) return;                                  // bottom_up_local_kernel
-    uint32_t g = parent_leaf[p];
+// Large trees (> LOCAL_MAX items, e.g. C5's 10 M-triangle group BLAS): one workgroup per CHUNK consecutive sorted
+// items finishes, through LDS, every node whose item range lies inside its chunk (a node's range holds its own
+// index, so it has an LDS slot there) — nearly all nodes; a thread whose climb reaches a node crossing a chunk
+// edge records that arrival, and a second kernel climbs from each recorded arrival with the device-wide hand-off
+// described above (kernel boundary: the chunk-finished boxes are visible to it).
+// (One device-wide pass over all 10 M nodes took 1.7 ms per C5 rebuild: every level an agent-scope round trip.)
+constexpr uint32_t CHUNK = 1024;               // = the chunk kernel's workgroup: one thread per item
+__device__ __forceinline__ bool chunk_local(const uint32_t *range, uint32_t g) {
+    return range[2 * g] / CHUNK == range[2 * g + 1] / CHUNK;
+}
+
+// device-wide climb from node g (its range crosses a chunk edge): the hand-off described above
+__device__ __forceinline__ void climb_top(const LbvhSeg &S, uint32_t g, const uint32_t *vals, const float *item_box,
+                                          const uint32_t *child, const uint32_t *parent, const uint32_t *range,
+                                          uint32_t *flag, float *nbox, uint32_t *height, uint32_t *kept) {
     while (g != NONE) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // this lane's sc1 stores have landed
         if (atomicAdd(&flag[g], 1u) == 0u) return;
@@ -417,6 +423,94 @@ __global__ void bottom_up_kernel(const LbvhSeg *segs, const unsigned long long *
         __hip_atomic_store(height + g, keep ? h + 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         kept[g] = keep ? 1u : 0u;
         g = parent[g];
+    }
+}
+
+__global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *segs, const unsigned long long *keys,
+                                                                const uint32_t *vals, const float *item_box, uint32_t n,
+                                                                const uint32_t *child, const uint32_t *parent,
+                                                                const uint32_t *parent_leaf, const uint32_t *range,
+                                                                float *nbox, uint32_t *height, uint32_t *kept,
+                                                                uint32_t *frontier) {
+    __shared__ float sleaf[CHUNK * 6];          // the chunk's item boxes, in sorted order
+    __shared__ float sbox[CHUNK * 6];           // node boxes, at the node's own position
+    __shared__ uint32_t sheight[CHUNK];
+    __shared__ uint32_t sflag[CHUNK];
+    __shared__ uint32_t snode[CHUNK];
+    const uint32_t lo = blockIdx.x * CHUNK, p = lo + threadIdx.x;
+    sflag[threadIdx.x] = 0;
+    const bool big = p < n && segs[seg_of_sorted(keys, p)].count > LOCAL_MAX;   // else bottom_up_local_kernel
+    if (big) {
+        const float2 *src = reinterpret_cast<const float2 *>(item_box + 6 * (size_t)vals[p]);
+#pragma unroll
+        for (int k = 0; k < 3; k++) { const float2 v = src[k]; sleaf[6 * threadIdx.x + 2 * k] = v.x; sleaf[6 * threadIdx.x + 2 * k + 1] = v.y; }
+    }
+    __syncthreads();
+    if (big) {
+        const LbvhSeg S = segs[seg_of_sorted(keys, p)];
+        uint32_t g = parent_leaf[p];
+        bool first = false;                             // stopped as a node's first arrival
+        while (g != NONE && chunk_local(range, g)) {
+            const uint32_t l = S.item_base + (g - S.node_base) - lo;   // the node's own position in the chunk
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (atomicAdd(&sflag[l], 1u) == 0u) { first = true; break; }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            float b[6];
+            uint32_t h = 0;
+#pragma unroll
+            for (int c = 0; c < 2; c++) {                              // union_children's order
+                const uint32_t ch = child[2 * g + c];
+                const float *cb;
+                uint32_t chh = 0;
+                if (ch & LEAF_BIT) {                                   // sorted position = the leaf's item index
+                    cb = sleaf + 6 * ((ch & ~LEAF_BIT) - lo);
+                } else {                                               // inside the parent's range: this chunk
+                    const uint32_t lc = S.item_base + (ch - S.node_base) - lo;
+                    cb = sbox + 6 * lc;
+                    chh = sheight[lc];
+                }
+                if (c == 0) {
+#pragma unroll
+                    for (int k = 0; k < 6; k++) b[k] = cb[k];
+                } else {
+                    float t[6];
+#pragma unroll
+                    for (int k = 0; k < 6; k++) t[k] = cb[k];
+                    merge_into(b, t);
+                }
+                h = chh > h ? chh : h;
+            }
+            const uint32_t size = range[2 * g + 1] - range[2 * g] + 1u;
+#pragma unroll
+            for (int k = 0; k < 6; k++) sbox[6 * l + k] = b[k];
+            sheight[l] = size > S.leaf_cap ? h + 1u : 0u;
+            snode[l] = g;
+            g = parent[g];
+        }
+        if (!first && g != NONE) {                      // g's range crosses a chunk edge: an arrival for the top pass
+            const uint32_t k = atomicAdd(frontier, 1u);
+            frontier[1 + k] = g;
+        }
+    }
+    __syncthreads();
+    if (sflag[threadIdx.x] == 2u) {                                    // a node finished here
+        const uint32_t l = threadIdx.x, g = snode[l];
+#pragma unroll
+        for (int k = 0; k < 6; k++) nbox[6 * (size_t)g + k] = sbox[6 * l + k];
+        height[g] = sheight[l];
+        kept[g] = (range[2 * g + 1] - range[2 * g] + 1u) > segs[seg_of_sorted(keys, p)].leaf_cap ? 1u : 0u;
+    }
+}
+
+// the top pass: one climb per arrival the chunk pass recorded (frontier[0] = count, then crossing-node ids)
+__global__ void bottom_up_top_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals,
+                                     const float *item_box, const uint32_t *child, const uint32_t *parent,
+                                     const uint32_t *range, uint32_t *flag, float *nbox, uint32_t *height, uint32_t *kept,
+                                     const uint32_t *frontier) {
+    const uint32_t count = frontier[0];
+    for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < count; i += gridDim.x * BLOCK) {
+        const uint32_t g = frontier[1 + i];
+        climb_top(segs[seg_of_sorted(keys, range[2 * g])], g, vals, item_box, child, parent, range, flag, nbox, height, kept);
     }
 }
 
@@ -949,7 +1043,7 @@ static void dfree(T *&p) {
 void LbvhBuilder::release() {
     dfree(segs_); dfree(seg_of_); dfree(members_); dfree(own_box_); dfree(own_cent_); dfree(bounds_);
     dfree(k0_); dfree(k1_); dfree(v0_); dfree(v1_); dfree(child_); dfree(parent_); dfree(parent_leaf_);
-    dfree(range_); dfree(flag_); dfree(height_); dfree(nbox_); dfree(kept_); dfree(pidx_); dfree(front_); dfree(count_);
+    dfree(range_); dfree(flag_); dfree(height_); dfree(nbox_); dfree(kept_); dfree(pidx_); dfree(front_); dfree(count_); dfree(frontier_);
     last_count_ = nullptr;
     if (tmp_) (void)hipFree(tmp_);
     tmp_ = nullptr; tmp_bytes_ = 0;
@@ -1039,9 +1133,14 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
                        parent_leaf_, range_, flag_);
     hipLaunchKernelGGL(bottom_up_local_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, v1_, box_, child_, parent_,
                        parent_leaf_, range_, nbox_, height_, kept_);
-    if (max_count_ > LOCAL_MAX)
-        hipLaunchKernelGGL(bottom_up_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, box_, N, child_,
-                           parent_, parent_leaf_, range_, flag_, nbox_, height_, kept_);
+    if (max_count_ > LOCAL_MAX) {
+        if (!frontier_) LB_TRY(dalloc(frontier_, 1 + 2 * (size_t)NI));   // <= 2 arrivals per internal node
+        LB_TRY(hipMemsetAsync(frontier_, 0, sizeof(uint32_t), stream));
+        hipLaunchKernelGGL(bottom_up_chunk_kernel, dim3((N + CHUNK - 1) / CHUNK), dim3(CHUNK), 0, stream, segs_, k1_, v1_,
+                           box_, N, child_, parent_, parent_leaf_, range_, nbox_, height_, kept_, frontier_);
+        hipLaunchKernelGGL(bottom_up_top_kernel, dim3(256), dim3(BLOCK), 0, stream, segs_, k1_, v1_, box_, child_, parent_,
+                           range_, flag_, nbox_, height_, kept_, frontier_);
+    }
     LB_TRY(hipGetLastError());
     if (!pair_count) {                                // collapse_wide needs the count of this build's pairs
         if (!count_) LB_TRY(dalloc(count_, 1));

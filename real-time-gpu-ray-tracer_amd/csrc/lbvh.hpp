@@ -128,6 +128,7 @@ private:
     uint32_t *parent_leaf_ = nullptr;     // per sorted position
     uint32_t *range_ = nullptr;           // 2 per interior node: first, last sorted position
     uint32_t *flag_ = nullptr;            // arrival counters
+    uint32_t *frontier_ = nullptr;        // trees > LOCAL_MAX items: [count, arrivals at chunk-crossing nodes]
     uint32_t *height_ = nullptr;          // per interior node
     float *nbox_ = nullptr;               // 6 per interior node
     uint32_t *kept_ = nullptr, *pidx_ = nullptr;
