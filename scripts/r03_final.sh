@@ -17,7 +17,7 @@ run() {  # name timeout cmd...
   if [ $rc -ne 0 ]; then tail -5 "$OUT/$name.log"; exit $rc; fi
 }
 [ -z "$NO_TESTS" ] && run tests 900 python -u -m pytest tests -m gpu -q -rf --timeout 120 --timeout-method thread
-for spec in ${CONFIGS:-C2:sah C3:sah C4:sah C2:lbvh C5:lbvh:rebuild}; do
+for spec in ${CONFIGS:-C2:sah C3:sah C4:sah C2:lbvh C5:lbvh:rebuild C5:lbvh}; do
   IFS=: read -r cfg build rb <<< "$spec"
   tag="${cfg}_${build}${rb:+_rebuild}"
   args="--config $cfg --build $build ${rb:+--rebuild}"
