@@ -332,6 +332,9 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 (default 1; 0 = instance order, for A/B — results are identical)
  *   "reserve"   : with "overlap", the persistent grid leaves this many workgroup slots free (default 16, two
  *                 per XCD) so the next lanes' schedule / upload / GPU TLAS kernels start beside the running launch
+ *   "stage_depth": pinned host staging buffers the per-frame upload cycles through (2..64, default 16, allocated on
+ *                 first use): the host stages frame k once frame k - depth's trace is done, so a larger depth lets
+ *                 the host run further ahead of many overlapped lanes (drains the scene when changed)
  *   "blas_double": RT_BUILD_LBVH rebuilds (option "rebuild", rt_scene_update_triangles): 1 = write a spare BLAS
  *                 set and swap it in, so a frame's rebuild overlaps the previous frame's trace (default 1;
  *                 0 = one set, a rebuild waits for every lane's trace)
