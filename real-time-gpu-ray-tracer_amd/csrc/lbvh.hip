@@ -583,7 +583,7 @@ __device__ __forceinline__ uint32_t material_slot(uint32_t type, uint32_t index,
 }
 
 __global__ void gather_blas_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals, uint32_t n,
-                                   RawPrimsGPU raw, PrimOutGPU out, const uint32_t *members) {
+                                   RawPrimsGPU raw, PrimOutGPU out, const uint32_t *item_member) {
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
     if (p >= n) return;
     const LbvhSeg S = segs[seg_of_sorted(keys, p)];
@@ -607,15 +607,7 @@ __global__ void gather_blas_kernel(const LbvhSeg *segs, const unsigned long long
         C.material = material_slot(t.material_type, t.material_index, raw.rough_count);
         C.orig_index = prim;
         C.pad = 0;
-        if (S.member_count) {             // a group's BLAS: the member instance holding `prim`, + 1
-            const uint32_t *M = members + 2 * (size_t)S.member_base;
-            uint32_t lo = 0, hi = S.member_count;          // last member whose first primitive <= prim
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) / 2;
-                if (M[2 * mid] <= prim) lo = mid; else hi = mid;
-            }
-            C.pad = M[2 * lo + 1] + 1u;
-        }
+        if (S.member_count) C.pad = item_member[vals[p]];   // a group's BLAS: the member instance holding `prim`, + 1
         out.tri_hot[slot] = H;
         out.tri_cold[slot] = C;
     } else if (S.ptype == RT_PRIM_SPHERE) {
@@ -1041,7 +1033,7 @@ static void dfree(T *&p) {
 }
 
 void LbvhBuilder::release() {
-    dfree(segs_); dfree(seg_of_); dfree(members_); dfree(own_box_); dfree(own_cent_); dfree(bounds_);
+    dfree(segs_); dfree(seg_of_); dfree(members_); dfree(item_member_); dfree(own_box_); dfree(own_cent_); dfree(bounds_);
     dfree(k0_); dfree(k1_); dfree(v0_); dfree(v1_); dfree(child_); dfree(parent_); dfree(parent_leaf_);
     dfree(range_); dfree(flag_); dfree(height_); dfree(nbox_); dfree(kept_); dfree(pidx_); dfree(front_); dfree(count_); dfree(frontier_);
     last_count_ = nullptr;
@@ -1101,11 +1093,36 @@ hipError_t LbvhBuilder::prep_blas_items(const RawPrimsGPU &raw, hipStream_t stre
     return hipGetLastError();
 }
 
+// item -> its member instance + 1 (group segments; 0 elsewhere), found once here instead of by every rebuild's gather
+__global__ void member_map_kernel(const LbvhSeg *segs, const uint32_t *seg_of, uint32_t n, const uint32_t *members,
+                                  uint32_t *item_member) {
+    const uint32_t it = blockIdx.x * BLOCK + threadIdx.x;
+    if (it >= n) return;
+    const LbvhSeg S = segs[seg_of[it]];
+    uint32_t v = 0;
+    if (S.member_count) {
+        const uint32_t prim = S.prim_base + (it - S.item_base);
+        const uint32_t *M = members + 2 * (size_t)S.member_base;
+        uint32_t lo = 0, hi = S.member_count;          // last member whose first primitive <= prim
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (M[2 * mid] <= prim) lo = mid; else hi = mid;
+        }
+        v = M[2 * lo + 1] + 1u;
+    }
+    item_member[it] = v;
+}
+
 hipError_t LbvhBuilder::set_members(const std::vector<uint32_t> &pairs, hipStream_t stream) {
     dfree(members_);
+    dfree(item_member_);
     if (pairs.empty()) return hipSuccess;
     LB_TRY(dalloc(members_, pairs.size()));
+    LB_TRY(dalloc(item_member_, (size_t)n_items_));
     LB_TRY(hipMemcpyAsync(members_, pairs.data(), pairs.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
+    hipLaunchKernelGGL(member_map_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, seg_of_, n_items_,
+                       members_, item_member_);
+    LB_TRY(hipGetLastError());
     return hipStreamSynchronize(stream);            // `pairs` (host) must outlive the copy
 }
 
@@ -1162,7 +1179,7 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
 
 hipError_t LbvhBuilder::gather_blas(const RawPrimsGPU &raw, const PrimOutGPU &out, hipStream_t stream) {
     hipLaunchKernelGGL(gather_blas_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, n_items_,
-                       raw, out, members_);
+                       raw, out, item_member_);
     return hipGetLastError();
 }
 

@@ -113,6 +113,7 @@ private:
     LbvhSeg *segs_ = nullptr;
     uint32_t *seg_of_ = nullptr;          // item -> segment
     uint32_t *members_ = nullptr;         // group segments: {first primitive, instance} pairs
+    uint32_t *item_member_ = nullptr;     // per item: its member instance + 1 (group segments), from members_
     float *box_ = nullptr;                // 6 floats per item (owned or caller's)
 public:
     bool size_classes_ = false;           // TLAS: size class above the Morton code (morton_kernel)

@@ -9,7 +9,7 @@ step tests 900 python -u -m pytest tests/test_gpu_lbvh.py tests/test_gpu_configs
 rm -f gpurun_out/ab.jsonl
 step ab_c5 900 bash scripts/ab_libs.sh 2 "head=librtamd_head.so new=default" --config C5 --build lbvh --rebuild --steps 12
 step ab_c2l 600 bash scripts/ab_libs.sh 2 "head=librtamd_head.so new=default" --build lbvh --rebuild
-step ab_c5d 900 bash scripts/ab_libs.sh 1 "new=default" --config C5 --build lbvh --rebuild --steps 12 --pre-opt blas_double=0
+
 cp gpurun_out/ab.jsonl $OUT/ab.jsonl
 step kst 600 rocprofv3 --kernel-trace --stats -d $OUT/kst -o run --output-format csv -- python3 bench.py --config C5 --build lbvh --rebuild --steps 12 --no-cpu-baseline
 exit 0
