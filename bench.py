@@ -330,13 +330,13 @@ def main():
         dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
         elapsed, rays = float(tmax[0]), int(t[1])
 
-    # the roofline's serialised launches: 20 frames back to back on one stream (no overlap partner, so each
-    # launch has the whole GPU: "grid_pct" 100), the GPU kept busy so its clocks stay where the timed region
-    # ran them; the HIP-event duration of each launch is the kernel's own
+    # the roofline's serialised launches: the timed frames again, back to back on one stream (no overlap partner,
+    # so each launch has the whole GPU: "grid_pct" 100), the GPU kept busy so its clocks stay where the timed
+    # region ran them; the HIP-event duration of each launch is the kernel's own
     if overlap:
         r.set_option("grid_pct", 100)
-    for k in range(20):
-        step(args.warmup + args.steps + k, sync=False, one_stream=True)
+    for k in range(args.steps):
+        step(args.warmup + k, sync=False, one_stream=True)
     torch.cuda.synchronize()
     _, serial_ms = r.collect()
     if overlap:
@@ -346,9 +346,10 @@ def main():
     # SURVEY 8d latency definition: wall time from the call to the framebuffer being ready (rank 0: the
     # assembled frame), synchronous frames, median of 20 after the timed region (untimed for `value`)
     lat = []
-    for k in range(20):
+    n_lat = min(20, args.steps)
+    for k in range(n_lat):                                 # the first timed frames, one at a time
         t1 = time.perf_counter()
-        step(args.warmup + args.steps + k, sync=False)    # enqueue, then wait for the whole device
+        step(args.warmup + k, sync=False)                  # enqueue, then wait for the whole device
         torch.cuda.synchronize()
         lat.append((time.perf_counter() - t1) * 1e3)
     _, sync_ms = r.collect()
@@ -359,9 +360,10 @@ def main():
     # 1.3-2.6 ms over the frames of one run), so every priced launch is priced with the work of the frame it
     # rendered — one counting pass per distinct frame (all ranks run the same passes: a pass gathers too)
     timed_frames = [args.warmup + k for k in range(args.steps)]
-    serial_frames = [args.warmup + args.steps + k for k in range(20)]
+    serial_frames = list(timed_frames)                       # the serialised launches re-render the timed frames
+    lat_frames = timed_frames[:n_lat]
     all_serial = not overlap                                 # every launch of the run was serialised
-    priced_frames = (pre_frames + timed_frames + serial_frames + serial_frames) if all_serial else serial_frames
+    priced_frames = (pre_frames + timed_frames + serial_frames + lat_frames) if all_serial else serial_frames
     assert not all_serial or len(priced_frames) == len(pre_ms) + len(kernel_ms) + len(serial_ms) + len(sync_ms), \
         (len(pre_frames), len(pre_ms), len(kernel_ms), len(serial_ms), len(sync_ms))
     work = {}
@@ -464,7 +466,8 @@ def main():
                 "timing": (f"mean HIP-event duration of all {len(every)} launches of the run, every one serialised "
                            "(--overlap 1: the launches a rocprofv3 --stats average of this command covers; kernel_ms)"
                            if all_serial else
-                           "mean HIP-event duration of 20 serialised launches, back to back on one stream (kernel_ms)"),
+                           "mean HIP-event duration of the timed frames rendered again, serialised back to back on one "
+                           "stream (kernel_ms)"),
                 "bytes_formula": "SURVEY 8(d): 32 aabb + 36 tri + 32 sphere/quad + 48 inst + 32 ray + 4 pixel",
                 "algorithmic_bytes_per_launch": int(bytes_launch),
                 "layout_bytes_per_launch": int(layout_bytes(cst)),
