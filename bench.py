@@ -201,10 +201,14 @@ def main():
     # ms/frame, C4 0.090 -> 0.054; profiles/r02_sweep_lanes8b.jsonl, r02_sweep_lanes8c.jsonl), while a
     # whole frame on one GPU is best with 3 lanes and the default 4 queues.  Set before HIP initialises.
     share = n > 1 or args.shard is not None
+    # with a communicator attached (N > 1, --attach-comm) RCCL's own streams take hardware queues as well: at 12
+    # two of three lanes shared one queue and ran back to back (world-1 comm path 0.29 ms/frame, 0.22 at 16-24;
+    # 1/8 shares 0.045 -> 0.043; profiles/r03_session2/comm_world1_hwq.jsonl)
+    want_q = 24 if (n > 1 or args.attach_comm) else (12 if share else 0)
     if os.environ.get("RTAMD_HWQ"):                    # A/B studies: an explicit queue count
         os.environ["GPU_MAX_HW_QUEUES"] = os.environ["RTAMD_HWQ"]
-    elif share and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 12:
-        os.environ["GPU_MAX_HW_QUEUES"] = "12"      # (the pool's boxes export 4, HIP's default)
+    elif want_q and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < want_q:
+        os.environ["GPU_MAX_HW_QUEUES"] = str(want_q)   # (the pool's boxes export 4, HIP's default)
 
     import numpy as np
     import torch
