@@ -5,6 +5,8 @@
 
 * profiles/pmc/<config>_<build>[_rebuild].json   the tagged PMC summaries bench.py prices `traffic` with
 * OUTDIR/bench_<tag>.json, serial_<tag>.json      the bench lines (pipelined default, serialised --overlap 1)
+* OUTDIR/serial_profiled_<tag>.json                the serialised line the rocprofv3-wrapped run printed (the same
+                                                   launches its kernel stats average: the summary compares these)
 * OUTDIR/kstats_<tag>.csv                          rocprofv3 --kernel-trace --stats of the serialised command
 * OUTDIR/summary.json                              per config: frac of the line, frac recomputed from the rocprof
                                                    average (algorithmic bytes / rocprof mean duration / 8 TB/s), the
@@ -62,6 +64,12 @@ def main():
                                    f"{t['config']}_{t['build']}{'_rebuild' if t['rebuild'] else ''}"
                                    f"{'_exact' if t['exact'] else ''}{'' if t['kernel'] else '_grid'}.json")
             shutil.copy(pmc, pmc_dst)
+        # the bench line printed by the rocprofv3-wrapped command itself: the very launches rocprof averaged
+        prof = line(os.path.join(SRC, f"kstats_{tag}.log"))
+        if prof is not None:
+            with open(os.path.join(OUT, f"serial_profiled_{tag}.json"), "w") as f:
+                json.dump(prof, f, indent=1)
+            ser = prof
         roof = ser["roofline"] if ser else None
         s = {"config": ser["config"]["workload"] if ser else None}
         if roof:
