@@ -269,6 +269,35 @@ def test_large_single_blas_device_wide_path(gpu_lib):
     assert f >= 0.999, (f, mx)
 
 
+def test_adjacent_large_blases_share_chunks(gpu_lib):
+    """Two BLASes of 3,000 and 5,000 triangles (both > 2048 items, so both take the chunked bottom-up: 1024-item
+    chunks through LDS, then the chunk-crossing nodes device-wide), adjacent in item order so that one chunk holds
+    items of both; rebuilt twice: every node of both trees equals the restatement bit for bit."""
+    tris, _ = scenes.synth_particles(8, 1024, seed=5)
+    s = scenes.demo_scene()
+    s.animated = False
+    s.triangles = np.concatenate([tris, s.triangles])
+    for d in s.instances:
+        if d["type"] == abi.TRIANGLE:
+            d["index"] += tris.shape[0]
+    s.instances.append(dict(type=abi.TRIANGLE, index=0, count=3000, shift=(0.0, 4.0, 0.0),
+                            rotate=(90.0, 0.0, 0.0), scale=(3.0, 3.0, 3.0)))
+    s.instances.append(dict(type=abi.TRIANGLE, index=3000, count=5000, shift=(2.0, 1.0, 0.0),
+                            rotate=(0.0, 30.0, 0.0), scale=(2.0, 2.0, 2.0)))
+    r = Renderer(s, update=False).build_acceleration_structure(0, mode="lbvh").configure_camera(160, 90)
+    r.set_option("rebuild", 1)
+    r.render(0)
+    blases = unique_blas(s)
+    for first, count in ((0, 3000), (3000, 5000)):
+        b = next(k for k, (t, f, c) in enumerate(blases) if t == abi.TRIANGLE and f == first and c == count)
+        boxes, cents = prim_items(s, abi.TRIANGLE, first, count)
+        nb, ci, refs = r.export_blas(b)
+        wb, wci, wrefs = lbvh_tree(boxes, cents, 4)
+        assert np.array_equal(ci, wci), (first, count)
+        assert np.array_equal(refs, wrefs + first) or np.array_equal(refs, wrefs), (first, count)
+        assert np.array_equal(nb, wb), (first, count)
+
+
 def test_rebuild_sah_then_lbvh_equals_fresh_lbvh(gpu_lib):
     """A scene built with SAH (instance records staged in TLAS slot order) and then rebuilt with LBVH
     must trace instance-ordered records again: frames and per-ray hits equal a fresh LBVH scene
