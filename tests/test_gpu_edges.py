@@ -1,0 +1,126 @@
+"""Edge cases of the trace path through the C ABI: ragged frame sizes (partial 8x8 units and 64x64
+tiles, single rows / columns, one pixel), scenes of a single primitive (one-leaf BLAS, one-record
+TLAS, mostly sky), and tiny frames on overlapped lanes across a heaviest-first reorder.
+
+The oracle (tests only) traverses the reference-order compat trees; EXACT frames on those trees are
+bit-identical in float RGB.  Single-primitive scenes have no hit ties, so every
+builder (compat / SAH / GPU LBVH) must give the oracle's bits there too.
+"""
+import numpy as np
+import pytest
+
+from rtamd import Renderer, abi, scenes
+
+pytestmark = pytest.mark.gpu
+
+THREADS = 16
+
+
+def _oracle(scene, w, h, seed=0, **cam):
+    from oracle.oracle import OracleScene
+    o = OracleScene(scene, build_seed=seed)
+    o.camera(w, h, **cam)
+    return o
+
+
+def _single(kind):
+    """One instance of one primitive above no ground (Main.cu's materials): the BLAS is one leaf."""
+    s = scenes.demo_scene()
+    s.animated = False
+    if kind == "sphere":
+        s.instances = [dict(type=abi.SPHERE, index=1, shift=(0.5, 0.2, 0.0))]
+    elif kind == "parallelogram":
+        s.instances = [dict(type=abi.PARALLELOGRAM, index=0, rotate=(0.0, 35.0, 0.0))]
+    else:
+        s.instances = [dict(type=abi.TRIANGLE, index=0, scale=(2.0, 2.0, 2.0))]
+    return s
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (7, 5), (65, 33), (130, 1), (1, 97), (9, 200)])
+def test_ragged_frame_sizes_exact(gpu_lib, w, h):
+    """Frames whose sides are not multiples of the 8x8 scheduling unit: every pixel written once,
+    float RGB bit-identical to the oracle, same ray count; a repeated render (after the reorder pass
+    has costed the frame) gives the same bytes."""
+    s = scenes.demo_with_particles(4)
+    r = Renderer(s).build_acceleration_structure(0).configure_camera(w, h, ray_trace_depth=3)
+    o = _oracle(s, w, h, 0, ray_trace_depth=3)
+    orgb, orgba, ocnt = o.render(threads=THREADS)
+    first = None
+    for rep in range(10):                       # reorder_period 8: launches 0 and 8 rebuild the order
+        rgba, rgb, st = r.render(0, exact=True, want_rgb=True, count_work=True)
+        assert st["pixels"] == w * h
+        assert (rgb != orgb).any(axis=2).sum() == 0, rep
+        assert st["rays"] == ocnt["rays"]
+        if first is None:
+            first = rgba
+        assert np.array_equal(rgba, first), rep
+    d = np.abs(first.astype(np.int32) - orgba.astype(np.int32)).max()
+    assert d <= 1
+
+
+@pytest.mark.parametrize("w,h", [(7, 5), (65, 33)])
+def test_ragged_frame_sizes_fast_kernels_agree(gpu_lib, w, h):
+    """FAST mode on ragged frames: the persistent kernel at every refill threshold gives the same
+    bytes, and stays within the FAST tolerance of the oracle."""
+    s = scenes.demo_with_particles(4)
+    r = Renderer(s).build_acceleration_structure(0).configure_camera(w, h, ray_trace_depth=2, sample_count=4)
+    o = _oracle(s, w, h, 0, ray_trace_depth=2, sample_count=4)
+    _, orgba, _ = o.render(threads=THREADS)
+    ref = None
+    for thr in (1, 16, 40, 64):
+        r.set_option("threshold", thr)
+        rgba, rgb, st = r.render(0, want_rgb=True)
+        if ref is None:
+            ref = rgb
+        assert np.array_equal(rgb, ref), thr
+        d = np.abs(rgba.astype(np.int32) - orgba.astype(np.int32)).max(axis=-1)
+        assert (d <= 1).mean() >= 0.99, thr
+
+
+@pytest.mark.parametrize("kind", ["sphere", "parallelogram", "triangle"])
+@pytest.mark.parametrize("mode", ["compat", "sah", "lbvh"])
+def test_single_primitive_scene(gpu_lib, kind, mode):
+    """One instance of one primitive: a one-leaf BLAS under a one-record TLAS (host-built or GPU
+    LBVH).  EXACT float RGB equals the oracle bit for bit and the work counters match (no ties, so
+    the builder cannot change which surface is hit)."""
+    s = _single(kind)
+    W, H = 96, 64
+    r = Renderer(s, update=False).build_acceleration_structure(0, mode=mode).configure_camera(W, H, ray_trace_depth=4)
+    o = _oracle(s, W, H, 0, ray_trace_depth=4)
+    orgb, orgba, ocnt = o.render(threads=THREADS)
+    rgba, rgb, st = r.render(0, exact=True, want_rgb=True, count_work=True)
+    assert (rgb != orgb).any(axis=2).sum() == 0
+    assert st["rays"] == ocnt["rays"]
+    if mode == "compat":
+        assert st["instance_visits"] == ocnt["instance_visits"]
+        assert st["triangle_tests"] == ocnt["triangle_tests"]
+        assert st["sphere_quad_tests"] == ocnt["sphere_quad_tests"]
+    # the primitive is hit and the rest is sky: both kinds of pixel are present
+    assert 0 < st["hits"] < st["rays"]
+    rgba_f, _, _ = r.render(0)
+    d = np.abs(rgba_f.astype(np.int32) - orgba.astype(np.int32)).max(axis=-1)
+    assert (d <= 1).mean() >= 0.999
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (7, 5), (17, 9)])
+def test_tiny_frames_on_overlapped_lanes(gpu_lib, w, h):
+    """Frames smaller than one scheduling unit on three overlapped lanes, over more launches than
+    the reorder period: every frame's bytes equal its synchronous render."""
+    import torch
+    s = scenes.demo_with_particles(6)
+    F = 12
+    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(w, h, ray_trace_depth=2)
+    ref = [r.render(f)[0] for f in range(F)]
+    r.collect()
+    r.set_option("overlap", 3)
+    lanes = [torch.cuda.Stream() for _ in range(3)]
+    bufs = [torch.zeros(w * h * 4, dtype=torch.uint8, device="cuda") for _ in range(F)]
+    torch.cuda.synchronize()
+    for f in range(F):
+        r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=lanes[f % 3].cuda_stream, sync=False)
+    _, kms = r.collect()
+    torch.cuda.synchronize()
+    for f in range(F):
+        assert np.array_equal(bufs[f].cpu().numpy(), ref[f].reshape(-1)), f
+    assert len(kms) == F
+    r.set_option("overlap", 0)
