@@ -56,6 +56,9 @@ def parse():
     p.add_argument("--overlap", type=int, default=None,
                    help="L >= 2: consecutive frames cycle L streams / library lanes so frame k+1 fills the CUs "
                         "frame k's tail leaves idle; 0 or 1: frames are serialised (default 3)")
+    p.add_argument("--lane-priority", type=int, default=None,
+                   help="overlap lanes on new HIP streams of this priority (torch: -1 high, 0 normal); default: "
+                        "new normal-priority streams for a share / the comm path, else the current stream + new ones")
     p.add_argument("--shard", default=None, help="R/N: trace only rank R's tiles of an N-rank split on this one GPU "
                                                  "(per-rank cost study; no gather)")
     p.add_argument("--opt", action="append", default=[], help="extra rt_scene_set_option key=value (A/B studies)")
@@ -249,6 +252,13 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     # "overlap": frame k runs on lanes[k % L]; each lane is a self-contained trace -> gather -> assemble chain
     lanes = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(L - 1)] if overlap else None
+    # a rank's share and the comm path: every lane on a new stream, none on the null stream (C2 1/8 share
+    # 0.0437 -> 0.0416 ms/frame, world-1 comm path 0.212 -> 0.191; the whole frame is equal either way, and a
+    # per-frame rebuild's overlap depends on which hardware queue its scene stream shares: C5 -8 %, C2-LBVH
+    # 2x slower; profiles/r03_session2/lane_streams_*.txt)
+    prio = args.lane_priority if args.lane_priority is not None else (0 if (share or args.attach_comm) else None)
+    if overlap and prio is not None:
+        lanes = [torch.cuda.Stream(priority=prio) for _ in range(L)]
     shard = tuple(int(v) for v in args.shard.split("/")) if args.shard else None
     if shard and (n > 1 or args.attach_comm):
         raise SystemExit("--shard is a one-GPU study")
@@ -423,6 +433,9 @@ def main():
                                                ("single-gpu through the world-1 comm path" if args.attach_comm
                                                 else "single-gpu"))),
                 "overlap_lanes": L,
+                "lane_streams": (None if not overlap else ("current stream + new streams" if prio is None
+                                                           else f"new streams, priority {prio}")),
+                "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4),
                 "tile": TILE,
                 "threshold": args.threshold if args.threshold is not None else "auto (64 at depth x spp <= 2, else 40)",
                 "options": args.pre_opt + args.opt,
