@@ -199,7 +199,7 @@ def main():
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE {world}")
     n = max(1, world)
     # a rank's 1/N share (N > 1, or the one-GPU --shard study) is bounded by its longest paths, not by its
-    # work: more frames in flight pay there (8 lanes with 15 % grids and 12 hardware queues per process, so
+    # work: more frames in flight pay there (8 lanes with 15 % grids (25 % since round 3) and 12 hardware queues per process, so
     # every lane and the RCCL communicators' streams get queues of their own: C2 1/8 share 0.067 -> 0.045
     # ms/frame, C4 0.090 -> 0.054; profiles/r02_sweep_lanes8b.jsonl, r02_sweep_lanes8c.jsonl), while a
     # whole frame on one GPU is best with 3 lanes and the default 4 queues.  Set before HIP initialises.
@@ -238,8 +238,8 @@ def main():
         k, v = kv.split("=")
         r.set_option(k, int(v, 0))
     # measured (profiles/r02_sweep_lanes.jsonl, r02_sweep_lanes8c.jsonl): 3 lanes at N = 1,
-    # 8 lanes on 15 % grids for a rank's 1/N share
-    # (the library's auto grid then gives each of 8 lanes' launches 15 % of the GPU while others are in flight)
+    # 8 lanes for a rank's 1/N share (the library's auto grid then gives each of 8 lanes' launches 25 % of the GPU
+    # while others are in flight; profiles/r03_session2/share_grid_*.txt)
     L = max(1, args.overlap if args.overlap is not None else (8 if share else 3))
     overlap = L > 1
     if overlap:
