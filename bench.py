@@ -58,7 +58,7 @@ def parse():
                         "frame k's tail leaves idle; 0 or 1: frames are serialised (default 3)")
     p.add_argument("--lane-priority", type=int, default=None,
                    help="overlap lanes on new HIP streams of this priority (torch: -1 high, 0 normal); default: "
-                        "new normal-priority streams for a share / the comm path, else the current stream + new ones")
+                        "new normal-priority streams, except the current stream + new ones with a per-frame rebuild")
     p.add_argument("--shard", default=None, help="R/N: trace only rank R's tiles of an N-rank split on this one GPU "
                                                  "(per-rank cost study; no gather)")
     p.add_argument("--opt", action="append", default=[], help="extra rt_scene_set_option key=value (A/B studies)")
@@ -201,13 +201,18 @@ def main():
     # a rank's 1/N share (N > 1, or the one-GPU --shard study) is bounded by its longest paths, not by its
     # work: more frames in flight pay there (8 lanes with 15 % grids (25 % since round 3) and 12 hardware queues per process, so
     # every lane and the RCCL communicators' streams get queues of their own: C2 1/8 share 0.067 -> 0.045
-    # ms/frame, C4 0.090 -> 0.054; profiles/r02_sweep_lanes8b.jsonl, r02_sweep_lanes8c.jsonl), while a
-    # whole frame on one GPU is best with 3 lanes and the default 4 queues.  Set before HIP initialises.
+    # ms/frame, C4 0.090 -> 0.054; profiles/r02_sweep_lanes8b.jsonl, r02_sweep_lanes8c.jsonl).  A whole frame on
+    # one GPU: 4 lanes off the null stream with 12 queues (C2 0.173 -> 0.164 ms/frame, C3 1.44 -> 1.39, C4 0.197 ->
+    # 0.190; profiles/r03_session2/lanes_new*.txt), except with a per-frame rebuild (below).  Set before HIP starts.
     share = n > 1 or args.shard is not None
+    # a per-frame BLAS rebuild overlaps the traces differently: C2-LBVH's runs 0.50 -> 1.0 ms/frame on lanes off the
+    # null stream (the rebuild kernels wait behind the lanes' grids), so those frames keep 3 lanes, the null stream
+    # as lane 0 and 4 queues (profiles/r03_session2/lane_streams_*.txt, scene_stream_priority_*.txt)
+    classic = not share and not args.attach_comm and args.rebuild
     # with a communicator attached (N > 1, --attach-comm) RCCL's own streams take hardware queues as well: at 12
     # two of three lanes shared one queue and ran back to back (world-1 comm path 0.29 ms/frame, 0.22 at 16-24;
     # 1/8 shares 0.045 -> 0.043; profiles/r03_session2/comm_world1_hwq.jsonl)
-    want_q = 24 if (n > 1 or args.attach_comm) else (12 if share else 0)
+    want_q = 24 if (n > 1 or args.attach_comm) else (0 if classic else 12)
     if os.environ.get("RTAMD_HWQ"):                    # A/B studies: an explicit queue count
         os.environ["GPU_MAX_HW_QUEUES"] = os.environ["RTAMD_HWQ"]
     elif want_q and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < want_q:
@@ -237,10 +242,10 @@ def main():
     for kv in args.opt:
         k, v = kv.split("=")
         r.set_option(k, int(v, 0))
-    # measured (profiles/r02_sweep_lanes.jsonl, r02_sweep_lanes8c.jsonl): 3 lanes at N = 1,
-    # 8 lanes for a rank's 1/N share (the library's auto grid then gives each of 8 lanes' launches 25 % of the GPU
-    # while others are in flight; profiles/r03_session2/share_grid_*.txt)
-    L = max(1, args.overlap if args.overlap is not None else (8 if share else 3))
+    # measured: 4 lanes for a whole frame (3 with a per-frame rebuild), 8 lanes for a rank's 1/N
+    # share (the library's auto grid then gives each launch 100 / lanes + 12 % of the GPU while others are in
+    # flight: 37 % at 4 lanes, 24 % at 8; profiles/r03_session2/share_grid_*.txt, lanes_new*.txt)
+    L = max(1, args.overlap if args.overlap is not None else (8 if share else (3 if classic else 4)))
     overlap = L > 1
     if overlap:
         r.set_option("overlap", L)
@@ -252,11 +257,9 @@ def main():
     stream = torch.cuda.current_stream().cuda_stream
     # "overlap": frame k runs on lanes[k % L]; each lane is a self-contained trace -> gather -> assemble chain
     lanes = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(L - 1)] if overlap else None
-    # a rank's share and the comm path: every lane on a new stream, none on the null stream (C2 1/8 share
-    # 0.0437 -> 0.0416 ms/frame, world-1 comm path 0.212 -> 0.191; the whole frame is equal either way, and a
-    # per-frame rebuild's overlap depends on which hardware queue its scene stream shares: C5 -8 %, C2-LBVH
-    # 2x slower; profiles/r03_session2/lane_streams_*.txt)
-    prio = args.lane_priority if args.lane_priority is not None else (0 if (share or args.attach_comm) else None)
+    # every lane on a new stream, none on the null stream (C2 1/8 share 0.0437 -> 0.0416 ms/frame, world-1 comm
+    # path 0.212 -> 0.191, the whole frame with 4 lanes above; profiles/r03_session2/lane_streams_*.txt)
+    prio = args.lane_priority if args.lane_priority is not None else (None if classic else 0)
     if overlap and prio is not None:
         lanes = [torch.cuda.Stream(priority=prio) for _ in range(L)]
     shard = tuple(int(v) for v in args.shard.split("/")) if args.shard else None

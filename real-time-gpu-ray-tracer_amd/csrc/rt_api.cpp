@@ -1774,10 +1774,11 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             bool partner = false;             // another lane's launch not finished yet (host query, ~1 us)
             for (int l = 0; s->overlap && l < rt_scene::NLANE && !partner; l++)
                 partner = l != q && s->r_lane[l] && hipEventQuery(s->r_lane[l]) == hipErrorNotReady;
-            // with a partner: half the GPU for up to 3 lanes, 2 / lanes of it with more (8 lanes: 25 %, the
-            // measured best for a rank's 1/2, 1/4 and 1/8 share once every lane runs off the null stream: C2 1/8
-            // 0.041 -> 0.038 ms/frame, 1/4 0.059 -> 0.052, profiles/r03_session2/share_grid_*.txt); alone: all of it
-            pct = !partner ? 100u : (s->lanes <= 3 ? 50u : std::max(12u, 200u / s->lanes));
+            // with a partner: half the GPU for up to 3 lanes, 1 / lanes + 12 % of it with more (4 lanes: 37 %, 8 lanes:
+            // 24 %: the measured best for a whole frame on 4 lanes and for a rank's 1/2, 1/4 and 1/8 share once every
+            // lane runs off the null stream: C2 0.173 -> 0.164 ms/frame, C2 1/8 share 0.041 -> 0.038, 1/4 0.059 ->
+            // 0.052; profiles/r03_session2/share_grid_*.txt, lanes_new*.txt); alone: all of it
+            pct = !partner ? 100u : (s->lanes <= 3 ? 50u : 100u / s->lanes + 12u);
         }
         if (pct < 100) blocks = std::max<uint32_t>(8u, blocks * pct / 100u);
         const uint32_t thr = s->threshold ? s->threshold : (cam.depth * cam.sqrt_s * cam.sqrt_s <= 2u ? 64u : 40u);
