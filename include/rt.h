@@ -347,8 +347,8 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "lds_blas"  : with "lds_scene" 2 and "group": the top levels of the first group's BLAS (quads numbered level
  *                 by level) fill the rest of the LDS scene region (default 1; 0 = from HBM; results identical)
  *   "grid_pct"  : persistent grid as a percentage of the resident workgroup capacity (1..100; default 0 = auto:
- *                 100 when no other lane's launch is in flight, else 50 with up to 3 lanes and 120 / lanes
- *                 (at least 12) with more, so several lanes' launches run side by side)
+ *                 100 when no other lane's launch is in flight, else 50 with up to 3 lanes and 100 / lanes + 12
+ *                 with more (37 at 4 lanes, 24 at 8), so several lanes' launches run side by side)
  *   "lds_scene" : FAST quad-tree kernel: 1 = every workgroup copies the frame's TLAS quads and, when they fit
  *                 as well, the instance hot records into 19 KB of LDS and reads them there; 2 = also the
  *                 sphere / parallelogram records and the instance cold records, while they fit (default 2;
