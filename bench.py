@@ -152,6 +152,19 @@ def lib_sha16():
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
+def build_provenance():
+    """The library's build stamp (rtamd/provenance.py): sources hash and the git HEAD that built it."""
+    from rtamd import provenance
+    ok, msg = provenance.check()
+    try:
+        with open(provenance.STAMP) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        d = {}
+    return {"stamp_ok": ok, "sources_sha16": (d.get("sources_sha256") or "")[:16], "git_head": d.get("git_head"),
+            "dirty_at_build": d.get("sources_dirty_at_build")}
+
+
 def pmc_tag(args):
     """What a PMC summary must have been measured on to price this run's launches: the same config, BVH
     builder, per-frame rebuild, kernel (EXACT / FAST, persistent / grid), scene options and library build."""
@@ -453,6 +466,12 @@ def main():
                           else "whole-frame throughput, serialised frames",
             "rays_per_frame": round(rays / args.steps, 1),
             "frame_latency_ms_median": round(float(np.median(lat)), 4),
+            # SURVEY 8(d) as a rate: the latency frames' rays (counted) over the median synchronous call-to-framebuffer
+            # time (one frame in flight, as the reference's loop keeps on its render stream, Renderer.cu:308-317)
+            # (N > 1: rank 0 counted only its own tiles, so the timed frames' mean over all ranks is used)
+            "value_latency": round((float(np.mean([work[f]["rays"] for f in lat_frames])) if n == 1 else rays / args.steps)
+                                   / (float(np.median(lat)) * 1e-3) / 1e6, 2),
+            "value_latency_unit": "Mrays/s",
             # host side of a timed rt_render call (update callback, instance records, TLAS build, staging)
             # and the part of it spent blocked on the GPU (a staging buffer still in use)
             "host_update_ms_median": round(float(np.median(timed_update[:, 0])), 4),
@@ -481,6 +500,7 @@ def main():
                 "traffic_source": traffic_src,
                 "traffic_note": traffic_why,
                 "lib_sha16": tag["lib_sha16"],
+                "build": build_provenance(),
                 "hbm_frac_measured": round(hbm_frac, 5) if hbm_frac is not None else None,
                 "kernel": kname,
                 "timing": (f"mean HIP-event duration of all {len(every)} launches of the run, every one serialised "

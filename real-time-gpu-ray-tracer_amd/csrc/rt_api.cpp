@@ -209,7 +209,9 @@ struct rt_scene {
     static constexpr uint8_t ALL_BLOCKS = 0xFF;
     static_assert(NLANE <= 8, "inst_dirty holds one bit per frame block");
     hipStream_t chain_stream[NLANE] = {};         // GPU-built frame b's records / TLAS were built on this stream
-    hipEvent_t ev_blas_built = nullptr;           // a GPU BLAS build on the scene stream finished
+    hipEvent_t ev_blas_built = nullptr;           // the last GPU BLAS build on the scene stream finished
+    uint64_t blas_build_seq = 0;                  // BLAS builds recorded on ev_blas_built so far
+    uint64_t blas_build_done = 0;                 // ... of which the host has seen the last one complete
     // pinned host staging, cycled independently of the frame blocks and twice as deep: a frame's staging is
     // reusable once its upload ran, which rt_render can only tell by the trace's completion event (a record
     // right after the copy kernel would idle the GPU ~5 us) — with one staging per block, the host waited for
@@ -551,6 +553,29 @@ rt_status drain(rt_scene *s) {
     return RT_OK;
 }
 
+// Order stream `st` after the last GPU BLAS build (ev_blas_built, recorded on the scene stream).  A build that has
+// already finished needs no wait (a host query, ~1 us): anything enqueued now runs after it.
+rt_status wait_blas_built(rt_scene *s, hipStream_t st) {
+    if (s->blas_build_done == s->blas_build_seq) return RT_OK;
+    const hipError_t q = hipEventQuery(s->ev_blas_built);
+    if (q == hipSuccess) {
+        s->blas_build_done = s->blas_build_seq;
+        return RT_OK;
+    }
+    if (q != hipErrorNotReady) return fail(RT_ERR_DEVICE, std::string("hipEventQuery: ") + hipGetErrorString(q));
+    HIP_TRY(hipStreamWaitEvent(st, s->ev_blas_built, 0));
+    return RT_OK;
+}
+
+// Every enqueued launch of the scene and the build of the current frame block (GPU-built frames build it on the
+// lane stream of the frame that staged it): the scene's own streams and events only, with the communicator's
+// bounded polls when one is attached (never a device-wide synchronisation).
+rt_status wait_frame_block(rt_scene *s) {
+    RT_TRY(drain(s));
+    if (s->active >= 0 && s->r_copied[s->active]) RT_TRY(wait_event(s, s->r_copied[s->active]));
+    return RT_OK;
+}
+
 // Host half of one frame: update callback, instance matrices, TLAS rebuild, staging, upload.
 // RT_BUILD_LBVH: the host stages matrices and transformed instance boxes only; the BLAS roots are
 // patched into the instance records and the TLAS is built by kernels on the scene's stream.
@@ -621,12 +646,15 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         const hipStream_t cs = small ? upload : s->stream;
         if (s->blas_builder && (s->rebuild_blas || s->blas_dirty)) {    // GPU-built BLASes only (scene stream)
             RT_TRY(gpu_build_blas(s));
-            if (cs != s->stream) {
-                if (!s->ev_blas_built) HIP_TRY(hipEventCreateWithFlags(&s->ev_blas_built, hipEventDisableTiming));
-                HIP_TRY(hipEventRecord(s->ev_blas_built, s->stream));
-                HIP_TRY(hipStreamWaitEvent(cs, s->ev_blas_built, 0));
-            }
+            if (!s->ev_blas_built) HIP_TRY(hipEventCreateWithFlags(&s->ev_blas_built, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(s->ev_blas_built, s->stream));
+            s->blas_build_seq++;
         }
+        // Every frame whose records / TLAS / trace run off the scene stream waits for the last BLAS build once per
+        // stream, not only the frame that enqueued it: a build swaps blas_roots / the primitive records to the set
+        // being written ("blas_double") or rewrites them in place, and a later frame on another lane stream that
+        // builds nothing would otherwise read them mid-build (rt_scene_update_triangles once, a group break)
+        if (cs != s->stream && s->blas_build_seq != 0) RT_TRY(wait_blas_built(s, cs));
         if (s->r_used[b]) HIP_TRY(hipStreamWaitEvent(cs, s->r_used[b], 0));      // block b no longer read
         // Instance::updateTransformArguments for every record of block b, on the GPU, with its BLAS root
         // (instances.hip); the deltas are read from the pinned staging block directly
@@ -650,7 +678,9 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
             a.leaf_cap = s->tlas_leaf;
             HIP_TRY(launch_tlas_small(a, cs));
             s->block_by_slot[b] = s->inst_by_slot;
-            s->frame_items[b] = live;
+            // the trace indexes the slot-ordered copy (live records) or, without "inst_by_slot", the record-order
+            // array, whose TLAS slots hold record indices up to n - 1 (lds_scene copies instance_count records)
+            s->frame_items[b] = s->inst_by_slot ? live : n;
             HIP_TRY(hipEventRecord(s->ev_copied[b], cs));
             s->r_copied[b] = s->r_staged[si] = s->ev_copied[b];
             s->active = b;
@@ -2257,7 +2287,7 @@ rt_status rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
     info->tlas_node_pairs = s->tlas_flat.pairs.size();
     if (s->gpu_tlas() && s->built) {                 // GPU-built TLAS: read the last frame's count / root
         HIP_TRY(hipSetDevice(s->device));
-        HIP_TRY(hipDeviceSynchronize());        // the frame's TLAS may have been built on a lane stream
+        RT_TRY(wait_frame_block(const_cast<rt_scene *>(s)));   // the frame's TLAS may have been built on a lane stream
         uint32_t np = 0;
         TreeRoot root{};
         HIP_TRY(hipMemcpy(&np, s->gpu_counts.p + 2 + s->active, sizeof np, hipMemcpyDeviceToHost));
@@ -2366,7 +2396,7 @@ rt_status rt_scene_export_tlas(const rt_scene *s, float *boxes, uint32_t *ci, ui
     Tree gpu_tree;
     if (s->gpu_tlas()) {
         HIP_TRY(hipSetDevice(s->device));
-        HIP_TRY(hipDeviceSynchronize());        // the frame's TLAS may have been built on a lane stream
+        RT_TRY(wait_frame_block(const_cast<rt_scene *>(s)));   // the frame's TLAS may have been built on a lane stream
         const uint8_t *fd = s->frame_dev[s->active];
         TreeRoot root{};
         std::vector<NodePair> pairs;

@@ -27,12 +27,24 @@ def oracle_lib():
     return oracle
 
 
+def pytest_report_header(config):
+    """Which library this run tests: its hash, the hash of the sources it was built from, the git HEAD
+    that built it (rtamd/provenance.py; the GPU box's copy of the tree has no .git)."""
+    from rtamd import provenance
+    ok, msg = provenance.check()
+    return [("tested " if ok else "PROVENANCE MISMATCH (rebuilt by the rtlib_path fixture): ") + msg]
+
+
 @pytest.fixture(scope="session")
 def rtlib_path():
-    """Path of librtamd.so, building it if missing (hipcc cross-compiles without a GPU)."""
-    from rtamd import abi
-    if not os.path.exists(abi.LIB_PATH):
+    """Path of librtamd.so, built from the sources in this tree: (re)built when missing or when its build
+    stamp does not match the library or the sources (hipcc cross-compiles without a GPU)."""
+    from rtamd import abi, provenance
+    if not os.path.exists(abi.LIB_PATH) or not provenance.check()[0]:
         subprocess.run(["make", "-s", "-j4", "-C", os.path.join(PKG, "csrc")], check=True)
+    ok, msg = provenance.check()
+    assert ok, msg
+    print(f"\n[provenance] {msg}", flush=True)
     return abi.LIB_PATH
 
 

@@ -68,6 +68,17 @@ def test_library_exports_every_declared_symbol(rtlib_path):
         assert re.search(rf"\bT {name}$", nm, re.M), name
 
 
+def test_library_is_built_from_this_tree(rtlib_path):
+    """The build stamp (rtamd/provenance.py) matches the library and the sources in the tree."""
+    from rtamd import provenance
+    ok, msg = provenance.check()
+    assert ok, msg
+    with open(provenance.STAMP) as f:
+        import json
+        d = json.load(f)
+    assert "real-time-gpu-ray-tracer_amd/csrc/trace_kernel.hip" in d["sources"] and "include/rt.h" in d["sources"]
+
+
 def test_library_loads_and_reports_abi(rtlib_path):
     lib = abi.load_library(rtlib_path)
     assert lib.rt_abi_version() == abi.RT_ABI_VERSION

@@ -211,6 +211,43 @@ def test_update_triangles_pipelined_frames(gpu_lib, group):
     r.cleanup()
 
 
+@pytest.mark.parametrize("double", [1, 0])
+def test_update_triangles_once_then_pipelined_frames(gpu_lib, double):
+    """One rt_scene_update_triangles, then frames on three overlapped lanes without waiting: only the first frame
+    enqueues the BLAS rebuild (on the scene stream); the frames after it on the other lanes build nothing and must
+    still wait for it before their instance records, TLAS and trace read the new BLAS set.  Every
+    frame equals the synchronous render of the same frame; both BLAS-set policies ("blas_double")."""
+    import torch
+    P = 200                                            # ~205 k triangles: a rebuild long enough to race with
+    s = scenes.demo_with_particles(P)
+    n_p = P * 1024
+    W, H, F, L = 256, 144, 9, 3
+    moved = s.triangles[:n_p].copy()
+    moved["vertex"] += np.asarray([0.04, -0.02, 0.03], np.float32)
+    ref_r = Renderer(s).set_option("blas_double", double).build_acceleration_structure(0, mode="lbvh")
+    ref_r.configure_camera(W, H, ray_trace_depth=2)
+    ref_r.update_triangles(0, moved)
+    ref = [ref_r.render(f)[0] for f in range(F)]
+    ref_r.cleanup()
+    r = Renderer(s).set_option("blas_double", double).build_acceleration_structure(0, mode="lbvh")
+    r.configure_camera(W, H, ray_trace_depth=2)
+    r.set_option("overlap", L)
+    lanes = [torch.cuda.Stream() for _ in range(L)]
+    bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(F)]
+    for f in range(3):                                 # frames on the old triangles first: the lanes are warm
+        r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=lanes[f % L].cuda_stream, sync=False)
+    r.synchronize()
+    torch.cuda.synchronize()
+    r.update_triangles(0, moved)
+    for f in range(F):
+        r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=lanes[f % L].cuda_stream, sync=False)
+    r.synchronize()
+    torch.cuda.synchronize()
+    for f in range(F):
+        assert np.array_equal(bufs[f].cpu().numpy().reshape(H, W, 4), ref[f]), f
+    r.cleanup()
+
+
 def test_update_triangles_needs_lbvh(gpu_lib):
     s = scenes.demo_with_particles(2)
     r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(32, 32)

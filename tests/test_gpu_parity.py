@@ -60,6 +60,27 @@ def test_exact_mode_bit_identical_demo(gpu_lib, depth):
     assert st["sphere_quad_tests"] == ocnt["sphere_quad_tests"]
 
 
+@pytest.mark.parametrize("kernel", [1, 0])
+def test_c1_exact_256_depth10(gpu_lib, kernel):
+    """BASELINE.json configs[0] (C1) at its own workload: the demo scene, 256x256, 1 spp, depth 10.  EXACT on the
+    reference's trees is bit-identical to the oracle's BVH frame (persistent and grid kernels) with equal work
+    counters, and within SURVEY 8(c)'s depth-10 bar (<= 0.05 % of pixels beyond 1 LSB) of the oracle's
+    brute-force loops (tests/test_oracle_kat.py::test_c1_bvh_equals_brute_force_256 pins BVH vs loops)."""
+    r, o = pair(scenes.demo_scene(), 0, 256, 256, ray_trace_depth=10)
+    r.set_option("kernel", kernel)
+    rgba, rgb, st = r.render(0, exact=True, want_rgb=True, count_work=True)
+    orgb, orgba, ocnt = o.render(threads=THREADS)
+    assert (rgb != orgb).any(axis=2).sum() == 0, float(np.abs(rgb - orgb).max())
+    assert frac_within(rgba, orgba)[0] == 1.0
+    for k in ("rays", "instance_visits", "triangle_tests", "sphere_quad_tests"):
+        assert st[k] == ocnt[k], k
+    _, brgba, _ = o.render(threads=THREADS, brute_force=2)
+    bad = int((np.abs(rgba.astype(np.int32) - brgba.astype(np.int32)).max(axis=2) > 1).sum())
+    assert bad <= 0.0005 * 256 * 256, bad
+    fast, _, _ = r.render(0)
+    assert int((np.abs(fast.astype(np.int32) - orgba.astype(np.int32)).max(axis=2) > 1).sum()) <= 0.0005 * 256 * 256
+
+
 def test_exact_mode_particles_and_animation(gpu_lib):
     s = scenes.demo_with_particles(12)
     r, o = pair(s, 5, 200, 120, ray_trace_depth=2)

@@ -284,3 +284,27 @@ def test_trace_counts_and_closest_hit(oracle_lib):
     t_exp = 2.0 + 1000.0 - math.sqrt(1000.0 ** 2 - 100.0)
     assert hits["instance"][0] == 0 and abs(hits["t"][0] - t_exp) < 1e-3
     assert hits["instance"][1] == abi.MISS                                     # straight up: sky
+
+
+# ---- C1 (BASELINE.json configs[0]): the demo scene at 256x256, BVH vs brute-force loops -------------------
+@pytest.mark.parametrize("depth", [1, 2, 10])
+def test_c1_bvh_equals_brute_force_256(oracle_lib, depth):
+    """the demo scene (2 spheres, parallelogram, triangle; 5 instances) traced at 256x256 with the
+    reference's TLAS/BLAS and with brute-force instance / primitive loops (the NO_AS intent of the dead
+    Kernel.cu:10-62 path, gated by each primitive's own box as the BVH leaves are).  Primary rays are identical
+    for every tree seed.  At depth >= 2 a bounce ray can hit two surfaces within the 1e-6 window, where the
+    later-tested one wins (Range.cuh:33-43) and the loop order differs from the tree's: measured 0 pixels for
+    tree seeds 1-5 and 1 (depth 2) / 2 (depth 10) of 65 536 for seed 0 (max 14 LSB) — inside SURVEY 8(c)'s
+    0.01 % (depth 2) and 0.05 % (depth 10) outlier bars, which the test asserts."""
+    from oracle.oracle import OracleScene
+    bar = {1: 0, 2: 0.0001, 10: 0.0005}[depth]
+    for seed in range(6):
+        o = OracleScene(scenes.demo_scene(), build_seed=seed)
+        o.camera(256, 256, ray_trace_depth=depth)
+        a_rgb, a, ca = o.render(threads=4)
+        b_rgb, b, cb = o.render(threads=4, brute_force=2)
+        bad = (np.abs(a.astype(np.int32) - b.astype(np.int32)).max(axis=2) > 1).sum()
+        assert bad <= bar * 256 * 256, (depth, seed, int(bad))
+        if depth == 1:
+            assert np.array_equal(a_rgb, b_rgb) and ca["rays"] == cb["rays"] == 256 * 256
+        assert abs(ca["rays"] - cb["rays"]) <= 2
