@@ -3,14 +3,29 @@
 
 #include <dlfcn.h>
 
+#include <cstdlib>
+
 namespace rtamd {
 namespace {
 
 Rccl load() {
     Rccl r;
     void *h = nullptr;
+    // RTAMD_RCCL_LIB: an explicit RCCL build (tests/fake_rccl: an N-rank world inside one process, so the world > 1
+    // gather runs on a one-GPU box); it must load, no fallback
+    if (const char *path = std::getenv("RTAMD_RCCL_LIB")) {
+        if (*path) {
+            h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+            if (!h) {
+                const char *e = dlerror();
+                r.error = std::string("cannot load RTAMD_RCCL_LIB=") + path + ": " + (e ? e : "not found");
+                return r;
+            }
+        }
+    }
     // an RCCL the process already holds (e.g. PyTorch's), else ROCm's
     for (const char *name : {"librccl.so.1", "librccl.so"}) {
+        if (h) break;
         h = dlopen(name, RTLD_NOW | RTLD_NOLOAD);
         if (h) break;
     }

@@ -388,7 +388,7 @@ struct rt_scene {
         delete comm;
         comm = nullptr;
         for (int q = 0; q < NLANE; q++) r_lane[q] = ev_lane_done[q];
-        r_done = nullptr;
+        r_done = ev_render_done;                   // never recorded after the build's drain: waits on it are no-ops
         for (int b = 0; b < NLANE; b++) { r_copied[b] = ev_copied[b]; r_used[b] = ev_used[b]; }
         for (hipEvent_t &e : r_staged) e = nullptr;     // drained: every staging buffer is free
     }
@@ -1707,7 +1707,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     }
     s->lane = s->overlap ? (s->lane + 1) % s->lanes : 0u;
     s->last_lane = q;
-    HIP_TRY(hipStreamWaitEvent(stream, s->overlap ? s->r_lane[q] : s->r_done, 0));
+    if (hipEvent_t prev = s->overlap ? s->r_lane[q] : s->r_done) HIP_TRY(hipStreamWaitEvent(stream, prev, 0));
     unsigned long long *lane_counters = s->counters + (size_t)q * CNT_NUM;   // only this lane's launches add here
     if (!(o.flags & RT_RENDER_KEEP_COUNTERS)) s->cnt_epoch++;
     bool zero_lane = s->lane_epoch[q] != s->cnt_epoch;                      // cleared before this launch

@@ -87,7 +87,14 @@ __device__ __forceinline__ f3 cross(f3 a, f3 b) {           // Vec3.cuh:120-126
 }
 // FAST mode replaces IEEE division / 1/sqrt by the hardware v_rcp_f32 / v_rsq_f32 (1 ulp);
 // EXACT mode keeps the reference's correctly rounded operations.
-__device__ __forceinline__ float rcp(float x) {
+// RT_FAST_IEEE (FAST build): 1 = the reference's correctly rounded division and 1/sqrt in the primitive tests and
+// the shading as well (only the box tests keep reciprocal slabs), 2 = the same except the triangle test.
+#ifndef RT_FAST_IEEE
+#define RT_FAST_IEEE 0
+#endif
+#define RT_IEEE_PRIM (RT_EXACT || RT_FAST_IEEE >= 1)
+#define RT_IEEE_TRI (RT_EXACT || RT_FAST_IEEE == 1)
+__device__ __forceinline__ float rcp(float x) {              // slab reciprocals (FAST)
 #if RT_EXACT
     return 1.0f / x;
 #else
@@ -95,14 +102,14 @@ __device__ __forceinline__ float rcp(float x) {
 #endif
 }
 __device__ __forceinline__ float fdiv(float a, float b) {
-#if RT_EXACT
+#if RT_IEEE_PRIM
     return a / b;
 #else
     return a * __builtin_amdgcn_rcpf(b);
 #endif
 }
 __device__ __forceinline__ f3 unit(f3 a) {                   // Vec3.cuh:129-137
-#if RT_EXACT
+#if RT_IEEE_PRIM
     const float f = 1.0f / sqrtf(dot(a, a));
 #else
     const float f = __builtin_amdgcn_rsqf(dot(a, a));
@@ -221,7 +228,7 @@ __device__ __forceinline__ bool tri_test(const TriHot &T, const RayP &r, float t
     const float det = dot(e1, h);
     if (fabsf(det) < FZERO) return false;
     const f3 s = sub(r.o, v0);
-#if RT_EXACT
+#if RT_IEEE_TRI
     u = dot(s, h) / det;
     if (!in_range(u, 0.0f, 1.0f)) return false;
     const f3 q = cross(s, e1);

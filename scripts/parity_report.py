@@ -5,6 +5,8 @@ For C2 (1080p, 1 spp, depth 2; also at depth 1) and C3 (1080p, 4 spp, depth 4), 
   * "bench":  FAST kernel, SAH trees, instance groups, quad traversal, LDS scene, 4 pipelined lanes (NO_SYNC
               frames on four streams into device buffers), i.e. bench.py's configuration;
   * "fast_compat": FAST kernel on the reference's own (median-split) trees — identical trees to the oracle's;
+  * "fast_compat_binary": FAST arithmetic on those trees with the binary node-pair traversal (the reference's
+              visit order), which separates arithmetic from visit-order ties;
   * "exact_compat": EXACT kernel on those trees (bit-identical by the parity tests)
 and compares each with the oracle's frame: pixels with any RGBA8 channel |d| > 1 (outliers), max |d|, and the
 per-channel float |d| of the linear RGB.  Output: one JSON object (stdout, or --out).
@@ -70,7 +72,10 @@ def main():
             print(f"oracle {cname} frame {f}: {time.time() - t0:.1f} s", flush=True)
         for mode in args.modes.split(","):
             build = "sah" if mode == "bench" else "compat"
-            r = Renderer(scene).build_acceleration_structure(0, mode=build).configure_camera(W, H, **cam)
+            r = Renderer(scene)
+            if mode == "fast_compat_binary":                 # FAST arithmetic on the reference's binary visit order
+                r.set_option("wide", 0)
+            r.build_acceleration_structure(0, mode=build).configure_camera(W, H, **cam)
             got = {}
             if mode == "bench":
                 L = 4

@@ -1,0 +1,109 @@
+"""World > 1 multi-GPU frames on one GPU through the fake RCCL (tests/fake_rccl/fake_rccl.hip).
+
+Run by tests/test_gpu_fake_rccl.py in a child process with RTAMD_RCCL_LIB set (the library resolves RCCL once
+per process).  Every rank is a scene of its own on device 0, driven from this thread in the order a real world's
+ranks would post their work (senders first, rank 0 last, the same lane sequence on every rank).  The library's
+world > 1 branch runs as on 8 GPUs: rank r traces its interleaved tiles into its lane's slab and sends it to
+rank 0 (grouped ncclSend / ncclRecv), rank 0 receives the slabs into its lane's gather buffer and assembles the
+frame (csrc/rt_api.cpp rt_render).  Prints one JSON line per case; exits non-zero on the first failure.
+"""
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "real-time-gpu-ray-tracer_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from rtamd import Renderer, abi, scenes  # noqa: E402
+
+W, H, DEPTH, TILE, F = 320, 192, 2, 32, 24
+
+
+def make(scene):
+    return Renderer(scene).build_acceleration_structure(0, mode="sah").configure_camera(W, H, ray_trace_depth=DEPTH)
+
+
+def world(scene, n, lanes=1, ncomm=1, sync=True):
+    """Frames 0..F-1 of an n-rank world; ncomm = lanes in use at attach (one communicator each), lanes >
+    ncomm shares them (lane q uses communicator q % ncomm)."""
+    rs = [make(scene) for _ in range(n)]
+    cid = Renderer.comm_unique_id()
+    for k, r in enumerate(rs):
+        if ncomm > 1:
+            r.set_option("overlap", ncomm)
+        r.attach_comm(cid, k, n, TILE, TILE)
+        r.set_comm_timeout(20000)
+        if lanes != ncomm:
+            r.set_option("overlap", lanes if lanes > 1 else 0)
+    out = []
+    if sync:
+        for f in range(F):
+            for k in reversed(range(n)):
+                rgba, _, st = rs[k].render(f)
+                if k == 0:
+                    out.append(rgba)
+    else:
+        streams = [[torch.cuda.Stream() for _ in range(lanes)] for _ in range(n)]
+        bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(F)]
+        torch.cuda.synchronize()
+        for f in range(F):
+            for k in reversed(range(n)):
+                rs[k].render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr() if k == 0 else None,
+                             stream=streams[k][f % lanes].cuda_stream, sync=False)
+        for r in rs:
+            r.synchronize()
+        torch.cuda.synchronize()
+        out = [b.cpu().numpy().reshape(H, W, 4) for b in bufs]
+    for r in rs:
+        r.cleanup()
+    return out
+
+
+def main():
+    assert os.environ.get("RTAMD_RCCL_LIB"), "run through tests/test_gpu_fake_rccl.py"
+    torch.cuda.set_device(0)
+    scene = scenes.demo_with_particles(12)
+    ref_r = make(scene)
+    ref = [ref_r.render(f)[0] for f in range(F)]
+    ref_r.cleanup()
+    assert not np.array_equal(ref[0], ref[F - 1])
+    cases = [(2, 1, 1, True), (8, 1, 1, True), (2, 3, 3, False), (8, 4, 2, False), (8, 8, 3, False)]
+    for n, lanes, ncomm, sync in cases:
+        t0 = time.time()
+        got = world(scene, n, lanes, ncomm, sync)
+        bad = [f for f in range(F) if not np.array_equal(got[f], ref[f])]
+        print(json.dumps({"world": n, "lanes": lanes, "communicators": ncomm, "sync": sync, "frames": F,
+                          "frames_differing": bad, "s": round(time.time() - t0, 2)}), flush=True)
+        assert not bad, (n, lanes, ncomm, sync, bad)
+
+    # a peer that never posts its send: rank 0's frame must fail with RT_ERR_DEVICE at the deadline, not hang
+    rs = [make(scene) for _ in range(2)]
+    cid = Renderer.comm_unique_id()
+    for k, r in enumerate(rs):
+        r.attach_comm(cid, k, 2, TILE, TILE)
+    rs[0].set_comm_timeout(1500)
+    t0 = time.time()
+    try:
+        rs[0].render(0)
+        raise AssertionError("rank 0's frame completed without its peer")
+    except abi.RtError as e:
+        msg = str(e)
+    dt = time.time() - t0
+    print(json.dumps({"case": "peer never sends", "error": msg, "s": round(dt, 2)}), flush=True)
+    assert msg.startswith("RT_ERR_DEVICE") and "not complete after 1500 ms" in msg, msg
+    assert 1.4 < dt < 15.0, dt
+    # the scene was detached by the abort: it renders whole single-GPU frames again
+    rs[0].comm = None
+    assert np.array_equal(rs[0].render(5)[0], ref[5])
+    for r in rs:
+        r.cleanup()
+    print(json.dumps({"ok": True}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
