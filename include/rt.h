@@ -308,6 +308,9 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 traversal loop to shade / regenerate (1..64; default 0 = auto: 64 when depth x samples <= 2,
  *                 else 40)
  *   "variant"   : persistent kernel register budget: 0 = compiler's choice, 4 = at least 4 waves per SIMD
+ *   "fast_math" : FAST frames only: 1 = hardware reciprocal / rsq and FMA contraction in the primitive tests, transforms
+ *                 and shading (about 8 % faster; 0.01-0.09 % of pixels then differ from the reference's arithmetic);
+ *                 0 (default) = the reference's correctly rounded arithmetic wherever a value reaches a hit or a pixel
  *   "queue_parts": persistent kernel work-queue bands (1..8, default 8; a wave starts on band XCC_ID % parts)
  *   "reorder"   : 1 (default) = each launch claims its band's 8x8 units heaviest-first, ordered by the
  *                 traversal work the previous launch of the same layout and lane recorded per unit (schedule.hip);

@@ -47,6 +47,12 @@ hipError_t launch_instance_slot_order(const uint32_t *, const InstHot *, const I
 hipError_t launch_instance_update(const InstDelta *, uint32_t, InstParams *, uint32_t, InstHot *, InstCold *, float *, float4 *,
                                   const uint32_t *, const TreeRoot *, const uint32_t *, bool, hipStream_t);
 uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool wide);
+// option "fast_math": the FAST kernels compiled with hardware reciprocals and FMA contraction (trace_fastmath.o)
+hipError_t launch_render_fastmath(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *, hipStream_t);
+hipError_t launch_trace_rays_fastmath(const SceneGPU &, const float *, uint32_t, rt_hit *, hipStream_t);
+hipError_t launch_render_persistent_fastmath(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
+                                             uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
+uint32_t persistent_blocks_per_cu_fastmath(uint32_t variant, bool wide);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -268,6 +274,10 @@ struct rt_scene {
     // 23 %, 40 ties 32; profiles/r02_sweep_thr2.jsonl)
     uint32_t threshold = 0;
     uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4)
+    // option "fast_math": FAST frames with hardware reciprocal / rsq and FMA contraction instead of the reference's
+    // correctly rounded arithmetic (C2 -7 %, C3 -9 % per pipelined frame; 0.008-0.09 % of pixels then differ from the
+    // oracle even on its own trees); default 0: bit-identical to the oracle on the reference's trees
+    bool fast_math = false;
     double update_wait_ms = 0.0;    // last frame_update: time blocked on ev_copied (GPU progress)
     bool use_persistent = true;
     uint32_t queue_parts = 8;       // one band per XCD (measured with "reorder": 8 beat 4, 2 and 1 on C2)
@@ -1683,7 +1693,8 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         out.supertile = s->supertile;
         if (s->timeline_on) {
             const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false)
-                                                    : persistent_blocks_per_cu_fast(s->variant, g.wide != 0));
+                                                    : (s->fast_math ? persistent_blocks_per_cu_fastmath(s->variant, g.wide != 0)
+                                                                   : persistent_blocks_per_cu_fast(s->variant, g.wide != 0)));
             const size_t words = (size_t)blocks * 4 * TIMELINE_WORDS;
             if (s->timeline.n < words) {
                 s->timeline.release();
@@ -1797,7 +1808,8 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     HIP_TRY(hipEventRecord(s->ring_start[slot], stream));
     if (s->use_persistent) {
         const uint32_t cap = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false)
-                                             : persistent_blocks_per_cu_fast(s->variant, g.wide != 0));
+                                             : (s->fast_math ? persistent_blocks_per_cu_fastmath(s->variant, g.wide != 0)
+                                                            : persistent_blocks_per_cu_fast(s->variant, g.wide != 0)));
         uint32_t blocks = s->overlap && cap > 2 * s->reserve ? cap - s->reserve : cap;
         uint32_t pct = s->grid_pct;
         if (pct == 0) {
@@ -1814,12 +1826,15 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         const uint32_t thr = s->threshold ? s->threshold : (cam.depth * cam.sqrt_s * cam.sqrt_s <= 2u ? 64u : 40u);
         HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, lane_counters, s->queue[q], blocks, thr,
                                                        s->variant, reset_queue, stream)
-                      : launch_render_persistent_fast(g, cam, out, count, lane_counters, s->queue[q], blocks, thr,
-                                                      s->variant, reset_queue, stream));
+                      : (s->fast_math ? launch_render_persistent_fastmath(g, cam, out, count, lane_counters, s->queue[q], blocks,
+                                                                          thr, s->variant, reset_queue, stream)
+                                      : launch_render_persistent_fast(g, cam, out, count, lane_counters, s->queue[q], blocks, thr,
+                                                                      s->variant, reset_queue, stream)));
     }
     else
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, lane_counters, stream)
-                      : launch_render_fast(g, cam, out, count, lane_counters, stream));
+                      : (s->fast_math ? launch_render_fastmath(g, cam, out, count, lane_counters, stream)
+                                      : launch_render_fast(g, cam, out, count, lane_counters, stream)));
     HIP_TRY(hipEventRecord(s->ring_stop[slot], stream));
     hipEvent_t done = s->ring_stop[slot];      // the launch's one completion event (see r_used)
     if (cm) {
@@ -1916,7 +1931,8 @@ rt_status rt_trace_rays(rt_scene *s, const float *rays, size_t n, uint32_t flags
     if (e == hipSuccess) e = hipStreamWaitEvent(s->stream, s->r_copied[s->active], 0);
     if (e == hipSuccess)
         e = (flags & RT_RENDER_EXACT) ? launch_trace_rays_exact(g, d_rays, (uint32_t)n, d_hits, s->stream)
-                                      : launch_trace_rays_fast(g, d_rays, (uint32_t)n, d_hits, s->stream);
+                                      : (s->fast_math ? launch_trace_rays_fastmath(g, d_rays, (uint32_t)n, d_hits, s->stream)
+                                                      : launch_trace_rays_fast(g, d_rays, (uint32_t)n, d_hits, s->stream));
     if (e == hipSuccess) e = hipEventRecord(s->ev_used[s->active], s->stream);
     if (e == hipSuccess) { s->r_used[s->active] = s->ev_used[s->active]; s->r_done = s->ev_used[s->active]; }
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
@@ -1939,6 +1955,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "variant") {
         if (value != 0 && value != 4) return fail(RT_ERR_INVALID_ARGUMENT, "variant must be 0 or 4");
         s->variant = (uint32_t)value;
+    } else if (k == "fast_math") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "fast_math must be 0 or 1");
+        s->fast_math = value == 1;
     } else if (k == "queue_parts") {
         if (value < 1 || value > (int64_t)QUEUE_MAX_PARTS) return fail(RT_ERR_INVALID_ARGUMENT, "queue_parts must be in 1..8");
         s->queue_parts = (uint32_t)value;

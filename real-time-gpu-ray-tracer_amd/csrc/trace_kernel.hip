@@ -8,12 +8,16 @@
 // (src/AS/BoundingBox.cu:34-72), Sphere/Parallelogram/Triangle::hit (src/Geometry/*.cu),
 // Rough/Metal::scatter (include/Material/*.cuh), Color3::castToUchar4 (Color3.cuh:99-114).
 //
-// This file is compiled twice:
+// This file is compiled three times:
 //   RT_EXACT=1, -ffp-contract=off : every float operation in the reference's order with IEEE
-//       division — bit-faithful to the oracle on identical trees (parity mode);
-//   RT_EXACT=0, -ffp-contract=fast: reciprocal-direction slab tests (one FMA per plane),
-//       reciprocal determinant, FMA-contracted transforms (performance mode; parity within
-//       the stated tolerance).
+//       division, the reference's binary trees and visit order — bit-faithful to the oracle on identical
+//       trees, equal work counters (parity mode);
+//   RT_EXACT=0 RT_FAST_IEEE=1, -ffp-contract=off (default): the persistent quad-tree kernel with
+//       reciprocal-direction slab tests (one explicit FMA per plane, a cull only) and the reference's
+//       arithmetic everywhere a value reaches a hit or a pixel — on the reference's trees its frames are
+//       bit-identical to the oracle's;
+//   RT_EXACT=0 RT_FAST_IEEE=0, -ffp-contract=fast (option "fast_math"): also reciprocal determinant /
+//       division, v_rsq, FMA-contracted transforms (parity within the measured tolerance).
 //
 // Traversal keeps the reference's visit order exactly: node pairs test both children of an
 // interior node (BLAS.cu:180-202), the near child (smaller entry t; ties -> left) is visited
@@ -31,10 +35,19 @@
 #error "compile with -DRT_EXACT=0 or 1"
 #endif
 
+// RT_FAST_IEEE (FAST builds): 1 = the reference's correctly rounded division and 1/sqrt everywhere except the box
+// tests' reciprocal slabs, compiled without FMA contraction (the default FAST kernel: on the reference's own trees
+// its frames are bit-identical to the oracle's); 0 = hardware v_rcp / v_rsq and FMA contraction
+// (option "fast_math": ~8 % faster on C2 / C3, and ~0.01-0.09 % of pixels differ, measured)
+#ifndef RT_FAST_IEEE
+#define RT_FAST_IEEE 1
+#endif
 #if RT_EXACT
 #define RT_SUFFIX(n) n##_exact
-#else
+#elif RT_FAST_IEEE
 #define RT_SUFFIX(n) n##_fast
+#else
+#define RT_SUFFIX(n) n##_fastmath
 #endif
 
 namespace rtamd {
@@ -85,15 +98,11 @@ __device__ __forceinline__ float dot(f3 a, f3 b) {          // Vec3.cuh:113-119
 __device__ __forceinline__ f3 cross(f3 a, f3 b) {           // Vec3.cuh:120-126
     return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
 }
-// FAST mode replaces IEEE division / 1/sqrt by the hardware v_rcp_f32 / v_rsq_f32 (1 ulp);
-// EXACT mode keeps the reference's correctly rounded operations.
-// RT_FAST_IEEE (FAST build): 1 = the reference's correctly rounded division and 1/sqrt in the primitive tests and
-// the shading as well (only the box tests keep reciprocal slabs), 2 = the same except the triangle test.
-#ifndef RT_FAST_IEEE
-#define RT_FAST_IEEE 0
-#endif
-#define RT_IEEE_PRIM (RT_EXACT || RT_FAST_IEEE >= 1)
-#define RT_IEEE_TRI (RT_EXACT || RT_FAST_IEEE == 1)
+// "fast_math" (RT_FAST_IEEE 0) replaces IEEE division / 1/sqrt by the hardware v_rcp_f32 / v_rsq_f32 (1 ulp);
+// EXACT and the default FAST build keep the reference's correctly rounded operations (the box tests' reciprocals
+// are the FAST kernels' own: prep / slab4, a cull only).
+#define RT_IEEE_PRIM (RT_EXACT || RT_FAST_IEEE)
+#define RT_IEEE_TRI RT_IEEE_PRIM
 __device__ __forceinline__ float rcp(float x) {              // slab reciprocals (FAST)
 #if RT_EXACT
     return 1.0f / x;

@@ -65,7 +65,7 @@ def test_c3_full_frame_fast_sah(gpu_lib, c3_scene, c3_oracle):
         rgba, rgb, st = r.render(0, want_rgb=True, count_work=True)     # raises on a traversal stack overflow
     assert abs(st["rays"] - ocnt["rays"]) <= 0.001 * ocnt["rays"], (st["rays"], ocnt["rays"])
     f, mx = frac_within(rgba, orgba)
-    assert f >= 0.995, (f, mx)
+    assert f >= 0.9995, (f, mx)                                          # SURVEY 8(c) depth >= 4: <= 0.05 % outliers
     for x0, y0, w, h in ((800, 620, 320, 160), (0, 0, 256, 128)):       # particle cluster, ground / sky
         f, mx = frac_within(rgba[y0:y0 + h, x0:x0 + w], orgba[y0:y0 + h, x0:x0 + w])
         assert f >= 0.995, ((x0, y0), f, mx)

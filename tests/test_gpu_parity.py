@@ -4,9 +4,12 @@ Tolerances:
   * EXACT mode (IEEE division, no FMA contraction) on identical trees: float RGB bit-identical,
     RGBA8 within 1 LSB (the GPU applies gamma with sqrtf, the reference with powf(x, 0.5)),
     identical work counters (rays, instance visits, primitive tests).
-  * FAST mode (reciprocal slabs / determinant, FMA): RGBA8 |d| <= 1 on >= 99.9 % of pixels at
-    depth 1-2 and >= 99.5 % at depth >= 4; per-ray closest hit identical on >= 99.9 % of rays
-    with |dt| <= 1e-4 * t.
+  * FAST mode (default: quad traversal with reciprocal slab culls, the reference's arithmetic for every value
+    that reaches a hit or a pixel): on identical trees bit-identical like EXACT (full C2 / C3 frames:
+    tests/test_gpu_parity_full.py); on other trees (SAH / LBVH: ties in the 1e-6 window) RGBA8 |d| <= 1 on
+    >= 99.9 % of pixels at depth 1-2 and >= 99.5 % at depth >= 4 on these small scenes; per-ray closest hit
+    identical on >= 99.9 % of rays with |dt| <= 1e-4 * t.  Option "fast_math" (hardware reciprocals, FMA) is
+    held to the same small-scene tolerance.
 """
 import numpy as np
 import pytest
@@ -94,9 +97,15 @@ def test_exact_mode_particles_and_animation(gpu_lib):
 
 @pytest.mark.parametrize("depth,need", [(1, 0.999), (2, 0.999), (10, 0.995)])
 def test_fast_mode_within_tolerance_demo(gpu_lib, depth, need):
+    """The default FAST kernel on the reference's trees is bit-identical to the oracle (its arithmetic is the
+    reference's wherever a value reaches a hit or a pixel); option "fast_math" is held to its tolerance."""
     r, o = pair(scenes.demo_scene(), 3, 240, 160, ray_trace_depth=depth)
     rgba, rgb, _ = r.render(0, want_rgb=True)
     orgb, orgba, _ = o.render(threads=THREADS)
+    assert (rgb != orgb).any(axis=2).sum() == 0, float(np.abs(rgb - orgb).max())
+    assert frac_within(rgba, orgba)[0] == 1.0
+    r.set_option("fast_math", 1)
+    rgba, rgb, _ = r.render(0, want_rgb=True)
     f, mx = frac_within(rgba, orgba)
     assert f >= need, (f, mx)
     assert np.abs(rgb - orgb).mean() < 2e-3
