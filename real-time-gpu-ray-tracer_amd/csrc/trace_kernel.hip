@@ -264,9 +264,11 @@ __device__ __forceinline__ bool sphere_test(const SphereHot &S, const RayP &r, f
     float delta = b * b - 4.0f * a * cc;
     if (delta < 0.0f) return false;
     delta = sqrtf(delta);
+    // the far root only when the near one is out of range (the same values; one correctly rounded division less
+    // for every ray that hits a sphere from outside, e.g. the ground)
     const float root1 = fdiv(-b - delta, a * 2.0f);
-    const float root2 = fdiv(-b + delta, a * 2.0f);
     if (in_range(root1, tmin, tmax)) { t = root1; return true; }
+    const float root2 = fdiv(-b + delta, a * 2.0f);
     if (in_range(root2, tmin, tmax)) { t = root2; return true; }
     return false;
 }
@@ -285,8 +287,9 @@ __device__ __forceinline__ bool quad_test(const QuadHot &Q, const RayP &r, float
     const f3 nx = ld3(Q.nx);
     if (fabsf(Q.den) < FZERO) return false;
     al = fdiv(dot(cross(p, ld3(Q.v)), nx), Q.den);
+    if (!in_range(al, 0.0f, 1.0f)) return false;                              // (the reference tests both after)
     be = fdiv(dot(cross(ld3(Q.u), p), nx), Q.den);
-    if (!in_range(al, 0.0f, 1.0f) || !in_range(be, 0.0f, 1.0f)) return false;
+    if (!in_range(be, 0.0f, 1.0f)) return false;
     t = tt;
     return true;
 }
