@@ -49,6 +49,7 @@ def test_paced_loop_holds_120_fps(gpu_lib):
     s = scenes.demo_with_particles(4)
     r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(256, 144, ray_trace_depth=2)
     buf = torch.zeros(256 * 144 * 4, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
     script = [interactive.input_state(key_w=1, dx=5)] * 12 + [interactive.input_state(key_quit=1)]
     t0 = time.perf_counter()
     cams, waits = interactive.run_scripted(r, script, [buf.data_ptr()], pace=True)

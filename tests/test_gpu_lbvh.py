@@ -234,6 +234,7 @@ def test_update_triangles_once_then_pipelined_frames(gpu_lib, double):
     r.set_option("overlap", L)
     lanes = [torch.cuda.Stream() for _ in range(L)]
     bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(F)]
+    torch.cuda.synchronize()
     for f in range(3):                                 # frames on the old triangles first: the lanes are warm
         r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=lanes[f % L].cuda_stream, sync=False)
     r.synchronize()

@@ -144,6 +144,7 @@ def _two_gpu_rank(rank, world, id_path, out_path):
     r.set_option("overlap", 3)                            # lanes beyond the attach-time communicators
     lanes = [torch.cuda.Stream() for _ in range(3)]
     bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(6)]
+    torch.cuda.synchronize()
     for f in range(6):
         r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=lanes[f % 3].cuda_stream, sync=False)
     r.synchronize()

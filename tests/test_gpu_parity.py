@@ -201,10 +201,12 @@ def test_tile_shards_assemble_to_full_frame(gpu_lib):
         slab_tiles = max(r.tiles_for_rank(tw, th, k, count) for k in range(count))
         slab_px = slab_tiles * tw * th
         gathered = torch.zeros(count * slab_px * 4, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()                  # torch's fill runs on its stream, not the scene's
         for k in range(count):
             r.render(0, tiles=(tw, th, k, count), rgba8_device=gathered.data_ptr() + k * slab_px * 4,
                      skip_update=True, want_rgba=False)
         frame = torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda")
+        torch.cuda.synchronize()
         r.assemble_tiles(gathered.data_ptr(), slab_tiles, tw, th, count, frame.data_ptr())
         r.synchronize()
         torch.cuda.synchronize()
@@ -429,6 +431,7 @@ def test_reorder_period_byte_identical(gpu_lib, period, lanes):
         r.set_option("overlap", lanes)
     streams = [torch.cuda.Stream() for _ in range(lanes)]
     bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(F)]
+    torch.cuda.synchronize()
     for f in range(F):
         r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=streams[f % lanes].cuda_stream, sync=False)
     torch.cuda.synchronize()
@@ -456,6 +459,7 @@ def test_claim_options_byte_identical(gpu_lib, opts):
         r.set_option(k, v)
     streams = [torch.cuda.Stream() for _ in range(3)]
     bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(F)]
+    torch.cuda.synchronize()
     for f in range(F):
         r.render(f, want_rgba=False, rgba8_device=bufs[f].data_ptr(), stream=streams[f % 3].cuda_stream, sync=False,
                  count_work=True, keep_counters=f > 0)
