@@ -22,6 +22,7 @@ def test_scripted_fly_through_equals_per_frame_camera(gpu_lib, lanes):
         r.set_option("overlap", lanes)
     streams = [torch.cuda.Stream() for _ in range(lanes)]
     bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(len(SCRIPT))]
+    torch.cuda.synchronize()                      # torch's fills run on its stream, not the lanes'
     script = [interactive.input_state(**d) for d in SCRIPT]
     cams, _ = interactive.run_scripted(r, script, [b.data_ptr() for b in bufs], streams=[x.cuda_stream for x in streams],
                                        pace=False, mouse_sensitivity=0.002)
