@@ -242,11 +242,6 @@ struct OutputGPU {
     const uint32_t *order;
     uint32_t *unit_cost;
     uint32_t cost_max;              // 1: a unit's cost is 64 x its longest path (atomicMax), not the sum of its paths
-    // persistent kernel, option "joiners": workgroups blockIdx.x >= core_blocks are late joiners — the grid is the
-    // whole resident capacity, but a launch that shares the GPU with other lanes' launches works with its first
-    // core_blocks workgroups; the rest are dispatched as slots free up and join only while the lane's queue still
-    // holds unclaimed items (a launch left alone at the end of a burst grows back to the whole GPU)
-    uint32_t core_blocks;
 };
 constexpr uint32_t QUEUE_STRIDE = 32;         // u32 words between partition heads (128 B lines)
 constexpr uint32_t QUEUE_MAX_PARTS = 8;

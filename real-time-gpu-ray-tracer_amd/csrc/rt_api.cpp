@@ -264,10 +264,6 @@ struct rt_scene {
     // that holds the rest of the GPU instead of waiting for its drain (C2, 3 lanes: 16 -> 0.260-0.261,
     // 8 -> 0.261-0.265, 0 -> 0.268-0.272 ms/frame; profiles/r02_sweep_lanes.jsonl)
     uint32_t reserve = 16;
-    // option "joiners": a launch on a partial grid ("grid_pct") is given the rest of the resident capacity as late-joiner
-    // workgroups, which work only while its queue still has items when they get a slot — the last frames of a burst
-    // are not left on a third of the GPU (layout.hpp OutputGPU::core_blocks)
-    bool joiners = true;
     uint32_t lane = 0;              // lane of the next rt_render (overlap)
     int last_lane = 0;              // lane of the last rt_render
     hipEvent_t ev_lane_done[NLANE] = {};   // last trace launch of each lane finished
@@ -1611,7 +1607,6 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     // consecutive frames concurrently on two streams.
     const int q = s->overlap ? (int)s->lane : 0;
     OutputGPU out{};
-    out.core_blocks = 0xFFFFFFFFu;             // every persistent workgroup is a core one unless "joiners" says otherwise
     out.nt_store = s->nt_store;
     const uint32_t W = s->width, H = s->height;
     size_t npix;
@@ -1827,12 +1822,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             // 0.052; profiles/r03_session2/share_grid_*.txt, lanes_new*.txt); alone: all of it
             pct = !partner ? 100u : (s->lanes <= 3 ? 50u : 100u / s->lanes + 12u);
         }
-        out.core_blocks = 0xFFFFFFFFu;
-        if (pct < 100) {
-            const uint32_t core = std::max<uint32_t>(8u, blocks * pct / 100u);
-            if (s->joiners) out.core_blocks = core;      // the rest of `blocks` join when the lane is left alone
-            else blocks = core;
-        }
+        if (pct < 100) blocks = std::max<uint32_t>(8u, blocks * pct / 100u);
         const uint32_t thr = s->threshold ? s->threshold : (cam.depth * cam.sqrt_s * cam.sqrt_s <= 2u ? 64u : 40u);
         HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, lane_counters, s->queue[q], blocks, thr,
                                                        s->variant, reset_queue, stream)
@@ -1968,9 +1958,6 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "fast_math") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "fast_math must be 0 or 1");
         s->fast_math = value == 1;
-    } else if (k == "joiners") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "joiners must be 0 or 1");
-        s->joiners = value == 1;
     } else if (k == "queue_parts") {
         if (value < 1 || value > (int64_t)QUEUE_MAX_PARTS) return fail(RT_ERR_INVALID_ARGUMENT, "queue_parts must be in 1..8");
         s->queue_parts = (uint32_t)value;

@@ -1227,25 +1227,6 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     __shared__ float4 lds_mat[LDS_MATERIALS];     // the scene's materials (shading reads them per hit)
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    if (blockIdx.x >= out.core_blocks) {
-        // a late joiner (option "joiners"): dispatched once a slot freed; it joins only while some band of the lane's
-        // queue still holds unclaimed items, and otherwise leaves before the LDS scene copy
-        bool open = false;
-        if (tid < (int)out.queue_parts) {
-            const uint32_t p = (uint32_t)tid, parts = out.queue_parts;
-            const uint32_t head = __hip_atomic_load(queue + p * QUEUE_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            uint32_t limit;
-            if (out.order) {
-                limit = __hip_atomic_load(queue + (QUEUE_MAX_PARTS + p) * QUEUE_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            } else {
-                const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
-                const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
-                limit = ((rows * (p + 1) / parts) - (rows * p / parts)) * upr * 64u;
-            }
-            open = head < limit;
-        }
-        if (!__syncthreads_or(open)) return;
-    }
     const bool mat_lds = sc.material_count <= LDS_MATERIALS;
     if (mat_lds && tid < (int)sc.material_count) lds_mat[tid] = reinterpret_cast<const float4 *>(sc.materials)[tid];
 #if !RT_EXACT
@@ -1564,7 +1545,7 @@ hipError_t launch_persistent_wpe(const SceneGPU &sc, const CameraGPU &cam, const
                                  uint32_t threshold, hipStream_t stream) {
     using namespace RT_SUFFIX(dev);
     const uint32_t need = (out.units + (BLOCK / 64) - 1) / (BLOCK / 64);
-    const dim3 grid(blocks_per_cu_cus < need ? blocks_per_cu_cus : need);   // core blocks + late joiners (out.core_blocks)
+    const dim3 grid(blocks_per_cu_cus < need ? blocks_per_cu_cus : need);
     if (count)
         hipLaunchKernelGGL((render_persistent_kernel<true, WPE, WIDE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
     else
