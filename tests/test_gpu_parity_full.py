@@ -47,7 +47,11 @@ CASES = {
     "C2d1": ("C2", dict(sample_count=1, ray_trace_depth=1)),
     "C2": ("C2", dict(sample_count=1, ray_trace_depth=2)),
     "C3": ("C3", dict(sample_count=4, ray_trace_depth=4)),
+    "C4": ("C4", dict(sample_count=1, ray_trace_depth=2)),     # the C3 scene at 1 spp, depth 2 (one GPU's frame)
+    "C5": ("C5", dict(sample_count=8, ray_trace_depth=2)),     # 10 M triangles, 4K, 8 -> 4 traced spp
 }
+# bench.py's configuration per case: the builder, the per-frame BLAS rebuild, the overlap lanes
+BENCH = {"C5": ("lbvh", True, 3)}
 
 
 @pytest.fixture(scope="module", params=list(CASES))
@@ -58,15 +62,19 @@ def case(request):
     return request.param, scene, cfg.width, cfg.height, cam, oracle_frames(scene, cfg.width, cfg.height, cam)
 
 
-def bench_frames(scene, W, H, cam, **opts):
-    """bench.py's configuration: SAH, 4 overlapped lanes on new streams, frames 0..37 pipelined into device buffers."""
+def bench_frames(scene, W, H, cam, name="C2", **opts):
+    """bench.py's configuration: SAH, 4 overlapped lanes on new streams, frames 0..37 pipelined into device buffers
+    (C5: GPU LBVH with every BLAS rebuilt each frame, 3 lanes with the current stream as the first)."""
     import torch
-    r = Renderer(scene).build_acceleration_structure(0, mode="sah").configure_camera(W, H, **cam)
+    build, rebuild, L = BENCH.get(name, ("sah", False, 4))
+    r = Renderer(scene).build_acceleration_structure(0, mode=build).configure_camera(W, H, **cam)
+    if rebuild:
+        r.set_option("rebuild", 1)
     for k, v in opts.items():
         r.set_option(k, v)
-    L = 4
     r.set_option("overlap", L)
-    lanes = [torch.cuda.Stream(priority=0) for _ in range(L)]
+    lanes = ([torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(L - 1)] if rebuild
+             else [torch.cuda.Stream(priority=0) for _ in range(L)])
     keep = {f: (torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda"),
                 torch.zeros(W * H * 3, dtype=torch.float32, device="cuda")) for f in FRAMES}
     scratch = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(L)]
@@ -84,7 +92,7 @@ def bench_frames(scene, W, H, cam, **opts):
 
 def test_bench_configuration_full_frame_within_survey_bars(gpu_lib, case):
     name, scene, W, H, cam, orc = case
-    got = bench_frames(scene, W, H, cam)
+    got = bench_frames(scene, W, H, cam, name)
     depth = cam["ray_trace_depth"]
     bar = 0.0001 if depth <= 2 else 0.0005
     for f in FRAMES:
@@ -116,7 +124,7 @@ def test_fast_math_option_measured_bar(gpu_lib, case):
     """Option "fast_math" (not the default): its own measured bar, <= 0.02 % outliers at depth <= 2 and <= 0.1 % at
     depth >= 4 on the bench configuration (measured 0.011 % / 0.088 %), and depth 1 within the float bar (measured 0)."""
     name, scene, W, H, cam, orc = case
-    got = bench_frames(scene, W, H, cam, fast_math=1)
+    got = bench_frames(scene, W, H, cam, name, fast_math=1)
     depth = cam["ray_trace_depth"]
     bar = 0.0002 if depth <= 2 else 0.001
     for f in FRAMES:
