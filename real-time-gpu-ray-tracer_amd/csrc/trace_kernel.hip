@@ -1253,11 +1253,15 @@ __device__ __forceinline__ uint64_t coop_owners(uint32_t helper_of) {
         owners |= 1ull << __builtin_amdgcn_readlane(helper_of, (int)__builtin_ctzll(m));
     return owners;
 }
-// idle lanes take entries from the bottom of tracing lanes' stack windows (round-robin over the owners)
-__device__ __forceinline__ void coop_steal(Trav &T, bool has, uint32_t &helper_of, uint32_t &px_steps, uint32_t lane) {
+// idle lanes take entries from the bottom of tracing lanes' stack windows (round-robin over the owners).
+// prefetch ("coop" 2): they copy the entries the owner pops next instead (top of its window) and traverse them
+// ahead of it, so its own fetches of those nodes and primitives hit in cache; nothing is taken from the owner and
+// nothing found is handed back, so every image stays exactly what the owner alone computes.
+__device__ __forceinline__ void coop_steal(Trav &T, bool has, uint32_t &helper_of, uint32_t &px_steps, uint32_t lane,
+                                           bool prefetch) {
     const bool idle = !has && !T.tracing && helper_of == NO_OWNER;
     const uint64_t idle_m = __ballot(idle);
-    const uint64_t own_m = __ballot(has && T.tracing && T.stk.sp >= 2);
+    const uint64_t own_m = __ballot(has && T.tracing && T.stk.sp >= (prefetch ? 1 : 2));
     if (!idle_m || !own_m) return;
     const uint32_t n_own = (uint32_t)__popcll(own_m);
     const uint32_t rank = (uint32_t)__popcll(idle_m & ((1ull << lane) - 1ull));
@@ -1274,7 +1278,16 @@ __device__ __forceinline__ void coop_steal(Trav &T, bool has, uint32_t &helper_o
         int take = -1;
         SEnt e;
         e.ref = REF_NONE; e.tn = 0u;
-        if (mine) {
+        if (mine && prefetch) {
+            uint32_t live = 0;
+            for (int k = sp_o - 1; k >= 0; k--) {           // the owner's next pops, nearest first
+                const SEnt c = unpack(col[k * BLOCK]);
+                if (__uint_as_float(c.tn) < tmax_o) {
+                    if (live == j) { take = k; e = c; break; }
+                    live++;
+                }
+            }
+        } else if (mine) {
             uint32_t live = 0;
             for (int k = 0; k + 1 < sp_o; k++) {           // the top entry stays with the owner (its next pop)
                 const SEnt c = unpack(col[k * BLOCK]);
@@ -1286,7 +1299,7 @@ __device__ __forceinline__ void coop_steal(Trav &T, bool has, uint32_t &helper_o
         }
         // every helper of o has read before any entry is marked taken (one wave: the loop above reconverges first)
         const bool got = take >= 0;
-        if (got) {
+        if (got && !prefetch) {
             SEnt dead = e;
             dead.tn = __float_as_uint(__builtin_huge_valf());
             col[take * BLOCK] = pack(dead);
@@ -1312,8 +1325,17 @@ __device__ __forceinline__ void coop_steal(Trav &T, bool has, uint32_t &helper_o
         }
     }
 }
-// after a round: one tmax per group; finished helpers hand their closest hit (and their steps) to the owner
-__device__ __forceinline__ void coop_sync(Trav &T, uint32_t &helper_of, uint32_t &px_steps, uint32_t lane) {
+// after a round: one tmax per group; finished helpers hand their closest hit (and their steps) to the owner.
+// prefetch: a helper only follows its owner's tmax down, and a finished one becomes idle again
+__device__ __forceinline__ void coop_sync(Trav &T, uint32_t &helper_of, uint32_t &px_steps, uint32_t lane, bool prefetch) {
+    if (prefetch) {
+        const float own = __shfl(T.tmax, (int)(helper_of == NO_OWNER ? lane : helper_of), 64);
+        if (helper_of != NO_OWNER) {
+            if (own < T.tmax) T.tmax = own;
+            if (!T.tracing) { helper_of = NO_OWNER; T.found = false; }
+        }
+        return;
+    }
     const uint64_t owners = coop_owners(helper_of);
     if (!owners) return;
     for (uint64_t m = owners; m; m &= m - 1) {
@@ -1491,20 +1513,25 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             continue;
         }
         // ---- traverse while enough lanes are busy
-        const bool coop = WIDE && out.coop && exhausted;    // wave-uniform: the cooperative tail (coop_steal)
-        uint64_t busy = 0;                                   // owners with a helper still attached (coop)
+        // wave-uniform: the cooperative tail (coop_steal; not in work-counting launches, which count the sequential work)
+        const bool coop = WIDE && !COUNT && out.coop && exhausted;
+        const bool prefetch = out.coop == 2;
+        uint64_t busy = 0;                                   // owners with a helper still attached (coop 1)
         for (;;) {
-            if (coop) coop_steal(T, has, helper_of, px_steps, (uint32_t)lane);
-            const uint64_t tr = __ballot(T.tracing);
+            if (coop) coop_steal(T, has, helper_of, px_steps, (uint32_t)lane, prefetch);
+            const uint64_t tr = __ballot(T.tracing && (helper_of == NO_OWNER || !prefetch));
             if (tr == 0) break;
-            if (coop) busy = coop_owners(helper_of);
+            if (coop && !prefetch) busy = coop_owners(helper_of);
             const uint64_t want = __ballot(!T.tracing && (has || !exhausted) && !((busy >> lane) & 1ull));
             if ((uint32_t)__popcll(want) >= threshold) break;
             spec_round<COUNT, WIDE>(T, sc, spill, cnt, pc, px_steps, COUNT || track);
-            if (coop) coop_sync(T, helper_of, px_steps, (uint32_t)lane);
+            if (coop) coop_sync(T, helper_of, px_steps, (uint32_t)lane, prefetch);
             n_rounds++;
         }
-        if (coop) busy = coop_owners(helper_of);
+        if (coop && !prefetch) busy = coop_owners(helper_of);
+        if (coop && prefetch && helper_of != NO_OWNER) {     // prefetchers still walking when their owners finished
+            T.tracing = false; T.found = false; helper_of = NO_OWNER;
+        }
         // ---- shade lanes whose segment finished (rayColor body, Kernel.cu:64-100)
         n_shades++;
         DIAG_T(t_shade);

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of one scene option on bench lines (interleaved runs in one call).
-# usage: OPT=joiners scripts/r04_ab.sh OUTNAME   (runs each case with --opt $OPT=0 and =1, REPS times)
+# usage: OPT=name [VALS="0 1"] scripts/r04_ab.sh OUTNAME   (runs each case with --opt $OPT=v for v in VALS, REPS times)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/$1
 mkdir -p $OUT
@@ -17,7 +17,7 @@ for rep in $(seq 1 $REPS); do
   IFS=';' read -ra CS <<< "$CASES"
   for c in "${CS[@]}"; do
     name=${c%%|*}; args=${c#*|}
-    for v in 0 1; do
+    for v in ${VALS:-0 1}; do
       timeout -k 10 300 python3 bench.py $args --no-cpu-baseline --opt $OPT=$v > $OUT/${name}_${v}_$rep.log 2>&1
       rc=$?
       if [ $rc -ne 0 ]; then echo "$name $v rc=$rc"; tail -5 $OUT/${name}_${v}_$rep.log; exit $rc; fi
