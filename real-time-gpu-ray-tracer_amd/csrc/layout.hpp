@@ -242,7 +242,6 @@ struct OutputGPU {
     const uint32_t *order;
     uint32_t *unit_cost;
     uint32_t cost_max;              // 1: a unit's cost is 64 x its longest path (atomicMax), not the sum of its paths
-    uint32_t coop;                  // option "coop": a wave whose queue is dry lends its idle lanes to its long paths
 };
 constexpr uint32_t QUEUE_STRIDE = 32;         // u32 words between partition heads (128 B lines)
 constexpr uint32_t QUEUE_MAX_PARTS = 8;

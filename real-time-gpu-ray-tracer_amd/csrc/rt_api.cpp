@@ -278,11 +278,6 @@ struct rt_scene {
     // correctly rounded arithmetic (C2 -7 %, C3 -9 % per pipelined frame; 0.008-0.09 % of pixels then differ from the
     // oracle even on its own trees); default 0: bit-identical to the oracle on the reference's trees
     bool fast_math = false;
-    // option "coop": FAST quad-tree frames — once a wave's queue is dry, its idle lanes help the long paths it still
-    // holds (trace_kernel.hip coop_steal): 1 = they take pending subtrees and hand their closest hits back (hits can
-    // then resolve 1e-6 ties in another order, depending on timing), 2 = they only walk ahead of the owner as
-    // prefetchers (images unchanged); 0 = off
-    uint32_t coop = 0;
     double update_wait_ms = 0.0;    // last frame_update: time blocked on ev_copied (GPU progress)
     bool use_persistent = true;
     uint32_t queue_parts = 8;       // one band per XCD (measured with "reorder": 8 beat 4, 2 and 1 on C2)
@@ -1694,7 +1689,6 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
 
     if (s->use_persistent) {
         out.queue_parts = s->queue_parts;
-        out.coop = s->coop;
         out.grab = s->grab;
         out.supertile = s->supertile;
         if (s->timeline_on) {
@@ -1961,9 +1955,6 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "variant") {
         if (value != 0 && value != 4) return fail(RT_ERR_INVALID_ARGUMENT, "variant must be 0 or 4");
         s->variant = (uint32_t)value;
-    } else if (k == "coop") {
-        if (value < 0 || value > 2) return fail(RT_ERR_INVALID_ARGUMENT, "coop must be 0, 1 or 2");
-        s->coop = (uint32_t)value;
     } else if (k == "fast_math") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "fast_math must be 0 or 1");
         s->fast_math = value == 1;

@@ -1220,152 +1220,6 @@ __device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t
     }
 }
 
-// ---- cooperative tail (option "coop", FAST quad-tree kernel) -----------------------------------------------
-// Once a wave's queue is dry it gets no new pixels, and a launch ends with the few long paths its last waves hold
-// (C2: the median wave's queue runs dry at ~225 us of a ~310 us serialised launch; a synchronous 1/8 share: 50 of
-// 137 us): each of those paths then runs alone, one dependent node fetch after the other.  From then on a wave's
-// idle lanes become helpers: each takes a pending entry (a far subtree, or the rest of a TLAS leaf) from the bottom
-// of a tracing lane's LDS stack window and traverses it with that lane's ray (world ray, instance-space ray of its
-// current instance, tmax); the owner culls the taken entry (its entry t set to +inf).  After every round the
-// group's tmax is the minimum of its members' (a closer hit found by one culls the others), and a helper whose
-// subtree is done hands its closest hit to the owner, which shades once no helper of it is tracing.  The closest
-// hit is the one sequential traversal finds, except where two surfaces lie within the 1e-6 window (the later-
-// tested one wins, Range.cuh:33-43) — the same tolerance as any other visit order (quad trees, SAH).
-constexpr uint32_t NO_OWNER = 64u;
-__device__ __forceinline__ float wave_min_f(float v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
-    return v;
-}
-__device__ __forceinline__ void shfl_ray(RayP &r, const RayP &src, int o) {
-    r.o = mk(__shfl(src.o.x, o, 64), __shfl(src.o.y, o, 64), __shfl(src.o.z, o, 64));
-    r.d = mk(__shfl(src.d.x, o, 64), __shfl(src.d.y, o, 64), __shfl(src.d.z, o, 64));
-#if !RT_EXACT
-    r.inv = mk(__shfl(src.inv.x, o, 64), __shfl(src.inv.y, o, 64), __shfl(src.inv.z, o, 64));
-    r.oinv = mk(__shfl(src.oinv.x, o, 64), __shfl(src.oinv.y, o, 64), __shfl(src.oinv.z, o, 64));
-    r.tiny = __shfl((int)src.tiny, o, 64) != 0;
-#endif
-}
-// owners (lanes with a helper still attached), as a wave-uniform mask
-__device__ __forceinline__ uint64_t coop_owners(uint32_t helper_of) {
-    uint64_t owners = 0;
-    for (uint64_t m = __ballot(helper_of != NO_OWNER); m; m &= m - 1)
-        owners |= 1ull << __builtin_amdgcn_readlane(helper_of, (int)__builtin_ctzll(m));
-    return owners;
-}
-// idle lanes take entries from the bottom of tracing lanes' stack windows (round-robin over the owners).
-// prefetch ("coop" 2): they copy the entries the owner pops next instead (top of its window) and traverse them
-// ahead of it, so its own fetches of those nodes and primitives hit in cache; nothing is taken from the owner and
-// nothing found is handed back, so every image stays exactly what the owner alone computes.
-__device__ __forceinline__ void coop_steal(Trav &T, bool has, uint32_t &helper_of, uint32_t &px_steps, uint32_t lane,
-                                           bool prefetch) {
-    const bool idle = !has && !T.tracing && helper_of == NO_OWNER;
-    const uint64_t idle_m = __ballot(idle);
-    const uint64_t own_m = __ballot(has && T.tracing && T.stk.sp >= (prefetch ? 1 : 2));
-    if (!idle_m || !own_m) return;
-    const uint32_t n_own = (uint32_t)__popcll(own_m);
-    const uint32_t rank = (uint32_t)__popcll(idle_m & ((1ull << lane) - 1ull));
-    uint32_t idx = 0;
-    for (uint64_t om = own_m; om; om &= om - 1, idx++) {
-        const int o = (int)__builtin_ctzll(om);
-        const bool mine = idle && rank % n_own == idx;
-        const uint64_t hm = __ballot(mine);
-        if (!hm) continue;
-        const int sp_o = __builtin_amdgcn_readlane(T.stk.sp, o);
-        const float tmax_o = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(T.tmax), o));
-        const uint32_t j = (uint32_t)__popcll(hm & ((1ull << lane) - 1ull));   // this helper's rank at owner o
-        LdsU2 *col = T.stk.lds + ((int)o - (int)lane);                          // owner o's stack column
-        int take = -1;
-        SEnt e;
-        e.ref = REF_NONE; e.tn = 0u;
-        if (mine && prefetch) {
-            uint32_t live = 0;
-            for (int k = sp_o - 1; k >= 0; k--) {           // the owner's next pops, nearest first
-                const SEnt c = unpack(col[k * BLOCK]);
-                if (__uint_as_float(c.tn) < tmax_o) {
-                    if (live == j) { take = k; e = c; break; }
-                    live++;
-                }
-            }
-        } else if (mine) {
-            uint32_t live = 0;
-            for (int k = 0; k + 1 < sp_o; k++) {           // the top entry stays with the owner (its next pop)
-                const SEnt c = unpack(col[k * BLOCK]);
-                if (__uint_as_float(c.tn) < tmax_o) {
-                    if (live == j) { take = k; e = c; break; }
-                    live++;
-                }
-            }
-        }
-        // every helper of o has read before any entry is marked taken (one wave: the loop above reconverges first)
-        const bool got = take >= 0;
-        if (got && !prefetch) {
-            SEnt dead = e;
-            dead.tn = __float_as_uint(__builtin_huge_valf());
-            col[take * BLOCK] = pack(dead);
-        }
-        const uint64_t gm = __ballot(got);
-        if (!gm) continue;
-        // the owner's ray state (every lane executes the shuffles; the takers keep it)
-        RayP wr, lr;
-        shfl_ray(wr, T.wr, o);
-        shfl_ray(lr, T.lr, o);
-        const uint32_t inst_o = (uint32_t)__builtin_amdgcn_readlane((int)T.cur_inst, o);
-        if (got) {
-            T.wr = wr; T.lr = lr;
-            T.cur_inst = inst_o;
-            T.tmax = tmax_o;
-            T.cur = e.ref; T.curT = __uint_as_float(e.tn);
-            T.pleaf = REF_NONE;
-            T.stk.sp = 0; T.stk.spilled = 0;
-            T.found = false;
-            T.tracing = true;
-            helper_of = (uint32_t)o;
-            px_steps = 0;
-        }
-    }
-}
-// after a round: one tmax per group; finished helpers hand their closest hit (and their steps) to the owner.
-// prefetch: a helper only follows its owner's tmax down, and a finished one becomes idle again
-__device__ __forceinline__ void coop_sync(Trav &T, uint32_t &helper_of, uint32_t &px_steps, uint32_t lane, bool prefetch) {
-    if (prefetch) {
-        const float own = __shfl(T.tmax, (int)(helper_of == NO_OWNER ? lane : helper_of), 64);
-        if (helper_of != NO_OWNER) {
-            if (own < T.tmax) T.tmax = own;
-            if (!T.tracing) { helper_of = NO_OWNER; T.found = false; }
-        }
-        return;
-    }
-    const uint64_t owners = coop_owners(helper_of);
-    if (!owners) return;
-    for (uint64_t m = owners; m; m &= m - 1) {
-        const uint32_t o = (uint32_t)__builtin_ctzll(m);
-        const bool in = lane == o || helper_of == o;
-        const float g = wave_min_f(in ? T.tmax : __builtin_huge_valf());
-        if (in && g < T.tmax) T.tmax = g;
-    }
-    for (uint64_t m = __ballot(helper_of != NO_OWNER && !T.tracing); m; m &= m - 1) {
-        const int h = (int)__builtin_ctzll(m);
-        const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)helper_of, h);
-        const uint32_t steps_h = (uint32_t)__builtin_amdgcn_readlane((int)px_steps, h);
-        if (__builtin_amdgcn_readlane((int)T.found, h)) {
-            const float ht = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(T.hit.t), h));
-            if (lane == o && (!T.found || ht < T.hit.t)) {
-                T.hit.t = ht;
-                T.hit.inst = (uint32_t)__builtin_amdgcn_readlane((int)T.hit.inst, h);
-                T.hit.ptype = (uint32_t)__builtin_amdgcn_readlane((int)T.hit.ptype, h);
-                T.hit.slot = (uint32_t)__builtin_amdgcn_readlane((int)T.hit.slot, h);
-                T.hit.u = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(T.hit.u), h));
-                T.hit.v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(T.hit.v), h));
-                T.found = true;
-                if (ht < T.tmax) T.tmax = ht;
-            }
-        }
-        if (lane == o) px_steps += steps_h;
-        if ((int)lane == h) { helper_of = NO_OWNER; T.found = false; }
-    }
-}
-
 template <bool COUNT, bool WIDE>
 __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out,
                                                        uint32_t *queue, uint32_t threshold, unsigned long long *counters) {
@@ -1390,7 +1244,6 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     uint32_t rays = 0, pixels = 0;
 
     bool has = false;                  // lane owns a pixel
-    uint32_t helper_of = NO_OWNER;     // cooperative tail: the lane whose ray this idle lane is helping with
     uint32_t px_steps = 0;             // traversal steps spent on the lane's pixel (COUNT cost map, reorder)
     uint32_t item = 0, sample = 0, depth = 0;
     Rng rng;
@@ -1513,30 +1366,19 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             continue;
         }
         // ---- traverse while enough lanes are busy
-        // wave-uniform: the cooperative tail (coop_steal; not in work-counting launches, which count the sequential work)
-        const bool coop = WIDE && !COUNT && out.coop && exhausted;
-        const bool prefetch = out.coop == 2;
-        uint64_t busy = 0;                                   // owners with a helper still attached (coop 1)
         for (;;) {
-            if (coop) coop_steal(T, has, helper_of, px_steps, (uint32_t)lane, prefetch);
-            const uint64_t tr = __ballot(T.tracing && (helper_of == NO_OWNER || !prefetch));
+            const uint64_t tr = __ballot(T.tracing);
             if (tr == 0) break;
-            if (coop && !prefetch) busy = coop_owners(helper_of);
-            const uint64_t want = __ballot(!T.tracing && (has || !exhausted) && !((busy >> lane) & 1ull));
+            const uint64_t want = __ballot(!T.tracing && (has || !exhausted));
             if ((uint32_t)__popcll(want) >= threshold) break;
             spec_round<COUNT, WIDE>(T, sc, spill, cnt, pc, px_steps, COUNT || track);
-            if (coop) coop_sync(T, helper_of, px_steps, (uint32_t)lane, prefetch);
             n_rounds++;
-        }
-        if (coop && !prefetch) busy = coop_owners(helper_of);
-        if (coop && prefetch && helper_of != NO_OWNER) {     // prefetchers still walking when their owners finished
-            T.tracing = false; T.found = false; helper_of = NO_OWNER;
         }
         // ---- shade lanes whose segment finished (rayColor body, Kernel.cu:64-100)
         n_shades++;
         DIAG_T(t_shade);
         bool fin = false;                    // lane wrote its pixel in this step
-        if (has && !T.tracing && !((busy >> lane) & 1ull)) {
+        if (has && !T.tracing) {
             rays++;
             bool path_done;
             f3 no = T.wr.o, nd = T.wr.d;                                     // next segment
