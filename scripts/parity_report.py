@@ -71,10 +71,12 @@ def main():
             oracle[f] = (orgb, orgba)
             print(f"oracle {cname} frame {f}: {time.time() - t0:.1f} s", flush=True)
         for mode in args.modes.split(","):
-            build = "sah" if mode == "bench" else "compat"
+            build = {"bench": "sah", "lbvh": "lbvh", "lbvh_nogroup": "lbvh", "sah_nogroup": "sah"}.get(mode, "compat")
             r = Renderer(scene)
             if mode == "fast_compat_binary":                 # FAST arithmetic on the reference's binary visit order
                 r.set_option("wide", 0)
+            if mode.endswith("_nogroup"):                    # one TLAS item per particle, as the reference has them
+                r.set_option("group", 0)
             r.build_acceleration_structure(0, mode=build).configure_camera(W, H, **cam)
             got = {}
             if mode == "bench":

