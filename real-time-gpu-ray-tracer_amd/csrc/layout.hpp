@@ -242,13 +242,6 @@ struct OutputGPU {
     const uint32_t *order;
     uint32_t *unit_cost;
     uint32_t cost_max;              // 1: a unit's cost is 64 x its longest path (atomicMax), not the sum of its paths
-    // option "joiners": workgroups blockIdx.x >= core_blocks are late joiners of a launch given a partial grid while
-    // other lanes' launches ran.  A joiner works only when its launch is the scene's only one in flight (the last frame
-    // of a burst), else it leaves at once; inflight[0] counts the scene's launches in flight (the first wave of a
-    // launch adds one, the last of its waves to finish takes it back), done_waves is this lane's finished-wave count
-    uint32_t core_blocks;
-    uint32_t *inflight;
-    uint32_t *done_waves;
 };
 constexpr uint32_t QUEUE_STRIDE = 32;         // u32 words between partition heads (128 B lines)
 constexpr uint32_t QUEUE_MAX_PARTS = 8;

@@ -264,11 +264,6 @@ struct rt_scene {
     // that holds the rest of the GPU instead of waiting for its drain (C2, 3 lanes: 16 -> 0.260-0.261,
     // 8 -> 0.261-0.265, 0 -> 0.268-0.272 ms/frame; profiles/r02_sweep_lanes.jsonl)
     uint32_t reserve = 16;
-    // option "joiners": a launch given a partial grid ("grid_pct" auto, other lanes in flight) is launched on the whole
-    // capacity; the workgroups beyond its share work only if it is left as the scene's only launch in flight (the last
-    // frames of a burst, which otherwise end on a third of the GPU) and leave at once otherwise
-    bool joiners = false;
-    uint32_t *launch_ctr = nullptr;           // device: [0] launches in flight, [1 + q] lane q's finished waves
     uint32_t lane = 0;              // lane of the next rt_render (overlap)
     int last_lane = 0;              // lane of the last rt_render
     hipEvent_t ev_lane_done[NLANE] = {};   // last trace launch of each lane finished
@@ -453,7 +448,6 @@ struct rt_scene {
             if (ev_lane_done[q]) (void)hipEventDestroy(ev_lane_done[q]);
         }
         if (counters_host) (void)hipHostFree(counters_host);
-        if (launch_ctr) (void)hipFree(launch_ctr);
         for (uint32_t i = 0; i < RING; i++) {
             if (ring_start[i]) (void)hipEventDestroy(ring_start[i]);
             if (ring_stop[i]) (void)hipEventDestroy(ring_stop[i]);
@@ -1428,10 +1422,6 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         if (!s->ring_stop[i]) HIP_TRY(hipEventCreate(&s->ring_stop[i]));
         if (!s->ring_post[i]) HIP_TRY(hipEventCreateWithFlags(&s->ring_post[i], hipEventDisableTiming));
     }
-    if (!s->launch_ctr) {
-        HIP_TRY(hipMalloc(&s->launch_ctr, (1 + rt_scene::NLANE) * sizeof(uint32_t)));
-        HIP_TRY(hipMemset(s->launch_ctr, 0, (1 + rt_scene::NLANE) * sizeof(uint32_t)));
-    }
     if (!s->counters) {
         HIP_TRY(hipMalloc(&s->counters, rt_scene::NLANE * CNT_NUM * sizeof(unsigned long long)));
         HIP_TRY(hipMemset(s->counters, 0, rt_scene::NLANE * CNT_NUM * sizeof(unsigned long long)));
@@ -1617,7 +1607,6 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     // consecutive frames concurrently on two streams.
     const int q = s->overlap ? (int)s->lane : 0;
     OutputGPU out{};
-    out.core_blocks = 0xFFFFFFFFu;             // every persistent workgroup is a core one unless "joiners" says otherwise
     out.nt_store = s->nt_store;
     const uint32_t W = s->width, H = s->height;
     size_t npix;
@@ -1833,18 +1822,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             // 0.052; profiles/r03_session2/share_grid_*.txt, lanes_new*.txt); alone: all of it
             pct = !partner ? 100u : (s->lanes <= 3 ? 50u : 100u / s->lanes + 12u);
         }
-        if (pct < 100) {
-            const uint32_t core = std::max<uint32_t>(8u, blocks * pct / 100u);
-            if (s->joiners && s->launch_ctr) {      // the rest of the capacity joins when this launch is left alone
-                out.core_blocks = core;
-            } else {
-                blocks = core;
-            }
-        }
-        if (s->joiners && s->launch_ctr) {          // every launch keeps the scene's in-flight count
-            out.inflight = s->launch_ctr;
-            out.done_waves = s->launch_ctr + 1 + q;
-        }
+        if (pct < 100) blocks = std::max<uint32_t>(8u, blocks * pct / 100u);
         const uint32_t thr = s->threshold ? s->threshold : (cam.depth * cam.sqrt_s * cam.sqrt_s <= 2u ? 64u : 40u);
         HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, lane_counters, s->queue[q], blocks, thr,
                                                        s->variant, reset_queue, stream)
@@ -1980,11 +1958,6 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "fast_math") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "fast_math must be 0 or 1");
         s->fast_math = value == 1;
-    } else if (k == "joiners") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "joiners must be 0 or 1");
-        RT_TRY(drain(s));                             // no launch in flight keeps an old count
-        if (s->launch_ctr) HIP_TRY(hipMemset(s->launch_ctr, 0, (1 + rt_scene::NLANE) * sizeof(uint32_t)));
-        s->joiners = value == 1;
     } else if (k == "queue_parts") {
         if (value < 1 || value > (int64_t)QUEUE_MAX_PARTS) return fail(RT_ERR_INVALID_ARGUMENT, "queue_parts must be in 1..8");
         s->queue_parts = (uint32_t)value;

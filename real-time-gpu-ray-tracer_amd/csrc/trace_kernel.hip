@@ -1227,41 +1227,6 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     __shared__ float4 lds_mat[LDS_MATERIALS];     // the scene's materials (shading reads them per hit)
     const int tid = threadIdx.x;
     const int lane = tid & 63;
-    const bool joiner = blockIdx.x >= out.core_blocks;
-    if (out.inflight) {
-        if (blockIdx.x == 0 && tid == 0) atomicAdd(out.inflight, 1u);
-        if (joiner) {
-            // a late joiner (option "joiners"): it joins only while its launch is the only one in flight and its queue
-            // still holds unclaimed items; otherwise it leaves before the LDS scene copy (a finished-wave count each)
-            bool open = false;
-            if (tid == 0) open = __hip_atomic_load(out.inflight, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u;
-            if (tid >= 64 && tid < 64 + (int)out.queue_parts) {
-                const uint32_t p = (uint32_t)(tid - 64), parts = out.queue_parts;
-                const uint32_t head = __hip_atomic_load(queue + p * QUEUE_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                uint32_t limit;
-                if (out.order) {
-                    limit = __hip_atomic_load(queue + (QUEUE_MAX_PARTS + p) * QUEUE_STRIDE, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                } else {
-                    const uint32_t rows = out.tile_count == 0 ? out.units / out.units_x : out.units;
-                    const uint32_t upr = out.tile_count == 0 ? out.units_x : 1u;
-                    limit = ((rows * (p + 1) / parts) - (rows * p / parts)) * upr * 64u;
-                }
-                open = head < limit;
-            }
-            __shared__ uint32_t votes[2];
-            if (tid < 2) votes[tid] = 0u;
-            __syncthreads();
-            if (open) atomicOr(&votes[tid < 64 ? 0 : 1], 1u);
-            __syncthreads();
-            if (!(votes[0] && votes[1])) {
-                if (lane == 0) {
-                    const uint32_t total = gridDim.x * (BLOCK / 64);
-                    if (atomicAdd(out.done_waves, 1u) + 1u == total) { *out.done_waves = 0u; atomicSub(out.inflight, 1u); }
-                }
-                return;
-            }
-        }
-    }
     const bool mat_lds = sc.material_count <= LDS_MATERIALS;
     if (mat_lds && tid < (int)sc.material_count) lds_mat[tid] = reinterpret_cast<const float4 *>(sc.materials)[tid];
 #if !RT_EXACT
@@ -1499,10 +1464,6 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     if (lane == 0) {
         atomicAdd(&counters[CNT_RAYS], (unsigned long long)wr);
         atomicAdd(&counters[CNT_PIXELS], (unsigned long long)wp);
-        if (out.inflight) {                       // the launch's last wave: it is no longer in flight
-            const uint32_t total = gridDim.x * (BLOCK / 64);
-            if (atomicAdd(out.done_waves, 1u) + 1u == total) { *out.done_waves = 0u; atomicSub(out.inflight, 1u); }
-        }
         if (out.timeline) {
             // the wave's index from its stack window address (threadIdx.x kept live to here was spilled)
             const uint32_t wv = (uint32_t)((const unsigned long long *)T.stk.lds - &lds_stack[0][0]) >> 6;
