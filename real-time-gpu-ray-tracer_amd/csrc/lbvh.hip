@@ -124,9 +124,6 @@ __device__ __forceinline__ uint32_t quant10(float c, float lo, float hi) {
     return q >= 1023.0f ? 1023u : (uint32_t)q;
 }
 
-__device__ __forceinline__ uint32_t seg_of_sorted(const unsigned long long *keys, uint32_t p) {
-    return (uint32_t)(keys[p] >> 32);
-}
 
 // ---- kernels -------------------------------------------------------------------------------
 __global__ void init_bounds_kernel(uint32_t *bounds, uint32_t n_segs) {
@@ -230,13 +227,13 @@ __global__ __launch_bounds__(BLOCK) void bounds_kernel(const uint32_t *seg_of, c
 // box up to the root inherits its extent, so rays descend into those subtrees for nothing (measured: a
 // GPU TLAS over C2's instances made the launch 28 % slower than the host SAH TLAS).
 __global__ void morton_kernel(const uint32_t *seg_of, const float4 *cent, uint32_t n, const uint32_t *bounds,
-                              const float *size_box, unsigned long long *keys, uint32_t *vals) {
+                              const float *size_box, uint32_t *keys, uint32_t *vals) {
     const uint32_t it = blockIdx.x * BLOCK + threadIdx.x;
     if (it >= n) return;
     const uint32_t seg = seg_of[it];
     const float4 c = cent[it];
     if (c.w != 0.0f) {                           // inactive item: behind every active one (no class bits reach ~0)
-        keys[it] = ((unsigned long long)seg << 32) | 0xFFFFFFFFull;
+        keys[it] = 0xFFFFFFFFu;
         vals[it] = it;
         return;
     }
@@ -252,24 +249,57 @@ __global__ void morton_kernel(const uint32_t *seg_of, const float4 *cent, uint32
         const uint32_t cls = ext >= 0.5f * spread ? 0u : (ext >= 0.0625f * spread ? 1u : 2u);
         m |= cls << 30;
     }
-    keys[it] = ((unsigned long long)seg << 32) | m;
+    keys[it] = m;
     vals[it] = it;
 }
 
+// Sorting happens per segment (items never leave their segment's range): trees of <= LOCAL_SORT_MAX items are
+// sorted by one workgroup in LDS (bitonic over (code, item) pairs, which is the stable radix order), larger ones by
+// one rocPRIM radix sort each over their 30- or 32-bit codes (LbvhBuilder::build).  A 64-bit (segment, code) key
+// over the whole forest cost C5 five 8-bit passes over 10 M 12-byte pairs per rebuild.
+constexpr uint32_t LOCAL_SORT_MAX = 2048;
+__global__ __launch_bounds__(BLOCK) void local_sort_kernel(const LbvhSeg *segs, const uint32_t *keys_in, uint32_t *keys_out,
+                                                           uint32_t *vals_out) {
+    __shared__ unsigned long long sk[LOCAL_SORT_MAX];
+    const LbvhSeg S = segs[blockIdx.x];
+    if (S.count == 0 || S.count > LOCAL_SORT_MAX) return;              // block-uniform
+    const uint32_t m = S.count, t = threadIdx.x;
+    uint32_t np = 1;
+    while (np < m) np <<= 1;
+    for (uint32_t k = t; k < np; k += BLOCK)
+        sk[k] = k < m ? ((unsigned long long)keys_in[S.item_base + k] << 32) | k : ~0ull;
+    __syncthreads();
+    for (uint32_t size = 2; size <= np; size <<= 1)
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (uint32_t k = t; k < np; k += BLOCK) {
+                const uint32_t o = k ^ stride;
+                if (o > k) {
+                    const unsigned long long x = sk[k], y = sk[o];
+                    if ((x > y) == ((k & size) == 0)) { sk[k] = y; sk[o] = x; }
+                }
+            }
+            __syncthreads();
+        }
+    for (uint32_t k = t; k < m; k += BLOCK) {
+        keys_out[S.item_base + k] = (uint32_t)(sk[k] >> 32);
+        vals_out[S.item_base + k] = S.item_base + (uint32_t)sk[k];
+    }
+}
+
 // Karras 2012, one thread per interior node.  Local indices are positions inside the segment.
-__global__ void karras_kernel(const LbvhSeg *segs, const unsigned long long *keys, uint32_t n, uint32_t *child,
+__global__ void karras_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *keys, uint32_t n, uint32_t *child,
                               uint32_t *parent, uint32_t *parent_leaf, uint32_t *range, uint32_t *flag) {
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
     if (p >= n) return;
-    const LbvhSeg S = segs[seg_of_sorted(keys, p)];
+    const LbvhSeg S = segs[seg_of[p]];
     const int m = (int)S.count;
     const int i = (int)(p - S.item_base);
-    const unsigned long long *K = keys + S.item_base;
+    const uint32_t *K = keys + S.item_base;
     if (m == 1) { parent_leaf[p] = NONE; return; }
     if (i >= m - 1) return;
     auto delta = [&](int a, int b) -> int {
         if (b < 0 || b >= m) return -1;
-        const uint32_t ka = (uint32_t)K[a], kb = (uint32_t)K[b];
+        const uint32_t ka = K[a], kb = K[b];
         if (ka != kb) return __clz(ka ^ kb);
         return 32 + __clz((uint32_t)a ^ (uint32_t)b);
     };
@@ -426,7 +456,7 @@ __device__ __forceinline__ void climb_top(const LbvhSeg &S, uint32_t g, const ui
     }
 }
 
-__global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *segs, const unsigned long long *keys,
+__global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *segs, const uint32_t *seg_of,
                                                                 const uint32_t *vals, const float *item_box, uint32_t n,
                                                                 const uint32_t *child, const uint32_t *parent,
                                                                 const uint32_t *parent_leaf, const uint32_t *range,
@@ -439,7 +469,7 @@ __global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *s
     __shared__ uint32_t snode[CHUNK];
     const uint32_t lo = blockIdx.x * CHUNK, p = lo + threadIdx.x;
     sflag[threadIdx.x] = 0;
-    const bool big = p < n && segs[seg_of_sorted(keys, p)].count > LOCAL_MAX;   // else bottom_up_local_kernel
+    const bool big = p < n && segs[seg_of[p]].count > LOCAL_MAX;   // else bottom_up_local_kernel
     if (big) {
         const float2 *src = reinterpret_cast<const float2 *>(item_box + 6 * (size_t)vals[p]);
 #pragma unroll
@@ -447,7 +477,7 @@ __global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *s
     }
     __syncthreads();
     if (big) {
-        const LbvhSeg S = segs[seg_of_sorted(keys, p)];
+        const LbvhSeg S = segs[seg_of[p]];
         uint32_t g = parent_leaf[p];
         bool first = false;                             // stopped as a node's first arrival
         while (g != NONE && chunk_local(range, g)) {
@@ -498,19 +528,19 @@ __global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *s
 #pragma unroll
         for (int k = 0; k < 6; k++) nbox[6 * (size_t)g + k] = sbox[6 * l + k];
         height[g] = sheight[l];
-        kept[g] = (range[2 * g + 1] - range[2 * g] + 1u) > segs[seg_of_sorted(keys, p)].leaf_cap ? 1u : 0u;
+        kept[g] = (range[2 * g + 1] - range[2 * g] + 1u) > segs[seg_of[p]].leaf_cap ? 1u : 0u;
     }
 }
 
 // the top pass: one climb per arrival the chunk pass recorded (frontier[0] = count, then crossing-node ids)
-__global__ void bottom_up_top_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals,
+__global__ void bottom_up_top_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *vals,
                                      const float *item_box, const uint32_t *child, const uint32_t *parent,
                                      const uint32_t *range, uint32_t *flag, float *nbox, uint32_t *height, uint32_t *kept,
                                      const uint32_t *frontier) {
     const uint32_t count = frontier[0];
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < count; i += gridDim.x * BLOCK) {
         const uint32_t g = frontier[1 + i];
-        climb_top(segs[seg_of_sorted(keys, range[2 * g])], g, vals, item_box, child, parent, range, flag, nbox, height, kept);
+        climb_top(segs[seg_of[range[2 * g]]], g, vals, item_box, child, parent, range, flag, nbox, height, kept);
     }
 }
 
@@ -527,14 +557,14 @@ __device__ __forceinline__ const float *child_box(uint32_t ch, const uint32_t *v
     return (ch & LEAF_BIT) ? item_box + 6 * (size_t)vals[ch & ~LEAF_BIT] : nbox + 6 * (size_t)ch;
 }
 
-__global__ void emit_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals, const float *item_box,
+__global__ void emit_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *vals, const float *item_box,
                             uint32_t n_int, const uint32_t *child, const uint32_t *range, const float *nbox,
                             const uint32_t *kept, const uint32_t *pidx, NodePair *pairs, uint32_t *pair_count) {
     const uint32_t g = blockIdx.x * BLOCK + threadIdx.x;
     if (g >= n_int) return;
     if (g == n_int - 1 && pair_count) *pair_count = pidx[g] + kept[g];
     if (!kept[g]) return;
-    const LbvhSeg S = segs[seg_of_sorted(keys, range[2 * g])];
+    const LbvhSeg S = segs[seg_of[range[2 * g]]];
     const uint32_t c0 = child[2 * g], c1 = child[2 * g + 1];
     const float *b0 = child_box(c0, vals, item_box, nbox), *b1 = child_box(c1, vals, item_box, nbox);
     NodePair P;
@@ -582,11 +612,11 @@ __device__ __forceinline__ uint32_t material_slot(uint32_t type, uint32_t index,
     return type == RT_MAT_ROUGH ? index : ((rough_count + index) | MAT_METAL_BIT);
 }
 
-__global__ void gather_blas_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals, uint32_t n,
+__global__ void gather_blas_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *vals, uint32_t n,
                                    RawPrimsGPU raw, PrimOutGPU out, const uint32_t *item_member) {
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
     if (p >= n) return;
-    const LbvhSeg S = segs[seg_of_sorted(keys, p)];
+    const LbvhSeg S = segs[seg_of[p]];
     const uint32_t slot = S.slot_base + (p - S.item_base);
     const uint32_t prim = S.prim_base + (vals[p] - S.item_base);
     if (S.ptype == RT_PRIM_TRIANGLE) {
@@ -639,11 +669,11 @@ __global__ void gather_blas_kernel(const LbvhSeg *segs, const unsigned long long
     }
 }
 
-__global__ void gather_items_kernel(const LbvhSeg *segs, const unsigned long long *keys, const uint32_t *vals, uint32_t n,
+__global__ void gather_items_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *vals, uint32_t n,
                                     uint32_t *slots) {
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
     if (p >= n) return;
-    const LbvhSeg S = segs[seg_of_sorted(keys, p)];
+    const LbvhSeg S = segs[seg_of[p]];
     slots[S.slot_base + (p - S.item_base)] = vals[p];
 }
 
@@ -1040,7 +1070,8 @@ void LbvhBuilder::release() {
     if (tmp_) (void)hipFree(tmp_);
     tmp_ = nullptr; tmp_bytes_ = 0;
     box_ = nullptr; cent_ = nullptr;
-    n_items_ = n_segs_ = seg_bits_ = 0;
+    n_items_ = n_segs_ = 0;
+    big_segs_.clear();
 }
 
 hipError_t LbvhBuilder::init(const std::vector<LbvhSeg> &segs, hipStream_t stream) {
@@ -1055,8 +1086,10 @@ hipError_t LbvhBuilder::init(const std::vector<LbvhSeg> &segs, hipStream_t strea
     n_segs_ = (uint32_t)segs.size();
     max_count_ = 0;
     for (const LbvhSeg &sg : segs) max_count_ = sg.count > max_count_ ? sg.count : max_count_;
-    seg_bits_ = 0;
-    while ((1ull << seg_bits_) < n_segs_) seg_bits_++;
+    big_segs_.clear();
+    uint32_t big_max = 0;
+    for (const LbvhSeg &sg : segs)
+        if (sg.count > LOCAL_SORT_MAX) { big_segs_.push_back({sg.item_base, sg.count}); big_max = std::max(big_max, sg.count); }
     const size_t N = n_items_, NI = max_pairs();
     LB_TRY(dalloc(segs_, n_segs_));
     LB_TRY(hipMemcpyAsync(segs_, segs.data(), n_segs_ * sizeof(LbvhSeg), hipMemcpyHostToDevice, stream));
@@ -1071,7 +1104,7 @@ hipError_t LbvhBuilder::init(const std::vector<LbvhSeg> &segs, hipStream_t strea
     LB_TRY(dalloc(range_, 2 * NI)); LB_TRY(dalloc(flag_, NI)); LB_TRY(dalloc(height_, NI));
     LB_TRY(dalloc(nbox_, 6 * NI)); LB_TRY(dalloc(kept_, NI)); LB_TRY(dalloc(pidx_, NI));
     size_t sort_bytes = 0, scan_bytes = 0;
-    LB_TRY(rocprim::radix_sort_pairs(nullptr, sort_bytes, k0_, k1_, v0_, v1_, N, 0, 32 + seg_bits_, stream));
+    if (big_max) LB_TRY(rocprim::radix_sort_pairs(nullptr, sort_bytes, k0_, k1_, v0_, v1_, big_max, 0, 32, stream));
     LB_TRY(rocprim::exclusive_scan(nullptr, scan_bytes, kept_, pidx_, 0u, NI, rocprim::plus<uint32_t>(), stream));
     tmp_bytes_ = sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
     LB_TRY(hipMalloc(&tmp_, tmp_bytes_ ? tmp_bytes_ : 1));
@@ -1145,17 +1178,25 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
                        size_classes_ ? box_ : nullptr, k0_, v0_);
     LB_TRY(hipGetLastError());
     size_t bytes = tmp_bytes_;
-    LB_TRY(rocprim::radix_sort_pairs(tmp_, bytes, k0_, k1_, v0_, v1_, N, 0, 32 + seg_bits_, stream));
-    hipLaunchKernelGGL(karras_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, k1_, N, child_, parent_,
+    if (big_segs_.size() < n_segs_)
+        hipLaunchKernelGGL(local_sort_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, k0_, k1_, v1_);
+    // BLAS codes are 30-bit Morton codes; TLAS items may carry size classes and inactive items (0xFFFFFFFF)
+    const int end_bit = (box_ == own_box_ && !size_classes_) ? 30 : 32;
+    for (const auto &b : big_segs_) {
+        bytes = tmp_bytes_;
+        LB_TRY(rocprim::radix_sort_pairs(tmp_, bytes, k0_ + b.first, k1_ + b.first, v0_ + b.first, v1_ + b.first, b.second, 0,
+                                         end_bit, stream));
+    }
+    hipLaunchKernelGGL(karras_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, seg_of_, k1_, N, child_, parent_,
                        parent_leaf_, range_, flag_);
     hipLaunchKernelGGL(bottom_up_local_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, v1_, box_, child_, parent_,
                        parent_leaf_, range_, nbox_, height_, kept_);
     if (max_count_ > LOCAL_MAX) {
         if (!frontier_) LB_TRY(dalloc(frontier_, 1 + 2 * (size_t)NI));   // <= 2 arrivals per internal node
         LB_TRY(hipMemsetAsync(frontier_, 0, sizeof(uint32_t), stream));
-        hipLaunchKernelGGL(bottom_up_chunk_kernel, dim3((N + CHUNK - 1) / CHUNK), dim3(CHUNK), 0, stream, segs_, k1_, v1_,
+        hipLaunchKernelGGL(bottom_up_chunk_kernel, dim3((N + CHUNK - 1) / CHUNK), dim3(CHUNK), 0, stream, segs_, seg_of_, v1_,
                            box_, N, child_, parent_, parent_leaf_, range_, nbox_, height_, kept_, frontier_);
-        hipLaunchKernelGGL(bottom_up_top_kernel, dim3(256), dim3(BLOCK), 0, stream, segs_, k1_, v1_, box_, child_, parent_,
+        hipLaunchKernelGGL(bottom_up_top_kernel, dim3(256), dim3(BLOCK), 0, stream, segs_, seg_of_, v1_, box_, child_, parent_,
                            range_, flag_, nbox_, height_, kept_, frontier_);
     }
     LB_TRY(hipGetLastError());
@@ -1167,7 +1208,7 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
     if (NI > 0) {
         bytes = tmp_bytes_;
         LB_TRY(rocprim::exclusive_scan(tmp_, bytes, kept_, pidx_, 0u, NI, rocprim::plus<uint32_t>(), stream));
-        hipLaunchKernelGGL(emit_kernel, dim3(blocks_for(NI)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, box_, NI, child_,
+        hipLaunchKernelGGL(emit_kernel, dim3(blocks_for(NI)), dim3(BLOCK), 0, stream, segs_, seg_of_, v1_, box_, NI, child_,
                            range_, nbox_, kept_, pidx_, pairs, pair_count);
     } else if (pair_count) {
         LB_TRY(hipMemsetAsync(pair_count, 0, sizeof(uint32_t), stream));
@@ -1178,7 +1219,7 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
 }
 
 hipError_t LbvhBuilder::gather_blas(const RawPrimsGPU &raw, const PrimOutGPU &out, hipStream_t stream) {
-    hipLaunchKernelGGL(gather_blas_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, n_items_,
+    hipLaunchKernelGGL(gather_blas_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, seg_of_, v1_, n_items_,
                        raw, out, item_member_);
     return hipGetLastError();
 }
@@ -1198,7 +1239,7 @@ hipError_t LbvhBuilder::collapse_wide(const NodePair *pairs, const TreeRoot *roo
 }
 
 hipError_t LbvhBuilder::gather_items(uint32_t *slots, hipStream_t stream) {
-    hipLaunchKernelGGL(gather_items_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, k1_, v1_, n_items_,
+    hipLaunchKernelGGL(gather_items_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, seg_of_, v1_, n_items_,
                        slots);
     return hipGetLastError();
 }

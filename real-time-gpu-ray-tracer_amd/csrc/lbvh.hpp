@@ -8,8 +8,8 @@
 // One builder instance owns the device workspace of one forest: a set of independent trees
 // ("segments") over disjoint, contiguous item ranges.  A build is a fixed sequence of kernels on
 // one stream, no host synchronisation:
-//   centroid bounds per segment -> 30-bit Morton key per item, segment id in the high word ->
-//   radix sort (rocPRIM) -> Karras radix-tree hierarchy per segment -> bottom-up box union
+//   centroid bounds per segment -> 30-bit Morton key per item -> sort within each segment (LDS bitonic for
+//   small trees, rocPRIM radix sort for large ones) -> Karras radix-tree hierarchy per segment -> bottom-up box union
 //   (arrival counters; one workgroup per tree of <= 2048 items, LDS hand-offs) -> subtrees of <= leaf_cap items collapse into leaves, the surviving
 //   interior nodes are compacted (exclusive scan) into the node-pair layout of layout.hpp ->
 //   per-segment root {box, ref}.
@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <utility>
 #include <vector>
 
 #include "layout.hpp"
@@ -109,7 +110,8 @@ public:
     hipError_t gather_items(uint32_t *slots, hipStream_t stream);
 
 private:
-    uint32_t n_items_ = 0, n_segs_ = 0, seg_bits_ = 0, max_count_ = 0;
+    uint32_t n_items_ = 0, n_segs_ = 0, max_count_ = 0;
+    std::vector<std::pair<uint32_t, uint32_t>> big_segs_;   // {item_base, count} of trees sorted by rocPRIM
     LbvhSeg *segs_ = nullptr;
     uint32_t *seg_of_ = nullptr;          // item -> segment
     uint32_t *members_ = nullptr;         // group segments: {first primitive, instance} pairs
@@ -122,7 +124,7 @@ private:
     float *own_box_ = nullptr;
     float4 *own_cent_ = nullptr;
     uint32_t *bounds_ = nullptr;          // 6 ordered-uint per segment (centroid bounds)
-    unsigned long long *k0_ = nullptr, *k1_ = nullptr;
+    uint32_t *k0_ = nullptr, *k1_ = nullptr;           // Morton codes (per item, then sorted within each segment)
     uint32_t *v0_ = nullptr, *v1_ = nullptr;
     uint32_t *child_ = nullptr;           // 2 per interior node: LEAF_BIT | sorted position, or node
     uint32_t *parent_ = nullptr;          // per interior node

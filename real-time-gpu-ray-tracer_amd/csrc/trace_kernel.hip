@@ -79,6 +79,11 @@ static_assert(LDS_DEPTH % 4 == 0, "half-pages move as 16 B pieces");
 #define RT_SLAB_TINY 0                  // the same for single-box tests (TLAS root, instance root boxes): 0 = the
                                         // reciprocal slab for every ray (C2 -1.6 %, C3 -1.1 %)
 #endif
+#ifndef RT_SLAB_PAD
+#define RT_SLAB_PAD 0                   // diagnostic: widen every FAST slab interval by a bound on the difference between
+                                        // the reciprocal-FMA plane distances and the reference's (mn - q) / d, so a FAST
+                                        // cull never rejects a box the reference's slab accepts (a superset of visits)
+#endif
 #ifndef TRI_AHEAD
 #define TRI_AHEAD 4                     // triangle records of a leaf requested before the first test (all 4 of a
                                         // full leaf: C2 serialised -2..-7 %, C3 -0.6 %; profiles/r02_ab_tri_ahead.jsonl)
@@ -174,6 +179,9 @@ struct RayP {
     f3 o, d;
 #if !RT_EXACT
     f3 inv, oinv;      // 1/d and o/d for one-FMA slab planes
+#if RT_SLAB_PAD
+    f3 pad;            // per axis: 2^-21 |o/d|, the absolute part of the plane-distance bound (RT_SLAB_PAD)
+#endif
     bool tiny;         // some |d_axis| < 1e-6: use the reference's parallel-axis branch
 #endif
 };
@@ -184,6 +192,9 @@ __device__ __forceinline__ void prep(RayP &r) {
     const auto nz = [](float x) { return fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x; };
     r.inv = mk(rcp(nz(r.d.x)), rcp(nz(r.d.y)), rcp(nz(r.d.z)));
     r.oinv = mk(r.o.x * r.inv.x, r.o.y * r.inv.y, r.o.z * r.inv.z);
+#if RT_SLAB_PAD
+    r.pad = mk(0x1p-21f * fabsf(r.oinv.x), 0x1p-21f * fabsf(r.oinv.y), 0x1p-21f * fabsf(r.oinv.z));
+#endif
 #else
     (void)r;
 #endif
@@ -214,6 +225,11 @@ __device__ __forceinline__ bool slab_ref(const float *b, const f3 &o, const f3 &
     return true;
 }
 
+#if RT_SLAB_PAD
+// the plane-distance interval [min, max] of one axis, widened by the bound (relative 2^-20 + absolute pad)
+__device__ __forceinline__ float pad_lo(float x, float p) { return x - fmaf(fabsf(x), 0x1p-20f, p); }
+__device__ __forceinline__ float pad_hi(float x, float p) { return x + fmaf(fabsf(x), 0x1p-20f, p); }
+#endif
 __device__ __forceinline__ bool slab(const float *b, const RayP &r, float tmin, float tmax, float &te) {
 #if RT_EXACT
     return slab_ref(b, r.o, r.d, tmin, tmax, te);
@@ -222,8 +238,13 @@ __device__ __forceinline__ bool slab(const float *b, const RayP &r, float tmin, 
     const float tx1 = fmaf(b[0], r.inv.x, -r.oinv.x), tx2 = fmaf(b[1], r.inv.x, -r.oinv.x);
     const float ty1 = fmaf(b[2], r.inv.y, -r.oinv.y), ty2 = fmaf(b[3], r.inv.y, -r.oinv.y);
     const float tz1 = fmaf(b[4], r.inv.z, -r.oinv.z), tz2 = fmaf(b[5], r.inv.z, -r.oinv.z);
+#if RT_SLAB_PAD
+    const float lo = fmaxf(fmaxf(tmin, pad_lo(fminf(tx1, tx2), r.pad.x)), fmaxf(pad_lo(fminf(ty1, ty2), r.pad.y), pad_lo(fminf(tz1, tz2), r.pad.z)));
+    const float hi = fminf(fminf(tmax, pad_hi(fmaxf(tx1, tx2), r.pad.x)), fminf(pad_hi(fmaxf(ty1, ty2), r.pad.y), pad_hi(fmaxf(tz1, tz2), r.pad.z)));
+#else
     const float lo = fmaxf(fmaxf(tmin, fminf(tx1, tx2)), fmaxf(fminf(ty1, ty2), fminf(tz1, tz2)));
     const float hi = fminf(fminf(tmax, fmaxf(tx1, tx2)), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
+#endif
     te = lo;
     return lo < hi;
 #endif
@@ -626,11 +647,23 @@ __device__ __forceinline__ R lds_or_global(uint32_t at, const R *g, uint32_t k) 
     return r;
 }
 
-__device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float oinv, float4 &tn, float4 &tf) {
-    const float a0 = fmaf(lo.x, inv, -oinv), b0 = fmaf(hi.x, inv, -oinv);
-    const float a1 = fmaf(lo.y, inv, -oinv), b1 = fmaf(hi.y, inv, -oinv);
-    const float a2 = fmaf(lo.z, inv, -oinv), b2 = fmaf(hi.z, inv, -oinv);
-    const float a3 = fmaf(lo.w, inv, -oinv), b3 = fmaf(hi.w, inv, -oinv);
+__device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float oinv, float4 &tn, float4 &tf,
+                                      float pad = 0.0f) {
+    float a0 = fmaf(lo.x, inv, -oinv), b0 = fmaf(hi.x, inv, -oinv);
+    float a1 = fmaf(lo.y, inv, -oinv), b1 = fmaf(hi.y, inv, -oinv);
+    float a2 = fmaf(lo.z, inv, -oinv), b2 = fmaf(hi.z, inv, -oinv);
+    float a3 = fmaf(lo.w, inv, -oinv), b3 = fmaf(hi.w, inv, -oinv);
+#if RT_SLAB_PAD
+    {
+        float n0 = pad_lo(fminf(a0, b0), pad), f0 = pad_hi(fmaxf(a0, b0), pad);
+        float n1 = pad_lo(fminf(a1, b1), pad), f1 = pad_hi(fmaxf(a1, b1), pad);
+        float n2 = pad_lo(fminf(a2, b2), pad), f2 = pad_hi(fmaxf(a2, b2), pad);
+        float n3 = pad_lo(fminf(a3, b3), pad), f3v = pad_hi(fmaxf(a3, b3), pad);
+        a0 = n0; b0 = f0; a1 = n1; b1 = f1; a2 = n2; b2 = f2; a3 = n3; b3 = f3v;
+    }
+#else
+    (void)pad;
+#endif
     tn = make_float4(fmaxf(tn.x, fminf(a0, b0)), fmaxf(tn.y, fminf(a1, b1)), fmaxf(tn.z, fminf(a2, b2)), fmaxf(tn.w, fminf(a3, b3)));
     tf = make_float4(fminf(tf.x, fmaxf(a0, b0)), fminf(tf.y, fmaxf(a1, b1)), fminf(tf.z, fmaxf(a2, b2)), fminf(tf.w, fmaxf(a3, b3)));
 }
@@ -666,9 +699,15 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
     bool h[4];
     if (!RT_WIDE_TINY || !r.tiny) {
         float4 tn = make_float4(TMIN, TMIN, TMIN, TMIN), tf = make_float4(T.tmax, T.tmax, T.tmax, T.tmax);
+#if RT_SLAB_PAD
+        slab4(lx, hx, r.inv.x, r.oinv.x, tn, tf, r.pad.x);
+        slab4(ly, hy, r.inv.y, r.oinv.y, tn, tf, r.pad.y);
+        slab4(lz, hz, r.inv.z, r.oinv.z, tn, tf, r.pad.z);
+#else
         slab4(lx, hx, r.inv.x, r.oinv.x, tn, tf);
         slab4(ly, hy, r.inv.y, r.oinv.y, tn, tf);
         slab4(lz, hz, r.inv.z, r.oinv.z, tn, tf);
+#endif
         t[0] = tn.x; t[1] = tn.y; t[2] = tn.z; t[3] = tn.w;
         h[0] = tn.x < tf.x; h[1] = tn.y < tf.y; h[2] = tn.z < tf.z; h[3] = tn.w < tf.w;
     } else {                                          // some |d_axis| < 1e-6: the reference's slab per child

@@ -7,7 +7,8 @@ For C2 (1080p, 1 spp, depth 2; also at depth 1) and C3 (1080p, 4 spp, depth 4), 
   * "fast_compat": FAST kernel on the reference's own (median-split) trees — identical trees to the oracle's;
   * "fast_compat_binary": FAST arithmetic on those trees with the binary node-pair traversal (the reference's
               visit order), which separates arithmetic from visit-order ties;
-  * "exact_compat": EXACT kernel on those trees (bit-identical by the parity tests)
+  * "exact_compat": EXACT kernel on those trees (bit-identical by the parity tests);
+  * "<mode>+opt=v+...": any of the above with extra set_option calls (e.g. "fast_compat+lds_scene=0+kernel=0")
 and compares each with the oracle's frame: pixels with any RGBA8 channel |d| > 1 (outliers), max |d|, and the
 per-channel float |d| of the linear RGB.  Output: one JSON object (stdout, or --out).
 RTAMD_LIB selects the library (variant builds, e.g. RT_WIDE_TINY=1 RT_SLAB_TINY=1).
@@ -33,6 +34,7 @@ def compare(rgba, rgb, orgba, orgb):
     if rgb is not None:
         fd = np.abs(rgb - orgb)
         out["float_max"] = float(fd.max())
+        out["float_ne"] = int((rgb != orgb).any(axis=-1).sum())
         out["float_gt_1e-3"] = int((fd.max(axis=-1) > 1e-3).sum())
     return out
 
@@ -70,13 +72,17 @@ def main():
             orgb, orgba, _ = o.render(threads=16)
             oracle[f] = (orgb, orgba)
             print(f"oracle {cname} frame {f}: {time.time() - t0:.1f} s", flush=True)
-        for mode in args.modes.split(","):
+        for spec in args.modes.split(","):
+            mode, *extra = spec.split("+")
             build = {"bench": "sah", "lbvh": "lbvh", "lbvh_nogroup": "lbvh", "sah_nogroup": "sah"}.get(mode, "compat")
             r = Renderer(scene)
             if mode == "fast_compat_binary":                 # FAST arithmetic on the reference's binary visit order
                 r.set_option("wide", 0)
             if mode.endswith("_nogroup"):                    # one TLAS item per particle, as the reference has them
                 r.set_option("group", 0)
+            for kv in extra:
+                k, v = kv.split("=")
+                r.set_option(k, int(v))
             r.build_acceleration_structure(0, mode=build).configure_camera(W, H, **cam)
             got = {}
             if mode == "bench":
@@ -104,13 +110,13 @@ def main():
             r.cleanup()
             for f in frames:
                 c = compare(got[f][0], got[f][1], oracle[f][1], oracle[f][0])
-                c.update({"config": cname, "mode": mode, "frame": f, "depth": cam["ray_trace_depth"], "spp": cfg.spp})
+                c.update({"config": cname, "mode": spec, "frame": f, "depth": cam["ray_trace_depth"], "spp": cfg.spp})
                 res["cases"].append(c)
                 print(json.dumps(c), flush=True)
                 if args.save_diff:
                     os.makedirs(args.save_diff, exist_ok=True)
                     d = np.abs(got[f][0].astype(np.int32) - oracle[f][1].astype(np.int32)).max(axis=-1)
-                    np.savez_compressed(os.path.join(args.save_diff, f"{cname}_{mode}_{f}.npz"),
+                    np.savez_compressed(os.path.join(args.save_diff, f"{cname}_{spec}_{f}.npz"),
                                         yx=np.argwhere(d > 1).astype(np.int32), d=d[d > 1].astype(np.int32))
     s = json.dumps(res, indent=1)
     if args.out:
