@@ -286,20 +286,35 @@ __global__ __launch_bounds__(BLOCK) void local_sort_kernel(const LbvhSeg *segs, 
     }
 }
 
-// Karras 2012, one thread per interior node.  Local indices are positions inside the segment.
-__global__ void karras_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *keys, uint32_t n, uint32_t *child,
-                              uint32_t *parent, uint32_t *parent_leaf, uint32_t *range, uint32_t *flag) {
+// Karras 2012, one thread per interior node.  Local indices are positions inside the segment.  The sorted codes
+// within KWIN positions of the workgroup's own are staged in LDS first: nearly every node's searches stay inside
+// that window (a range of <= KWIN / 2 items), so a search step is an LDS read, not a dependent global load.
+constexpr int KWIN = 256;
+__global__ __launch_bounds__(BLOCK) void karras_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *keys,
+                                                       uint32_t n, uint32_t *child, uint32_t *parent, uint32_t *parent_leaf,
+                                                       uint32_t *range, uint32_t *flag) {
+    __shared__ uint32_t skey[BLOCK + 2 * KWIN];
+    const int64_t w0 = (int64_t)blockIdx.x * BLOCK - KWIN;       // position of skey[0]
+    for (int k = threadIdx.x; k < BLOCK + 2 * KWIN; k += BLOCK) {
+        const int64_t q = w0 + k;
+        skey[k] = (q >= 0 && q < (int64_t)n) ? keys[q] : 0u;
+    }
+    __syncthreads();
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
     if (p >= n) return;
     const LbvhSeg S = segs[seg_of[p]];
     const int m = (int)S.count;
     const int i = (int)(p - S.item_base);
-    const uint32_t *K = keys + S.item_base;
     if (m == 1) { parent_leaf[p] = NONE; return; }
     if (i >= m - 1) return;
-    auto delta = [&](int a, int b) -> int {
+    const auto key = [&](int a) -> uint32_t {                    // code at segment position a (0 <= a < m)
+        const int64_t pos = (int64_t)S.item_base + a, o = pos - w0;
+        return (o >= 0 && o < BLOCK + 2 * KWIN) ? skey[o] : keys[pos];
+    };
+    const uint32_t ki = key(i);
+    auto delta = [&](int a, int b) -> int {                      // a == i throughout
         if (b < 0 || b >= m) return -1;
-        const uint32_t ka = K[a], kb = K[b];
+        const uint32_t ka = ki, kb = key(b);
         if (ka != kb) return __clz(ka ^ kb);
         return 32 + __clz((uint32_t)a ^ (uint32_t)b);
     };
@@ -456,6 +471,9 @@ __device__ __forceinline__ void climb_top(const LbvhSeg &S, uint32_t g, const ui
     }
 }
 
+// The chunk's own nodes (the interior node at each of its positions: child refs, item range, parent) are staged
+// in LDS with one coalesced load per thread before the climbs, so a climb step waits on LDS only (reading them
+// from HBM / L2 per step made every level a dependent global round trip: 0.64 ms per C5 rebuild).
 __global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *segs, const uint32_t *seg_of,
                                                                 const uint32_t *vals, const float *item_box, uint32_t n,
                                                                 const uint32_t *child, const uint32_t *parent,
@@ -466,30 +484,47 @@ __global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *s
     __shared__ float sbox[CHUNK * 6];           // node boxes, at the node's own position
     __shared__ uint32_t sheight[CHUNK];
     __shared__ uint32_t sflag[CHUNK];
-    __shared__ uint32_t snode[CHUNK];
+    __shared__ uint2 schild[CHUNK], srange[CHUNK];   // the interior node at each position (segment's last: unused)
+    __shared__ uint32_t sparent[CHUNK];
+    constexpr uint32_t FRONT_LDS = 256;         // this chunk's arrivals for the top pass (~20 typical; more go direct)
+    __shared__ uint32_t sfront[FRONT_LDS];
+    __shared__ uint32_t sfront_n, sfront_at;
     const uint32_t lo = blockIdx.x * CHUNK, p = lo + threadIdx.x;
     sflag[threadIdx.x] = 0;
-    const bool big = p < n && segs[seg_of[p]].count > LOCAL_MAX;   // else bottom_up_local_kernel
+    if (threadIdx.x == 0) sfront_n = 0;
+    const uint32_t seg = p < n ? seg_of[p] : NONE;
+    const bool big = seg != NONE && segs[seg].count > LOCAL_MAX;   // else bottom_up_local_kernel
+    LbvhSeg S;
     if (big) {
+        S = segs[seg];
         const float2 *src = reinterpret_cast<const float2 *>(item_box + 6 * (size_t)vals[p]);
 #pragma unroll
         for (int k = 0; k < 3; k++) { const float2 v = src[k]; sleaf[6 * threadIdx.x + 2 * k] = v.x; sleaf[6 * threadIdx.x + 2 * k + 1] = v.y; }
+        if (p - S.item_base + 1u < S.count) {
+            const uint32_t g = S.node_base + (p - S.item_base);
+            schild[threadIdx.x] = reinterpret_cast<const uint2 *>(child)[g];
+            srange[threadIdx.x] = reinterpret_cast<const uint2 *>(range)[g];
+            sparent[threadIdx.x] = parent[g];
+        }
     }
     __syncthreads();
     if (big) {
-        const LbvhSeg S = segs[seg_of[p]];
         uint32_t g = parent_leaf[p];
         bool first = false;                             // stopped as a node's first arrival
-        while (g != NONE && chunk_local(range, g)) {
-            const uint32_t l = S.item_base + (g - S.node_base) - lo;   // the node's own position in the chunk
+        while (g != NONE) {
+            const uint32_t l = S.item_base + (g - S.node_base) - lo;   // the node's own position, if in this chunk
+            if (l >= CHUNK) break;                                     // its range leaves the chunk
+            const uint2 rg = srange[l];
+            if (rg.x / CHUNK != rg.y / CHUNK) break;                   // the same
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (atomicAdd(&sflag[l], 1u) == 0u) { first = true; break; }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             float b[6];
             uint32_t h = 0;
+            const uint2 cc = schild[l];
 #pragma unroll
             for (int c = 0; c < 2; c++) {                              // union_children's order
-                const uint32_t ch = child[2 * g + c];
+                const uint32_t ch = c == 0 ? cc.x : cc.y;
                 const float *cb;
                 uint32_t chh = 0;
                 if (ch & LEAF_BIT) {                                   // sorted position = the leaf's item index
@@ -510,25 +545,32 @@ __global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *s
                 }
                 h = chh > h ? chh : h;
             }
-            const uint32_t size = range[2 * g + 1] - range[2 * g] + 1u;
+            const uint32_t size = rg.y - rg.x + 1u;
 #pragma unroll
             for (int k = 0; k < 6; k++) sbox[6 * l + k] = b[k];
             sheight[l] = size > S.leaf_cap ? h + 1u : 0u;
-            snode[l] = g;
-            g = parent[g];
+            g = sparent[l];
         }
         if (!first && g != NONE) {                      // g's range crosses a chunk edge: an arrival for the top pass
-            const uint32_t k = atomicAdd(frontier, 1u);
-            frontier[1 + k] = g;
+            const uint32_t k = atomicAdd(&sfront_n, 1u);
+            if (k < FRONT_LDS) sfront[k] = g;
+            else frontier[1 + atomicAdd(frontier, 1u)] = g;
         }
     }
     __syncthreads();
-    if (sflag[threadIdx.x] == 2u) {                                    // a node finished here
-        const uint32_t l = threadIdx.x, g = snode[l];
+    // one global reservation per chunk (~20 arrivals each): a per-arrival atomic on the one frontier counter
+    // serialised ~200 k same-address atomics per C5 rebuild at the L2 (0.64 ms for the whole kernel)
+    const uint32_t nf = sfront_n < FRONT_LDS ? sfront_n : FRONT_LDS;
+    if (threadIdx.x == 0 && nf) sfront_at = atomicAdd(frontier, nf);
+    __syncthreads();
+    if (threadIdx.x < nf) frontier[1 + sfront_at + threadIdx.x] = sfront[threadIdx.x];
+    if (sflag[threadIdx.x] == 2u) {                                    // the node at this position finished here
+        const uint32_t l = threadIdx.x, g = S.node_base + (p - S.item_base);
+        const uint2 rg = srange[l];
 #pragma unroll
         for (int k = 0; k < 6; k++) nbox[6 * (size_t)g + k] = sbox[6 * l + k];
         height[g] = sheight[l];
-        kept[g] = (range[2 * g + 1] - range[2 * g] + 1u) > segs[seg_of[p]].leaf_cap ? 1u : 0u;
+        kept[g] = (rg.y - rg.x + 1u) > S.leaf_cap ? 1u : 0u;
     }
 }
 

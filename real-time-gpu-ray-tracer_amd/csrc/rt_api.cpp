@@ -189,6 +189,7 @@ struct rt_scene {
     // 0.252 -> 0.229 ms/frame; a C2 1/8 share 0.115 -> 0.084; C3 1.64 -> 1.59,
     // profiles/r02_sweep_grid2.jsonl), else 100 (a frame alone on the GPU takes all of it)
     uint32_t grid_pct = 0;
+    static constexpr uint64_t BIG_LAUNCH_PATHS = 16ull << 20;
     uint32_t wide_merge = 0;        // quad trees: binary subtrees of <= wide_merge items become one leaf (set before build)
     DevBuf<TriHot> tri_hot;
     DevBuf<TriCold> tri_cold;
@@ -353,6 +354,9 @@ struct rt_scene {
     // RT_BUILD_LBVH rebuilds (option "blas_double", default on): a rebuild writes a spare BLAS set and swaps it
     // in, so frame k+1's rebuild runs while frame k's trace still reads the other set (C5: the rebuild no
     // longer waits for every lane's trace).  ev_blas_lane[q]: lane q's last trace of the current set.
+    // Option "blas_sets" = 3 (default; 2 = one spare): two spare sets in rotation, so frame k+1's rebuild waits only
+    // for frame k-2's trace and three traces stay in flight beside it (spare[0] = the set read longest ago, the next
+    // one written; C5 with the rebuild 11.18 -> 10.85 ms/frame, profiles/r04/c5_grid/).
     struct BlasSet {
         DevBuf<NodePair> pairs; DevBuf<NodeQuad> quads; DevBuf<TreeRoot> roots;
         DevBuf<TriHot> tri_hot; DevBuf<TriCold> tri_cold; DevBuf<SphereHot> sph_hot; DevBuf<PrimCold> sph_cold;
@@ -362,7 +366,8 @@ struct rt_scene {
             pairs.release(); quads.release(); roots.release(); tri_hot.release(); tri_cold.release();
             sph_hot.release(); sph_cold.release(); quad_hot.release(); quad_cold.release();
         }
-    } spare;
+    } spare[2];
+    uint32_t blas_sets = 3;
     hipEvent_t ev_blas_lane[NLANE] = {};
     bool blas_double = true;
     uint64_t blas_builds = 0;
@@ -426,10 +431,11 @@ struct rt_scene {
         raw_tris.release(); raw_sph.release(); raw_quad.release(); blas_roots.release(); inst_blas.release();
         blas_wide_refs.release();
         gpu_counts.release(); inst_params.release();
-        spare.release();
+        for (BlasSet &sp : spare) sp.release();
         for (int q = 0; q < NLANE; q++) {
             if (ev_blas_lane[q]) (void)hipEventDestroy(ev_blas_lane[q]);
-            if (spare.ev_lane[q]) (void)hipEventDestroy(spare.ev_lane[q]);
+            for (BlasSet &sp : spare)
+                if (sp.ev_lane[q]) (void)hipEventDestroy(sp.ev_lane[q]);
         }
         if (ev_render_done) (void)hipEventDestroy(ev_render_done);
         if (ev_blas_built) (void)hipEventDestroy(ev_blas_built);
@@ -944,7 +950,7 @@ rt_status lbvh_sync_groups(rt_scene *s) {
         s->inst_dirty[s->inst.size() + g] = rt_scene::ALL_BLOCKS;
     }
     s->lbvh_intact = now;
-    s->spare.release();                                   // re-sized with the next double-buffered build
+    for (rt_scene::BlasSet &sp : s->spare) sp.release();   // re-sized with the next double-buffered build
     return lbvh_segments(s);
 }
 
@@ -953,7 +959,7 @@ rt_status lbvh_sync_groups(rt_scene *s) {
 rt_status gpu_build_blas(rt_scene *s) {
     if (s->blas_double && s->blas_builds > 0) {
         // into the spare set: wait only for the traces that read it (each lane's last one), then swap it in
-        rt_scene::BlasSet &sp = s->spare;
+        rt_scene::BlasSet &sp = s->spare[0];
         rt_status st;
         if (sp.pairs.n != s->blas_pairs.n || sp.tri_hot.n != s->tri_hot.n || sp.sph_hot.n != s->sph_hot.n ||
             sp.quad_hot.n != s->quad_hot.n || sp.roots.n != s->blas_roots.n) {
@@ -982,6 +988,7 @@ rt_status gpu_build_blas(rt_scene *s) {
         std::swap(s->sph_hot, sp.sph_hot); std::swap(s->sph_cold, sp.sph_cold);
         std::swap(s->quad_hot, sp.quad_hot); std::swap(s->quad_cold, sp.quad_cold);
         for (int q = 0; q < rt_scene::NLANE; q++) std::swap(s->ev_blas_lane[q], sp.ev_lane[q]);
+        if (s->blas_sets == 3) std::swap(s->spare[0], s->spare[1]);   // the set frame k-1 read is written next
         s->blas_dirty = false;
         s->blas_builds++;
         return RT_OK;
@@ -1025,14 +1032,15 @@ rt_status gpu_setup_blas(rt_scene *s, const uint32_t *slot_count) {
     delete s->blas_builder;
     s->blas_builder = nullptr;
     s->lbvh_intact.assign(s->groups.size(), 1);       // members start with the group's transform (frame 0 re-checks)
-    s->spare.release();
+    for (rt_scene::BlasSet &sp : s->spare) sp.release();
     if ((st = lbvh_segments(s)) != RT_OK) return st;
     if ((st = alloc_buf(s->gpu_counts, 2 + rt_scene::NLANE)) != RT_OK) return st;
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
     if (!s->r_done) s->r_done = s->ev_render_done;
     for (int q = 0; q < rt_scene::NLANE; q++) {       // "blas_double": every trace records its lane's event from now on
         if (!s->ev_blas_lane[q]) HIP_TRY(hipEventCreateWithFlags(&s->ev_blas_lane[q], hipEventDisableTiming));
-        if (!s->spare.ev_lane[q]) HIP_TRY(hipEventCreateWithFlags(&s->spare.ev_lane[q], hipEventDisableTiming));
+        for (rt_scene::BlasSet &sp : s->spare)
+            if (!sp.ev_lane[q]) HIP_TRY(hipEventCreateWithFlags(&sp.ev_lane[q], hipEventDisableTiming));
     }
     s->blas_builds = 0;
     if ((st = gpu_build_blas(s)) != RT_OK) return st;
@@ -1821,6 +1829,10 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             // lane runs off the null stream: C2 0.173 -> 0.164 ms/frame, C2 1/8 share 0.041 -> 0.038, 1/4 0.059 ->
             // 0.052; profiles/r03_session2/share_grid_*.txt, lanes_new*.txt); alone: all of it
             pct = !partner ? 100u : (s->lanes <= 3 ? 50u : 100u / s->lanes + 12u);
+            // a launch of >= BIG_LAUNCH_PATHS camera paths (C5: 4K x 4 traced spp = 33 M) keeps all of it: its own
+            // tail is a small part of its span, and a half grid only stretches the span (C5 5.88 -> 5.43 ms/frame
+            // with trees built once, 13.3 -> 11.2 with the per-frame rebuild; profiles/r04/c5_grid/)
+            if ((uint64_t)out.units * 64u * cam.sqrt_s * cam.sqrt_s >= rt_scene::BIG_LAUNCH_PATHS) pct = 100u;
         }
         if (pct < 100) blocks = std::max<uint32_t>(8u, blocks * pct / 100u);
         const uint32_t thr = s->threshold ? s->threshold : (cam.depth * cam.sqrt_s * cam.sqrt_s <= 2u ? 64u : 40u);
@@ -1987,6 +1999,10 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "costmap") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
         s->costmap_on = value == 1;
+    } else if (k == "blas_sets") {
+        if (value != 2 && value != 3) return fail(RT_ERR_INVALID_ARGUMENT, "blas_sets must be 2 or 3");
+        RT_TRY(drain(s));
+        s->blas_sets = (uint32_t)value;
     } else if (k == "blas_double") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "blas_double must be 0 or 1");
         s->blas_double = value == 1;

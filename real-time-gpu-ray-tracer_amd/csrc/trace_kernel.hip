@@ -70,19 +70,16 @@ static_assert(LDS_DEPTH % 4 == 0, "half-pages move as 16 B pieces");
 #define RT_CHAIN_ROOT_LEAF 1            // quad trees: an entered instance whose BLAS root is a leaf (a sphere, a
                                         // parallelogram, a small mesh) has it tested in the same leaf round
 #endif
-#ifndef RT_WIDE_TINY
-#define RT_WIDE_TINY 0                  // 1: quad steps take the reference's parallel-axis slab (BoundingBox.cu:44-50)
-                                        // for rays with some |d| < 1e-6; 0: the reciprocal slab on d clamped to
-                                        // +-1e-20 for every ray (a conservative cull of the true ray: C2 -6 %, C3 -3.5 %)
+#ifndef RT_SLAB_CONS
+#define RT_SLAB_CONS 1                  // FAST slabs are conservative: the interval [lo, hi] a box test computes with
+                                        // reciprocal-FMA planes is widened by a bound on its distance from the
+                                        // reference's (mn - q) / d interval before the lo < hi test (and a popped entry's
+                                        // lo before its lo < tmax re-test), so a FAST cull never rejects a box the
+                                        // reference's slab accepts; entries keep the unwidened lo, so children are still
+                                        // ordered by it
 #endif
-#ifndef RT_SLAB_TINY
-#define RT_SLAB_TINY 0                  // the same for single-box tests (TLAS root, instance root boxes): 0 = the
-                                        // reciprocal slab for every ray (C2 -1.6 %, C3 -1.1 %)
-#endif
-#ifndef RT_SLAB_PAD
-#define RT_SLAB_PAD 0                   // diagnostic: widen every FAST slab interval by a bound on the difference between
-                                        // the reciprocal-FMA plane distances and the reference's (mn - q) / d, so a FAST
-                                        // cull never rejects a box the reference's slab accepts (a superset of visits)
+#ifndef RT_NZ_MIN
+#define RT_NZ_MIN FZERO                 // |d_axis| below this is clamped to +-1e-20 for the slab reciprocals (prep)
 #endif
 #ifndef TRI_AHEAD
 #define TRI_AHEAD 4                     // triangle records of a leaf requested before the first test (all 4 of a
@@ -179,21 +176,27 @@ struct RayP {
     f3 o, d;
 #if !RT_EXACT
     f3 inv, oinv;      // 1/d and o/d for one-FMA slab planes
-#if RT_SLAB_PAD
-    f3 pad;            // per axis: 2^-21 |o/d|, the absolute part of the plane-distance bound (RT_SLAB_PAD)
+#if RT_SLAB_CONS
+    float pad;         // the absolute part of the plane-distance bound: 2^-22 max |o/d| over the non-parallel axes
 #endif
-    bool tiny;         // some |d_axis| < 1e-6: use the reference's parallel-axis branch
 #endif
 };
 __device__ __forceinline__ void prep(RayP &r) {
 #if !RT_EXACT
-    r.tiny = fabsf(r.d.x) < FZERO || fabsf(r.d.y) < FZERO || fabsf(r.d.z) < FZERO;
-    // |d| < 1e-20 -> +-1e-20: finite reciprocals, so a branch-free slab never forms 0 * inf
-    const auto nz = [](float x) { return fabsf(x) < 1e-20f ? copysignf(1e-20f, x) : x; };
+    // |d| < 1e-6 (the reference's parallel-axis threshold, BoundingBox.cu:44-50) -> +-1e-20: the plane distances
+    // of that axis are +-1e20 * (face - o), so the axis rejects the box exactly when o lies outside the slab and
+    // constrains nothing otherwise — the reference's parallel branch, with finite reciprocals (never 0 * inf)
+    const auto nz = [](float x) { return fabsf(x) < RT_NZ_MIN ? copysignf(1e-20f, x) : x; };
     r.inv = mk(rcp(nz(r.d.x)), rcp(nz(r.d.y)), rcp(nz(r.d.z)));
     r.oinv = mk(r.o.x * r.inv.x, r.o.y * r.inv.y, r.o.z * r.inv.z);
-#if RT_SLAB_PAD
-    r.pad = mk(0x1p-21f * fabsf(r.oinv.x), 0x1p-21f * fabsf(r.oinv.y), 0x1p-21f * fabsf(r.oinv.z));
+#if RT_SLAB_CONS
+    {   // fmaf(b, inv, -oinv) differs from (b - o) / d by <= 2^-24 |o / d| (oinv's rounding) + ~2^-21.7 |t| (the
+        // reciprocal's 1 ulp, the fma's and the reference's roundings); parallel axes only decide inside / outside
+        const float px = fabsf(r.d.x) < RT_NZ_MIN ? 0.0f : fabsf(r.oinv.x);
+        const float py = fabsf(r.d.y) < RT_NZ_MIN ? 0.0f : fabsf(r.oinv.y);
+        const float pz = fabsf(r.d.z) < RT_NZ_MIN ? 0.0f : fabsf(r.oinv.z);
+        r.pad = 0x1p-22f * fmaxf(px, fmaxf(py, pz));
+    }
 #endif
 #else
     (void)r;
@@ -225,28 +228,26 @@ __device__ __forceinline__ bool slab_ref(const float *b, const f3 &o, const f3 &
     return true;
 }
 
-#if RT_SLAB_PAD
-// the plane-distance interval [min, max] of one axis, widened by the bound (relative 2^-20 + absolute pad)
-__device__ __forceinline__ float pad_lo(float x, float p) { return x - fmaf(fabsf(x), 0x1p-20f, p); }
-__device__ __forceinline__ float pad_hi(float x, float p) { return x + fmaf(fabsf(x), 0x1p-20f, p); }
+#if RT_SLAB_CONS
+// a box's entry / exit distance widened by the bound above (lo, hi >= TMIN > 0 wherever lo < hi can hold)
+__device__ __forceinline__ float cons_lo(float lo, float pad) { return fmaf(lo, 1.0f - 0x1p-20f, -pad); }
+__device__ __forceinline__ float cons_hi(float hi, float pad) { return fmaf(hi, 1.0f + 0x1p-20f, pad); }
 #endif
 __device__ __forceinline__ bool slab(const float *b, const RayP &r, float tmin, float tmax, float &te) {
 #if RT_EXACT
     return slab_ref(b, r.o, r.d, tmin, tmax, te);
 #else
-    if (RT_SLAB_TINY && r.tiny) return slab_ref(b, r.o, r.d, tmin, tmax, te);
     const float tx1 = fmaf(b[0], r.inv.x, -r.oinv.x), tx2 = fmaf(b[1], r.inv.x, -r.oinv.x);
     const float ty1 = fmaf(b[2], r.inv.y, -r.oinv.y), ty2 = fmaf(b[3], r.inv.y, -r.oinv.y);
     const float tz1 = fmaf(b[4], r.inv.z, -r.oinv.z), tz2 = fmaf(b[5], r.inv.z, -r.oinv.z);
-#if RT_SLAB_PAD
-    const float lo = fmaxf(fmaxf(tmin, pad_lo(fminf(tx1, tx2), r.pad.x)), fmaxf(pad_lo(fminf(ty1, ty2), r.pad.y), pad_lo(fminf(tz1, tz2), r.pad.z)));
-    const float hi = fminf(fminf(tmax, pad_hi(fmaxf(tx1, tx2), r.pad.x)), fminf(pad_hi(fmaxf(ty1, ty2), r.pad.y), pad_hi(fmaxf(tz1, tz2), r.pad.z)));
-#else
     const float lo = fmaxf(fmaxf(tmin, fminf(tx1, tx2)), fmaxf(fminf(ty1, ty2), fminf(tz1, tz2)));
     const float hi = fminf(fminf(tmax, fmaxf(tx1, tx2)), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
-#endif
     te = lo;
+#if RT_SLAB_CONS
+    return cons_lo(lo, r.pad) < cons_hi(hi, r.pad);
+#else
     return lo < hi;
+#endif
 #endif
 }
 
@@ -453,6 +454,18 @@ struct Trav {
     Stack stk;
 };
 
+// A popped entry (or the speculative successor) survives its re-test: the reference re-runs the box test with the
+// current tmax, which accepts it iff its entry t < tmax (the exit side passed at the push and tmax only shrinks).
+// RT_SLAB_CONS: the entry is widened by its ray's bound first (a BLAS entry belongs to the current instance's ray).
+__device__ __forceinline__ bool pop_keep(const Trav &T, float tn, uint32_t ref) {
+#if !RT_EXACT && RT_SLAB_CONS
+    return cons_lo(tn, (ref & REF_BLAS) ? T.lr.pad : T.wr.pad) < T.tmax;
+#else
+    (void)ref;
+    return tn < T.tmax;
+#endif
+}
+
 // R: this frame's TLAS root (the persistent kernel holds it in SGPRs, loaded once per wave)
 __device__ __forceinline__ void trav_init(Trav &T, const TreeRoot &R, const f3 &o, const f3 &d) {
     T.wr.o = o; T.wr.d = d; prep(T.wr);
@@ -553,7 +566,7 @@ __device__ __forceinline__ void trav_step(Trav &T, const SceneGPU &sc, SEnt *spi
     // pop until an entry survives the re-test (entry t < tmax)
     while (!T.stk.empty()) {
         const SEnt e = stack_pop(T.stk, spill);
-        if (__uint_as_float(e.tn) < T.tmax) { T.cur = e.ref; return; }
+        if (pop_keep(T, __uint_as_float(e.tn), e.ref)) { T.cur = e.ref; return; }
     }
     T.tracing = false;
 }
@@ -576,7 +589,7 @@ __device__ __forceinline__ void pop_next(Trav &T, const SEnt *spill) {
     while (!T.stk.empty()) {
         const SEnt e = stack_pop(T.stk, spill);
         const float tn = __uint_as_float(e.tn);
-        if (tn < T.tmax) { T.cur = e.ref; T.curT = tn; return; }
+        if (pop_keep(T, tn, e.ref)) { T.cur = e.ref; T.curT = tn; return; }
     }
     T.cur = REF_NONE;
 }
@@ -647,23 +660,11 @@ __device__ __forceinline__ R lds_or_global(uint32_t at, const R *g, uint32_t k) 
     return r;
 }
 
-__device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float oinv, float4 &tn, float4 &tf,
-                                      float pad = 0.0f) {
-    float a0 = fmaf(lo.x, inv, -oinv), b0 = fmaf(hi.x, inv, -oinv);
-    float a1 = fmaf(lo.y, inv, -oinv), b1 = fmaf(hi.y, inv, -oinv);
-    float a2 = fmaf(lo.z, inv, -oinv), b2 = fmaf(hi.z, inv, -oinv);
-    float a3 = fmaf(lo.w, inv, -oinv), b3 = fmaf(hi.w, inv, -oinv);
-#if RT_SLAB_PAD
-    {
-        float n0 = pad_lo(fminf(a0, b0), pad), f0 = pad_hi(fmaxf(a0, b0), pad);
-        float n1 = pad_lo(fminf(a1, b1), pad), f1 = pad_hi(fmaxf(a1, b1), pad);
-        float n2 = pad_lo(fminf(a2, b2), pad), f2 = pad_hi(fmaxf(a2, b2), pad);
-        float n3 = pad_lo(fminf(a3, b3), pad), f3v = pad_hi(fmaxf(a3, b3), pad);
-        a0 = n0; b0 = f0; a1 = n1; b1 = f1; a2 = n2; b2 = f2; a3 = n3; b3 = f3v;
-    }
-#else
-    (void)pad;
-#endif
+__device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float oinv, float4 &tn, float4 &tf) {
+    const float a0 = fmaf(lo.x, inv, -oinv), b0 = fmaf(hi.x, inv, -oinv);
+    const float a1 = fmaf(lo.y, inv, -oinv), b1 = fmaf(hi.y, inv, -oinv);
+    const float a2 = fmaf(lo.z, inv, -oinv), b2 = fmaf(hi.z, inv, -oinv);
+    const float a3 = fmaf(lo.w, inv, -oinv), b3 = fmaf(hi.w, inv, -oinv);
     tn = make_float4(fmaxf(tn.x, fminf(a0, b0)), fmaxf(tn.y, fminf(a1, b1)), fmaxf(tn.z, fminf(a2, b2)), fmaxf(tn.w, fminf(a3, b3)));
     tf = make_float4(fminf(tf.x, fmaxf(a0, b0)), fminf(tf.y, fmaxf(a1, b1)), fminf(tf.z, fmaxf(a2, b2)), fminf(tf.w, fmaxf(a3, b3)));
 }
@@ -697,29 +698,18 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
     const RayP &r = blas ? T.lr : T.wr;
     float t[4];
     bool h[4];
-    if (!RT_WIDE_TINY || !r.tiny) {
+    {
         float4 tn = make_float4(TMIN, TMIN, TMIN, TMIN), tf = make_float4(T.tmax, T.tmax, T.tmax, T.tmax);
-#if RT_SLAB_PAD
-        slab4(lx, hx, r.inv.x, r.oinv.x, tn, tf, r.pad.x);
-        slab4(ly, hy, r.inv.y, r.oinv.y, tn, tf, r.pad.y);
-        slab4(lz, hz, r.inv.z, r.oinv.z, tn, tf, r.pad.z);
-#else
         slab4(lx, hx, r.inv.x, r.oinv.x, tn, tf);
         slab4(ly, hy, r.inv.y, r.oinv.y, tn, tf);
         slab4(lz, hz, r.inv.z, r.oinv.z, tn, tf);
-#endif
         t[0] = tn.x; t[1] = tn.y; t[2] = tn.z; t[3] = tn.w;
+#if RT_SLAB_CONS
+        h[0] = cons_lo(tn.x, r.pad) < cons_hi(tf.x, r.pad); h[1] = cons_lo(tn.y, r.pad) < cons_hi(tf.y, r.pad);
+        h[2] = cons_lo(tn.z, r.pad) < cons_hi(tf.z, r.pad); h[3] = cons_lo(tn.w, r.pad) < cons_hi(tf.w, r.pad);
+#else
         h[0] = tn.x < tf.x; h[1] = tn.y < tf.y; h[2] = tn.z < tf.z; h[3] = tn.w < tf.w;
-    } else {                                          // some |d_axis| < 1e-6: the reference's slab per child
-        const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
-        const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
-        const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
-#pragma unroll
-        for (int k = 0; k < 4; k++) {
-            const float b[6] = {LX[k], HX[k], LY[k], HY[k], LZ[k], HZ[k]};
-            t[k] = 0.0f;
-            h[k] = slab_ref(b, r.o, r.d, TMIN, T.tmax, t[k]);
-        }
+#endif
     }
     float t0 = h[0] ? t[0] : __builtin_huge_valf(), t1 = h[1] ? t[1] : __builtin_huge_valf();
     float t2 = h[2] ? t[2] : __builtin_huge_valf(), t3 = h[3] ? t[3] : __builtin_huge_valf();
@@ -898,7 +888,7 @@ __device__ __forceinline__ uint32_t spec_leaf_phase(Trav &T, const SceneGPU &sc,
             }
         }
         if (chained) pop_next(T, spill);                                   // the root leaf is done
-        else if (T.cur != REF_NONE && !(T.curT < T.tmax)) pop_next(T, spill);   // re-test the successor
+        else if (T.cur != REF_NONE && !pop_keep(T, T.curT, T.cur)) pop_next(T, spill);   // re-test the successor
     }
     if (T.cur == REF_NONE) T.tracing = false;
     return chained ? 1u : 0u;

@@ -8,10 +8,12 @@ For C2 (1080p, 1 spp, depth 2; also at depth 1) and C3 (1080p, 4 spp, depth 4), 
   * "fast_compat_binary": FAST arithmetic on those trees with the binary node-pair traversal (the reference's
               visit order), which separates arithmetic from visit-order ties;
   * "exact_compat": EXACT kernel on those trees (bit-identical by the parity tests);
+  * "exact_sah" / "exact_lbvh": the EXACT kernel (the reference's traversal order and arithmetic) on the bench's
+              SAH / LBVH trees — what the reference's algorithm itself renders on those trees;
   * "<mode>+opt=v+...": any of the above with extra set_option calls (e.g. "fast_compat+lds_scene=0+kernel=0")
 and compares each with the oracle's frame: pixels with any RGBA8 channel |d| > 1 (outliers), max |d|, and the
 per-channel float |d| of the linear RGB.  Output: one JSON object (stdout, or --out).
-RTAMD_LIB selects the library (variant builds, e.g. RT_WIDE_TINY=1 RT_SLAB_TINY=1).
+RTAMD_LIB selects the library (variant builds, e.g. RT_SLAB_CONS=0).
 """
 from __future__ import annotations
 
@@ -50,6 +52,7 @@ def main():
     ap.add_argument("--modes", default="bench,fast_compat,exact_compat")
     ap.add_argument("--out", default=None)
     ap.add_argument("--save-diff", default=None, help="directory: save outlier masks (npz) per case")
+    ap.add_argument("--pairs", default="", help="mode pairs a:b compared with each other too (e.g. bench:exact_sah)")
     args = ap.parse_args()
     frames = [int(f) for f in args.frames.split(",")]
     res = {"lib": os.environ.get("RTAMD_LIB", "default"), "cases": []}
@@ -72,9 +75,11 @@ def main():
             orgb, orgba, _ = o.render(threads=16)
             oracle[f] = (orgb, orgba)
             print(f"oracle {cname} frame {f}: {time.time() - t0:.1f} s", flush=True)
+        kept = {}
         for spec in args.modes.split(","):
             mode, *extra = spec.split("+")
-            build = {"bench": "sah", "lbvh": "lbvh", "lbvh_nogroup": "lbvh", "sah_nogroup": "sah"}.get(mode, "compat")
+            build = {"bench": "sah", "lbvh": "lbvh", "lbvh_nogroup": "lbvh", "sah_nogroup": "sah", "exact_sah": "sah",
+                     "exact_lbvh": "lbvh"}.get(mode, "compat")
             r = Renderer(scene)
             if mode == "fast_compat_binary":                 # FAST arithmetic on the reference's binary visit order
                 r.set_option("wide", 0)
@@ -105,9 +110,10 @@ def main():
                     got[f] = (rgba_buf[f].cpu().numpy().reshape(H, W, 4), rgb_buf[f].cpu().numpy().reshape(H, W, 3))
             else:
                 for f in frames:
-                    rgba, rgb, _ = r.render(f, exact=(mode == "exact_compat"), want_rgb=True)
+                    rgba, rgb, _ = r.render(f, exact=mode.startswith("exact"), want_rgb=True)
                     got[f] = (rgba, rgb)
             r.cleanup()
+            kept[spec] = got
             for f in frames:
                 c = compare(got[f][0], got[f][1], oracle[f][1], oracle[f][0])
                 c.update({"config": cname, "mode": spec, "frame": f, "depth": cam["ray_trace_depth"], "spp": cfg.spp})
@@ -118,6 +124,13 @@ def main():
                     d = np.abs(got[f][0].astype(np.int32) - oracle[f][1].astype(np.int32)).max(axis=-1)
                     np.savez_compressed(os.path.join(args.save_diff, f"{cname}_{spec}_{f}.npz"),
                                         yx=np.argwhere(d > 1).astype(np.int32), d=d[d > 1].astype(np.int32))
+        for pr in filter(None, args.pairs.split(",")):
+            a, b = pr.split(":")
+            for f in frames:
+                c = compare(kept[a][f][0], kept[a][f][1], kept[b][f][0], kept[b][f][1])
+                c.update({"config": cname, "mode": f"{a} vs {b}", "frame": f, "depth": cam["ray_trace_depth"], "spp": cfg.spp})
+                res["cases"].append(c)
+                print(json.dumps(c), flush=True)
     s = json.dumps(res, indent=1)
     if args.out:
         with open(args.out, "w") as fh:

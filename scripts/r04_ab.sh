@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B of one scene option on bench lines (interleaved runs in one call).
 # usage: OPT=name [VALS="0 1"] scripts/r04_ab.sh OUTNAME   (runs each case with --opt $OPT=v for v in VALS, REPS times)
+#        OPT=lib VALS="default nocons" ...                  (library A/B: RTAMD_LIB=lib/librtamd_$v.so, "default" = the build)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/$1
 mkdir -p $OUT
@@ -18,7 +19,12 @@ for rep in $(seq 1 $REPS); do
   for c in "${CS[@]}"; do
     name=${c%%|*}; args=${c#*|}
     for v in ${VALS:-0 1}; do
-      timeout -k 10 300 python3 bench.py $args --no-cpu-baseline --opt $OPT=$v > $OUT/${name}_${v}_$rep.log 2>&1
+      if [ "$OPT" = lib ]; then
+        if [ "$v" = default ]; then lib=""; else lib=$PWD/real-time-gpu-ray-tracer_amd/lib/librtamd_$v.so; fi
+        RTAMD_LIB=$lib timeout -k 10 300 python3 bench.py $args --no-cpu-baseline > $OUT/${name}_${v}_$rep.log 2>&1
+      else
+        timeout -k 10 300 python3 bench.py $args --no-cpu-baseline --opt $OPT=$v > $OUT/${name}_${v}_$rep.log 2>&1
+      fi
       rc=$?
       if [ $rc -ne 0 ]; then echo "$name $v rc=$rc"; tail -5 $OUT/${name}_${v}_$rep.log; exit $rc; fi
       python3 - "$OUT/${name}_${v}_$rep.log" "$name" "$v" <<'PY'

