@@ -41,6 +41,11 @@ LATENCY_BOUND_FRAC = 0.25
 PMC_DIR = os.path.join(REPO, "profiles", "pmc")
 
 
+# width, height, requested spp per config (read before HIP starts; checked against rtamd.scenes.CONFIGS in main)
+FRAME_DIMS = {"C1": (256, 256, 1), "C2": (1920, 1080, 1), "C3": (1920, 1080, 4), "C4": (1920, 1080, 1),
+              "C5": (3840, 2160, 8)}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -221,7 +226,12 @@ def main():
     # a per-frame BLAS rebuild overlaps the traces differently: C2-LBVH's runs 0.50 -> 1.0 ms/frame on lanes off the
     # null stream (the rebuild kernels wait behind the lanes' grids), so those frames keep 3 lanes, the null stream
     # as lane 0 and 4 queues (profiles/r03_session2/lane_streams_*.txt, scene_stream_priority_*.txt)
-    classic = not share and not args.attach_comm and args.rebuild
+    # ... but not a launch of >= 16 M camera paths (C5): the rebuild kernels then sat behind lane 0's traces in the null
+    # stream's hardware queue, and lanes off it run C5 with the rebuild 10.5-10.8 -> 9.7-9.8 ms/frame
+    # (profiles/r04/c5_rebuild/r04s16_*)
+    w, h, spp = FRAME_DIMS[args.config]
+    big = w * h * int(spp ** 0.5) ** 2 >= (16 << 20)
+    classic = not share and not args.attach_comm and args.rebuild and not big
     # with a communicator attached (N > 1, --attach-comm) RCCL's own streams take hardware queues as well: at 12
     # two of three lanes shared one queue and ran back to back (world-1 comm path 0.29 ms/frame, 0.22 at 16-24;
     # 1/8 shares 0.045 -> 0.043; profiles/r03_session2/comm_world1_hwq.jsonl)
@@ -241,6 +251,7 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
 
     cfg = scenes.CONFIGS[args.config]
+    assert FRAME_DIMS[args.config] == (cfg.width, cfg.height, cfg.spp), "FRAME_DIMS out of date"
     scene = scenes.config_scene(cfg)
     r = Renderer(scene, device=local_rank)
     for kv in args.pre_opt:
@@ -258,7 +269,11 @@ def main():
     # measured: 4 lanes for a whole frame (3 with a per-frame rebuild), 8 lanes for a rank's 1/N
     # share (the library's auto grid then gives each launch 100 / lanes + 12 % of the GPU while others are in
     # flight: 37 % at 4 lanes, 24 % at 8; profiles/r03_session2/share_grid_*.txt, lanes_new*.txt)
-    L = max(1, args.overlap if args.overlap is not None else (8 if share else (3 if classic else 4)))
+    # a per-frame rebuild of a >= 16 M-path frame (C5): 2 lanes (the rebuild kernels then find slots between two
+    # traces instead of three or four: 9.78 / 9.76 -> 8.82 ms/frame; 1 lane 13.7; profiles/r04/c5_rebuild/r04s17_*,
+    # r04s18_*); trees built once keep 4 (5.46 against 5.86 with 3, 6.43 with 2)
+    L = max(1, args.overlap if args.overlap is not None else
+            (8 if share else (3 if classic else (2 if args.rebuild and big else 4))))
     overlap = L > 1
     if overlap:
         r.set_option("overlap", L)

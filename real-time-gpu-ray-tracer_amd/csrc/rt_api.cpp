@@ -356,7 +356,7 @@ struct rt_scene {
     // longer waits for every lane's trace).  ev_blas_lane[q]: lane q's last trace of the current set.
     // Option "blas_sets" = 3 (default; 2 = one spare): two spare sets in rotation, so frame k+1's rebuild waits only
     // for frame k-2's trace and three traces stay in flight beside it (spare[0] = the set read longest ago, the next
-    // one written; C5 with the rebuild 11.18 -> 10.85 ms/frame, profiles/r04/c5_grid/).
+    // one written; C5 with the rebuild 11.18 -> 10.85 ms/frame, profiles/r04/c5_rebuild/).
     struct BlasSet {
         DevBuf<NodePair> pairs; DevBuf<NodeQuad> quads; DevBuf<TreeRoot> roots;
         DevBuf<TriHot> tri_hot; DevBuf<TriCold> tri_cold; DevBuf<SphereHot> sph_hot; DevBuf<PrimCold> sph_cold;
@@ -1831,7 +1831,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
             pct = !partner ? 100u : (s->lanes <= 3 ? 50u : 100u / s->lanes + 12u);
             // a launch of >= BIG_LAUNCH_PATHS camera paths (C5: 4K x 4 traced spp = 33 M) keeps all of it: its own
             // tail is a small part of its span, and a half grid only stretches the span (C5 5.88 -> 5.43 ms/frame
-            // with trees built once, 13.3 -> 11.2 with the per-frame rebuild; profiles/r04/c5_grid/)
+            // with trees built once, 13.3 -> 11.2 with the per-frame rebuild; profiles/r04/c5_rebuild/)
             if ((uint64_t)out.units * 64u * cam.sqrt_s * cam.sqrt_s >= rt_scene::BIG_LAUNCH_PATHS) pct = 100u;
         }
         if (pct < 100) blocks = std::max<uint32_t>(8u, blocks * pct / 100u);
