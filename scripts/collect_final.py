@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Collect scripts/r03_final.sh output (gpurun_out/final/) into profiles/:
+"""Collect scripts/r03_final.sh / r04_final.sh output (gpurun_out/$FINAL_SRC, default final/) into profiles/:
 
     python scripts/collect_final.py [OUTDIR=profiles/r03_final]
 
@@ -19,7 +19,7 @@ import shutil
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-SRC = os.path.join(REPO, "gpurun_out", "final")
+SRC = os.path.join(REPO, "gpurun_out", os.environ.get("FINAL_SRC", "final"))
 OUT = os.path.join(REPO, sys.argv[1] if len(sys.argv) > 1 else "profiles/r03_final")
 PEAK = 8000.0
 

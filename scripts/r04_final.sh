@@ -6,7 +6,7 @@
 #   `traffic` with; the driver's own command last.
 # usage: [CONFIGS="C2:sah ..."] [NO_TESTS=1] scripts/r04_final.sh
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-OUT=gpurun_out/final4
+OUT=gpurun_out/${FINAL_OUT:-final4}
 mkdir -p $OUT
 export TMPDIR=/tmp
 run() {  # name timeout cmd...
