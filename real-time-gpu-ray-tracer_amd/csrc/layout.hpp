@@ -14,6 +14,8 @@
 #pragma once
 #include <stdint.h>
 
+#include "../../include/rt.h"
+
 namespace rtamd {
 
 // ---- node references (32 bit) --------------------------------------------------------
@@ -85,8 +87,8 @@ struct alignas(16) NodeQuad {       // 128 B
 static_assert(sizeof(NodeQuad) == 128, "NodeQuad must be 128 B");
 
 struct alignas(16) TriHot {         // 48 B: Moller-Trumbore operands (Triangle.cu:4-44)
-    float v0[3]; float pad0;
-    float e1[3]; float pad1;
+    float v0[3]; float pad0;            // GPU-built BLASes without cold records (SceneGPU::raw_tris): the caller's
+    float e1[3]; float pad1;            // triangle index (pad0) and the group member instance + 1 (pad1), as bits
     float e2[3]; float pad2;
 };
 struct alignas(16) TriCold {        // 48 B: vertex normals + material + caller index
@@ -153,6 +155,9 @@ struct SceneGPU {
     const InstCold *inst_cold;
     const TriHot *tri_hot;
     const TriCold *tri_cold;
+    // GPU-built BLASes (option "cold_records" 0): no TriCold records; a hit triangle's normals and material come from
+    // the caller's triangle (index in TriHot::pad0), so a per-frame rebuild writes and reads half the bytes
+    const rt_triangle *raw_tris;
     const SphereHot *sph_hot;
     const PrimCold *sph_cold;
     const QuadHot *quad_hot;

@@ -662,24 +662,30 @@ __global__ void gather_blas_kernel(const LbvhSeg *segs, const uint32_t *seg_of, 
     const uint32_t slot = S.slot_base + (p - S.item_base);
     const uint32_t prim = S.prim_base + (vals[p] - S.item_base);
     if (S.ptype == RT_PRIM_TRIANGLE) {
-        const rt_triangle t = raw.tris[prim];
+        const rt_triangle &t = raw.tris[prim];
         const V3 v0 = of(t.vertex[0]);
         const V3 e1 = of(t.vertex[1]) - v0, e2 = of(t.vertex[2]) - v0;
-        V3 nn[3];
-        if (t.has_normals) { nn[0] = of(t.normal[0]); nn[1] = of(t.normal[1]); nn[2] = of(t.normal[2]); }
-        else { const V3 u = unit(cross(e1, e2)); nn[0] = u; nn[1] = u; nn[2] = u; }
+        const uint32_t member = S.member_count ? item_member[vals[p]] : 0u;   // a group's BLAS: member instance + 1
         TriHot H;
         H.v0[0] = v0.x; H.v0[1] = v0.y; H.v0[2] = v0.z; H.pad0 = 0.0f;
         H.e1[0] = e1.x; H.e1[1] = e1.y; H.e1[2] = e1.z; H.pad1 = 0.0f;
         H.e2[0] = e2.x; H.e2[1] = e2.y; H.e2[2] = e2.z; H.pad2 = 0.0f;
+        if (!out.tri_cold) {                          // no cold records: the index and member ride in the pads
+            H.pad0 = __uint_as_float(prim);
+            H.pad1 = __uint_as_float(member);
+            out.tri_hot[slot] = H;
+            return;
+        }
+        V3 nn[3];
+        if (t.has_normals) { nn[0] = of(t.normal[0]); nn[1] = of(t.normal[1]); nn[2] = of(t.normal[2]); }
+        else { const V3 u = unit(cross(e1, e2)); nn[0] = u; nn[1] = u; nn[2] = u; }
         TriCold C;
         C.n0[0] = nn[0].x; C.n0[1] = nn[0].y; C.n0[2] = nn[0].z;
         C.n1[0] = nn[1].x; C.n1[1] = nn[1].y; C.n1[2] = nn[1].z;
         C.n2[0] = nn[2].x; C.n2[1] = nn[2].y; C.n2[2] = nn[2].z;
         C.material = material_slot(t.material_type, t.material_index, raw.rough_count);
         C.orig_index = prim;
-        C.pad = 0;
-        if (S.member_count) C.pad = item_member[vals[p]];   // a group's BLAS: the member instance holding `prim`, + 1
+        C.pad = member;
         out.tri_hot[slot] = H;
         out.tri_cold[slot] = C;
     } else if (S.ptype == RT_PRIM_SPHERE) {

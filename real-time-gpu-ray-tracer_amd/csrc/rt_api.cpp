@@ -190,6 +190,12 @@ struct rt_scene {
     // profiles/r02_sweep_grid2.jsonl), else 100 (a frame alone on the GPU takes all of it)
     uint32_t grid_pct = 0;
     static constexpr uint64_t BIG_LAUNCH_PATHS = 16ull << 20;
+    // option "cold_records" (RT_BUILD_LBVH, set before rt_scene_build; default 0): 1 = the BLAS builds write TriCold
+    // records (normals, material, caller index) as the host builders do; 0 = they write TriHot only, with the caller's
+    // triangle index and group member in its pads, and a hit reads normals and material from the caller's triangle
+    // (SceneGPU::raw_tris) — a C5 rebuild's leaf-ordered gather then moves about half the bytes
+    bool cold_records = false;
+    bool raw_shading() const { return build_mode == RT_BUILD_LBVH && !cold_records; }
     uint32_t wide_merge = 0;        // quad trees: binary subtrees of <= wide_merge items become one leaf (set before build)
     DevBuf<TriHot> tri_hot;
     DevBuf<TriCold> tri_cold;
@@ -806,7 +812,8 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.inst_hot = reinterpret_cast<const InstHot *>(s->frame_dev[b] + (gpu_slots ? s->off_hot_s : s->off_hot));
     g.inst_cold = reinterpret_cast<const InstCold *>(s->frame_dev[b] + (gpu_slots ? s->off_cold_s : s->off_cold));
     g.inst_by_slot = s->block_by_slot[b] ? 1u : 0u;   // how frame block b's instance records were staged
-    g.tri_hot = s->tri_hot.p; g.tri_cold = s->tri_cold.p;
+    g.tri_hot = s->tri_hot.p; g.tri_cold = s->raw_shading() ? nullptr : s->tri_cold.p;
+    g.raw_tris = s->raw_shading() ? s->raw_tris.p : nullptr;
     g.sph_hot = s->sph_hot.p; g.sph_cold = s->sph_cold.p;
     g.quad_hot = s->quad_hot.p; g.quad_cold = s->quad_cold.p;
     g.materials = s->materials.p;
@@ -978,7 +985,8 @@ rt_status gpu_build_blas(rt_scene *s) {
         for (int q = 0; q < rt_scene::NLANE; q++)      // created with the first set (gpu_setup_blas); never recorded: no wait
             HIP_TRY(hipStreamWaitEvent(s->stream, sp.ev_lane[q], 0));
         const RawPrimsGPU raw{s->raw_tris.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
-        const PrimOutGPU out{sp.tri_hot.p, sp.tri_cold.p, sp.sph_hot.p, sp.sph_cold.p, sp.quad_hot.p, sp.quad_cold.p};
+        const PrimOutGPU out{sp.tri_hot.p, s->raw_shading() ? nullptr : sp.tri_cold.p, sp.sph_hot.p, sp.sph_cold.p,
+                             sp.quad_hot.p, sp.quad_cold.p};
         HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
         HIP_TRY(s->blas_builder->build(sp.pairs.p, sp.roots.p, s->gpu_counts.p, s->stream));
         HIP_TRY(s->blas_builder->collapse_wide(sp.pairs.p, sp.roots.p, sp.quads.p, nullptr, s->stream));
@@ -997,7 +1005,8 @@ rt_status gpu_build_blas(rt_scene *s) {
     for (int q = 0; q < rt_scene::NLANE; q++)           // "overlap": the other lane's trace may still be running
         if (s->blas_builds && s->r_lane[q]) HIP_TRY(hipStreamWaitEvent(s->stream, s->r_lane[q], 0));
     const RawPrimsGPU raw{s->raw_tris.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
-    const PrimOutGPU out{s->tri_hot.p, s->tri_cold.p, s->sph_hot.p, s->sph_cold.p, s->quad_hot.p, s->quad_cold.p};
+    const PrimOutGPU out{s->tri_hot.p, s->raw_shading() ? nullptr : s->tri_cold.p, s->sph_hot.p, s->sph_cold.p,
+                         s->quad_hot.p, s->quad_cold.p};
     HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
     HIP_TRY(s->blas_builder->build(s->blas_pairs.p, s->blas_roots.p, s->gpu_counts.p, s->stream));
     HIP_TRY(s->blas_builder->collapse_wide(s->blas_pairs.p, s->blas_roots.p, s->blas_quads.p, nullptr, s->stream));
@@ -1024,7 +1033,11 @@ rt_status gpu_setup_blas(rt_scene *s, const uint32_t *slot_count) {
     if ((st = upload(s->raw_sph, s->spheres)) != RT_OK) return st;
     if ((st = upload(s->raw_quad, s->quads)) != RT_OK) return st;
     if ((st = alloc_buf(s->tri_hot, slot_count[RT_PRIM_TRIANGLE])) != RT_OK) return st;
-    if ((st = alloc_buf(s->tri_cold, slot_count[RT_PRIM_TRIANGLE])) != RT_OK) return st;
+    if (s->cold_records) {
+        if ((st = alloc_buf(s->tri_cold, slot_count[RT_PRIM_TRIANGLE])) != RT_OK) return st;
+    } else {
+        s->tri_cold.release();                          // raw_shading(): no TriCold records
+    }
     if ((st = alloc_buf(s->sph_hot, slot_count[RT_PRIM_SPHERE])) != RT_OK) return st;
     if ((st = alloc_buf(s->sph_cold, slot_count[RT_PRIM_SPHERE])) != RT_OK) return st;
     if ((st = alloc_buf(s->quad_hot, slot_count[RT_PRIM_PARALLELOGRAM])) != RT_OK) return st;
@@ -1999,6 +2012,10 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "costmap") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
         s->costmap_on = value == 1;
+    } else if (k == "cold_records") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "cold_records must be 0 or 1");
+        if (s->built) return fail(RT_ERR_STATE, "cold_records must be set before rt_scene_build");
+        s->cold_records = value == 1;
     } else if (k == "blas_sets") {
         if (value != 2 && value != 3) return fail(RT_ERR_INVALID_ARGUMENT, "blas_sets must be 2 or 3");
         RT_TRY(drain(s));
@@ -2152,12 +2169,15 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
         // the slots [slot_base, slot_base + count) of its primitives, in leaf order
         HIP_TRY(hipSetDevice(s->device));
         RT_TRY(drain(s));
-        const size_t n = s->tri_cold.n;
+        const bool raw = s->raw_shading();             // the index rides in TriHot::pad0 (option "cold_records" 0)
+        const size_t n = s->tri_hot.n;
         *bytes = n * sizeof(uint32_t);
         if (capacity && n) {
             const size_t m = std::min(capacity / sizeof(uint32_t), n);
-            HIP_TRY(hipMemcpy2D(dst, sizeof(uint32_t), reinterpret_cast<const uint8_t *>(s->tri_cold.p) + offsetof(TriCold, orig_index),
-                                sizeof(TriCold), sizeof(uint32_t), m, hipMemcpyDeviceToHost));
+            const uint8_t *src0 = raw ? reinterpret_cast<const uint8_t *>(s->tri_hot.p) + offsetof(TriHot, pad0)
+                                      : reinterpret_cast<const uint8_t *>(s->tri_cold.p) + offsetof(TriCold, orig_index);
+            HIP_TRY(hipMemcpy2D(dst, sizeof(uint32_t), src0, raw ? sizeof(TriHot) : sizeof(TriCold), sizeof(uint32_t), m,
+                                hipMemcpyDeviceToHost));
         }
         return RT_OK;
     } else if (k == "unit_cost" || k == "unit_order") {
@@ -2226,8 +2246,9 @@ rt_status rt_scene_update_triangles(rt_scene *s, size_t first, size_t count, con
     for (size_t k = 0; k < count; k++) material_slot(s, tris[k].material_type, tris[k].material_index, ok);
     if (!ok) return fail(RT_ERR_INVALID_ARGUMENT, "triangle references a material out of range");
     HIP_TRY(hipSetDevice(s->device));
-    // no drain: traces never read raw_tris, and the copy is ordered behind the scene stream's pending BLAS
-    // builds (the next build, which the frame update enqueues after it, reads the new triangles)
+    // no drain: the copy is ordered behind the scene stream's pending BLAS builds (the next build, which the frame
+    // update enqueues after it, reads the new triangles); with raw_shading() traces read raw_tris at their hits too,
+    // so it also waits for every lane's last trace (and the last synchronous one)
     if (s->ev_raw_staged) RT_TRY(wait_event(s, s->ev_raw_staged));      // the previous staged copy is done
     else HIP_TRY(hipEventCreateWithFlags(&s->ev_raw_staged, hipEventDisableTiming));
     if (count > s->raw_stage_cap) {
@@ -2239,6 +2260,11 @@ rt_status rt_scene_update_triangles(rt_scene *s, size_t first, size_t count, con
     }
     std::memcpy(s->raw_stage, tris, count * sizeof(rt_triangle));
     std::memcpy(s->tris.data() + first, tris, count * sizeof(rt_triangle));
+    if (s->raw_shading()) {
+        if (s->r_done) HIP_TRY(hipStreamWaitEvent(s->stream, s->r_done, 0));
+        for (int q = 0; q < rt_scene::NLANE; q++)
+            if (s->r_lane[q]) HIP_TRY(hipStreamWaitEvent(s->stream, s->r_lane[q], 0));
+    }
     HIP_TRY(hipMemcpyAsync(s->raw_tris.p + first, s->raw_stage, count * sizeof(rt_triangle), hipMemcpyHostToDevice, s->stream));
     HIP_TRY(hipEventRecord(s->ev_raw_staged, s->stream));
     // instance boxes derived from the triangles (RenderPin.cu:124-139); VTK-style bounds stay as given
@@ -2404,7 +2430,15 @@ rt_status rt_scene_export_blas(const rt_scene *s, uint32_t b, float *boxes, uint
         HIP_TRY(read_back(roots, s->blas_roots.p, s->blas_roots.n));
         const uint32_t type = s->blas[b].type;
         std::vector<uint32_t> orig;
-        if (type == RT_PRIM_TRIANGLE) {
+        if (type == RT_PRIM_TRIANGLE && s->raw_shading()) {
+            std::vector<TriHot> h;
+            HIP_TRY(read_back(h, s->tri_hot.p, s->tri_hot.n));
+            for (const TriHot &x : h) {
+                uint32_t v;
+                std::memcpy(&v, &x.pad0, sizeof v);
+                orig.push_back(v);
+            }
+        } else if (type == RT_PRIM_TRIANGLE) {
             std::vector<TriCold> c;
             HIP_TRY(read_back(c, s->tri_cold.p, s->tri_cold.n));
             for (const TriCold &x : c) orig.push_back(x.orig_index);

@@ -128,6 +128,16 @@ __device__ __forceinline__ f3 unit(f3 a) {                   // Vec3.cuh:129-137
     return mk(a.x * f, a.y * f, a.z * f);
 }
 __device__ __forceinline__ float comp(f3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
+// unit(e1 x e2) with the arithmetic the BLAS builders store a triangle's normals with (lbvh.hip gather_blas_kernel,
+// host_math.hpp; Triangle.cuh:26-46): correctly rounded 1 / sqrt, no contraction, in every FAST variant
+__device__ __forceinline__ f3 tri_face_normal(f3 a, f3 b) {
+#pragma clang fp contract(off)
+    const f3 c = mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+    float d = 0.0f;
+    d += c.x * c.x; d += c.y * c.y; d += c.z * c.z;
+    const float f = 1.0f / sqrtf(d);
+    return mk(c.x * f, c.y * f, c.z * f);
+}
 
 __device__ __forceinline__ bool f_eq(float a, float b) { return fabsf(a - b) < FZERO; }
 __device__ __forceinline__ bool in_range(float v, float mn, float mx) {      // Range.cuh:33-43
@@ -955,7 +965,11 @@ struct Surface { f3 p, n; uint32_t material; uint32_t orig; uint32_t member; }; 
 
 // Recompute the hit point / normal of the closest hit exactly as the primitive hit function and
 // Instance::hit (Instance.cu:41-45) would have stored them.
-template <bool LDSS = false>
+// RAW: where a hit triangle's normals / material / caller index come from — 0 its TriCold record, 1 the caller's
+// triangle (SceneGPU::raw_tris, GPU-built BLASes without cold records), 2 whichever the scene has (a runtime branch).
+// The persistent kernel is instantiated per scene kind (0 / 1): with the branch inlined, host-built scenes' kernel
+// lost 2 VGPRs to spills and ~1 % per frame (profiles/r04/cold_records/).
+template <bool LDSS = false, int RAW = 2>
 __device__ __forceinline__ Surface finalize(const SceneGPU &sc, const f3 &wo, const f3 &wd, const Hit &h) {
 #if !RT_EXACT
     const InstCold IC = LDSS ? lds_or_global(sc.lds_icold, sc.inst_cold, h.inst) : sc.inst_cold[h.inst];
@@ -979,10 +993,28 @@ __device__ __forceinline__ Surface finalize(const SceneGPU &sc, const f3 &wo, co
     f3 n;
     Surface s;
     if (h.ptype == RT_PRIM_TRIANGLE) {                                         // Triangle.cu:40-42
-        const TriCold &T = sc.tri_cold[h.slot];
-        const f3 nn = unit(add(add(scl(ld3(T.n0), (1.0f - h.u) - h.v), scl(ld3(T.n1), h.u)), scl(ld3(T.n2), h.v)));
+        f3 n0, n1, n2;
+        if (RAW == 1 || (RAW == 2 && sc.raw_tris)) {   // GPU-built BLAS without cold records (layout.hpp SceneGPU)
+            const TriHot &H = sc.tri_hot[h.slot];
+            s.orig = __float_as_uint(H.pad0);
+            s.member = __float_as_uint(H.pad1);
+            const rt_triangle &R = sc.raw_tris[s.orig];
+            if (R.has_normals) {
+                n0 = mk(R.normal[0].x, R.normal[0].y, R.normal[0].z);
+                n1 = mk(R.normal[1].x, R.normal[1].y, R.normal[1].z);
+                n2 = mk(R.normal[2].x, R.normal[2].y, R.normal[2].z);
+            } else {
+                n0 = tri_face_normal(ld3(H.e1), ld3(H.e2)); n1 = n0; n2 = n0;
+            }
+            s.material = R.material_type == RT_MAT_ROUGH ? R.material_index
+                                                         : ((sc.rough_count + R.material_index) | MAT_METAL_BIT);
+        } else {
+            const TriCold &T = sc.tri_cold[h.slot];
+            n0 = ld3(T.n0); n1 = ld3(T.n1); n2 = ld3(T.n2);
+            s.material = T.material; s.orig = T.orig_index; s.member = T.pad;
+        }
+        const f3 nn = unit(add(add(scl(n0, (1.0f - h.u) - h.v), scl(n1, h.u)), scl(n2, h.v)));
         n = dot(ld, nn) < 0.0f ? nn : neg(nn);
-        s.material = T.material; s.orig = T.orig_index; s.member = T.pad;
     } else if (h.ptype == RT_PRIM_SPHERE) {                                    // Sphere.cu:37-39
 #if !RT_EXACT
         const SphereHot S = LDSS ? lds_or_global(sc.lds_sph_hot, sc.sph_hot, h.slot) : sc.sph_hot[h.slot];
@@ -1249,7 +1281,7 @@ __device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t
     }
 }
 
-template <bool COUNT, bool WIDE>
+template <bool COUNT, bool WIDE, int RAW>
 __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out,
                                                        uint32_t *queue, uint32_t threshold, unsigned long long *counters) {
     __shared__ unsigned long long lds_stack[LDS_DEPTH][BLOCK];
@@ -1413,7 +1445,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             f3 no = T.wr.o, nd = T.wr.d;                                     // next segment
             if (T.found) {
                 if (COUNT) cnt.hits++;
-                const Surface s = finalize<WIDE>(sc, T.wr.o, T.wr.d, T.hit);
+                const Surface s = finalize<WIDE, RAW>(sc, T.wr.o, T.wr.d, T.hit);
                 DIAG_WAIT_VM();
                 DIAG_T(t_hit);
                 const uint32_t mi = s.material & ~MAT_METAL_BIT;
@@ -1518,11 +1550,11 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
 }
 
 // Register budget variants: WPE = minimum waves per SIMD the compiler must allow (0 = its choice).
-template <bool COUNT, int WPE, bool WIDE = false>
+template <bool COUNT, int WPE, bool WIDE = false, int RAW = 2>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
 void render_persistent_kernel(SceneGPU sc, CameraGPU cam, OutputGPU out, uint32_t *queue, uint32_t threshold,
                               unsigned long long *counters) {
-    render_persistent_body<COUNT, WIDE>(sc, cam, out, queue, threshold, counters);
+    render_persistent_body<COUNT, WIDE, RAW>(sc, cam, out, queue, threshold, counters);
 }
 
 __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const float *rays, uint32_t n, rt_hit *hits) {
@@ -1568,7 +1600,7 @@ hipError_t RT_SUFFIX(launch_render)(const SceneGPU &sc, const CameraGPU &cam, co
 }
 
 namespace {
-template <int WPE, bool WIDE = false>
+template <int WPE, bool WIDE = false, int RAW = 2>
 hipError_t launch_persistent_wpe(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
                                  unsigned long long *counters, uint32_t *queue, uint32_t blocks_per_cu_cus,
                                  uint32_t threshold, hipStream_t stream) {
@@ -1576,16 +1608,16 @@ hipError_t launch_persistent_wpe(const SceneGPU &sc, const CameraGPU &cam, const
     const uint32_t need = (out.units + (BLOCK / 64) - 1) / (BLOCK / 64);
     const dim3 grid(blocks_per_cu_cus < need ? blocks_per_cu_cus : need);
     if (count)
-        hipLaunchKernelGGL((render_persistent_kernel<true, WPE, WIDE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
+        hipLaunchKernelGGL((render_persistent_kernel<true, WPE, WIDE, RAW>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
     else
-        hipLaunchKernelGGL((render_persistent_kernel<false, WPE, WIDE>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
+        hipLaunchKernelGGL((render_persistent_kernel<false, WPE, WIDE, RAW>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
     return hipGetLastError();
 }
 template <int WPE, bool WIDE = false>
 uint32_t blocks_per_cu_wpe() {
     using namespace RT_SUFFIX(dev);
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false, WPE, WIDE>, BLOCK, 0) != hipSuccess) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false, WPE, WIDE, (WIDE ? 0 : 2)>, BLOCK, 0) != hipSuccess) return 1;
     return n > 0 ? (uint32_t)n : 1u;
 }
 #if RT_EXACT
@@ -1604,16 +1636,20 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
         const hipError_t e = hipMemsetAsync(queue, 0, QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
     }
-    if (sc.wide && HAS_WIDE) {
-        if (variant == 4) return launch_persistent_wpe<4, HAS_WIDE>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-        return launch_persistent_wpe<3, HAS_WIDE>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+    if (sc.wide && HAS_WIDE) {              // quad trees: one instance per scene kind (finalize's RAW)
+        if (sc.raw_tris) {
+            if (variant == 4) return launch_persistent_wpe<4, HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+            return launch_persistent_wpe<3, HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+        }
+        if (variant == 4) return launch_persistent_wpe<4, HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+        return launch_persistent_wpe<3, HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     }
     if (variant == 4) return launch_persistent_wpe<4>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
     return launch_persistent_wpe<0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
 }
 
 uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, bool wide) {
-    if (wide && HAS_WIDE) return variant == 4 ? blocks_per_cu_wpe<4, HAS_WIDE>() : blocks_per_cu_wpe<3, HAS_WIDE>();
+    if (wide && HAS_WIDE) return variant == 4 ? blocks_per_cu_wpe<4, HAS_WIDE>() : blocks_per_cu_wpe<3, HAS_WIDE>();   // (RAW 0; 1 has the same budget)
     if (variant == 4) return blocks_per_cu_wpe<4>();
     return blocks_per_cu_wpe<0>();
 }

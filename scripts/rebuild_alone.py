@@ -17,10 +17,15 @@ def main():
     ap.add_argument("--config", default="C5")
     ap.add_argument("--updates", type=int, default=20)
     ap.add_argument("--opt", action="append", default=[])
+    ap.add_argument("--pre-opt", action="append", default=[], help="options set before the build")
     a = ap.parse_args()
     from rtamd import Renderer, scenes
     cfg = scenes.CONFIGS[a.config]
-    r = Renderer(scenes.config_scene(cfg)).build_acceleration_structure(0, mode="lbvh")
+    r = Renderer(scenes.config_scene(cfg))
+    for kv in a.pre_opt:
+        k, v = kv.split("=")
+        r.set_option(k, int(v))
+    r.build_acceleration_structure(0, mode="lbvh")
     r.configure_camera(cfg.width, cfg.height, sample_count=cfg.spp, ray_trace_depth=cfg.depth)
     r.set_option("rebuild", 1)
     for kv in a.opt:
@@ -35,7 +40,7 @@ def main():
         r.update(f)
     r.synchronize()
     ms = (time.perf_counter() - t0) / a.updates * 1e3
-    print(json.dumps({"config": a.config, "updates": a.updates, "ms_per_update": round(ms, 4), "opts": a.opt}), flush=True)
+    print(json.dumps({"config": a.config, "updates": a.updates, "ms_per_update": round(ms, 4), "opts": a.pre_opt + a.opt}), flush=True)
     r.cleanup()
 
 
