@@ -70,12 +70,12 @@ __device__ __forceinline__ void merge_into(float *m, const float *a) {   // Boun
     }
 }
 
-__device__ __forceinline__ void tri_box_centroid(const rt_triangle &t, Box &bx, V3 &c) {   // Triangle.cu:46-62, .cuh:53-61
+__device__ __forceinline__ void tri_box_centroid(const float *t, Box &bx, V3 &c) {   // Triangle.cu:46-62, .cuh:53-61
     V3 mn, mx;
     float lo[3], hi[3], cc[3];
 #pragma unroll
     for (int i = 0; i < 3; i++) {
-        const float a = comp(of(t.vertex[0]), i), b = comp(of(t.vertex[1]), i), d = comp(of(t.vertex[2]), i);
+        const float a = t[i], b = t[3 + i], d = t[6 + i];              // vertices 0, 1, 2 (9 floats)
         float l = a, h = a;
         if (b < l) l = b;
         if (d < l) l = d;
@@ -140,7 +140,7 @@ __global__ void prep_blas_kernel(const LbvhSeg *segs, const uint32_t *seg_of, ui
     const uint32_t prim = S.prim_base + (it - S.item_base);
     Box bx;
     V3 c;
-    if (S.ptype == RT_PRIM_TRIANGLE) tri_box_centroid(raw.tris[prim], bx, c);
+    if (S.ptype == RT_PRIM_TRIANGLE) tri_box_centroid(raw.tri_verts + 9 * (size_t)prim, bx, c);
     else if (S.ptype == RT_PRIM_SPHERE) sphere_box_centroid(raw.spheres[prim], bx, c);
     else quad_box_centroid(raw.quads[prim], bx, c);
 #pragma unroll
@@ -662,9 +662,9 @@ __global__ void gather_blas_kernel(const LbvhSeg *segs, const uint32_t *seg_of, 
     const uint32_t slot = S.slot_base + (p - S.item_base);
     const uint32_t prim = S.prim_base + (vals[p] - S.item_base);
     if (S.ptype == RT_PRIM_TRIANGLE) {
-        const rt_triangle &t = raw.tris[prim];
-        const V3 v0 = of(t.vertex[0]);
-        const V3 e1 = of(t.vertex[1]) - v0, e2 = of(t.vertex[2]) - v0;
+        const float *tv = raw.tri_verts + 9 * (size_t)prim;
+        const V3 v0 = v3(tv[0], tv[1], tv[2]);
+        const V3 e1 = v3(tv[3], tv[4], tv[5]) - v0, e2 = v3(tv[6], tv[7], tv[8]) - v0;
         const uint32_t member = S.member_count ? item_member[vals[p]] : 0u;   // a group's BLAS: member instance + 1
         TriHot H;
         H.v0[0] = v0.x; H.v0[1] = v0.y; H.v0[2] = v0.z; H.pad0 = 0.0f;
@@ -676,6 +676,7 @@ __global__ void gather_blas_kernel(const LbvhSeg *segs, const uint32_t *seg_of, 
             out.tri_hot[slot] = H;
             return;
         }
+        const rt_triangle &t = raw.tris[prim];
         V3 nn[3];
         if (t.has_normals) { nn[0] = of(t.normal[0]); nn[1] = of(t.normal[1]); nn[2] = of(t.normal[2]); }
         else { const V3 u = unit(cross(e1, e2)); nn[0] = u; nn[1] = u; nn[2] = u; }
@@ -1085,6 +1086,22 @@ __global__ __launch_bounds__(SMALL_BLOCK) void tlas_small_kernel(SmallTlasArgs a
 }
 
 }  // namespace lbvh
+
+__global__ void extract_tri_verts_kernel(const rt_triangle *tris, float *verts, size_t first, size_t count) {
+    const size_t k = (size_t)blockIdx.x * lbvh::BLOCK + threadIdx.x;
+    if (k >= count) return;
+    const rt_triangle &t = tris[first + k];
+    float *v = verts + 9 * (first + k);
+#pragma unroll
+    for (int i = 0; i < 3; i++) { v[3 * i] = t.vertex[i].x; v[3 * i + 1] = t.vertex[i].y; v[3 * i + 2] = t.vertex[i].z; }
+}
+
+hipError_t extract_tri_verts(const rt_triangle *tris, float *verts, size_t first, size_t count, hipStream_t stream) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(extract_tri_verts_kernel, dim3((uint32_t)((count + lbvh::BLOCK - 1) / lbvh::BLOCK)), dim3(lbvh::BLOCK), 0, stream, tris,
+                       verts, first, count);
+    return hipGetLastError();
+}
 
 hipError_t launch_tlas_small(const SmallTlasArgs &a, hipStream_t stream) {
     hipLaunchKernelGGL(lbvh::tlas_small_kernel, dim3(1), dim3(lbvh::SMALL_BLOCK), 0, stream, a);

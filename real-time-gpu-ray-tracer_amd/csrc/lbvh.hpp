@@ -46,6 +46,8 @@ struct LbvhSeg {            // one tree of the forest
 // cold records from them on every BLAS build).
 struct RawPrimsGPU {
     const rt_triangle *tris;
+    const float *tri_verts; // the triangles' vertices alone, 9 floats each (extract_tri_verts): what the box / Morton
+                            // pass and the leaf-ordered gather read, 36 of the 88 B of an rt_triangle
     const rt_sphere *spheres;
     const rt_parallelogram *quads;
     uint32_t rough_count;   // material slot of metal m = rough_count + m
@@ -70,6 +72,8 @@ struct SmallTlasArgs {
     uint32_t leaf_cap;
 };
 hipError_t launch_tlas_small(const SmallTlasArgs &a, hipStream_t stream);
+// verts[9 k ..] = the vertices of tris[k] for k in [first, first + count)
+hipError_t extract_tri_verts(const rt_triangle *tris, float *verts, size_t first, size_t count, hipStream_t stream);
 
 class LbvhBuilder {
 public:

@@ -338,6 +338,7 @@ struct rt_scene {
     // RT_BUILD_LBVH: GPU builders and the raw caller primitives they read
     LbvhBuilder *blas_builder = nullptr, *tlas_builder = nullptr;
     DevBuf<rt_triangle> raw_tris;
+    DevBuf<float> raw_verts;            // 9 floats per triangle (extract_tri_verts): the builder's reads
     // rt_scene_update_triangles: the new triangles are staged in pinned memory and copied on the scene stream,
     // behind the BLAS builds that read raw_tris (the only readers) and without waiting for any trace
     rt_triangle *raw_stage = nullptr;
@@ -434,7 +435,7 @@ struct rt_scene {
         timeline.release(); costmap.release();
         for (int q = 0; q < NLANE; q++) { unit_cost[q].release(); unit_order[q].release(); }
         delete blas_builder; delete tlas_builder;
-        raw_tris.release(); raw_sph.release(); raw_quad.release(); blas_roots.release(); inst_blas.release();
+        raw_tris.release(); raw_verts.release(); raw_sph.release(); raw_quad.release(); blas_roots.release(); inst_blas.release();
         blas_wide_refs.release();
         gpu_counts.release(); inst_params.release();
         for (BlasSet &sp : spare) sp.release();
@@ -984,7 +985,7 @@ rt_status gpu_build_blas(rt_scene *s) {
         }
         for (int q = 0; q < rt_scene::NLANE; q++)      // created with the first set (gpu_setup_blas); never recorded: no wait
             HIP_TRY(hipStreamWaitEvent(s->stream, sp.ev_lane[q], 0));
-        const RawPrimsGPU raw{s->raw_tris.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
+        const RawPrimsGPU raw{s->raw_tris.p, s->raw_verts.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
         const PrimOutGPU out{sp.tri_hot.p, s->raw_shading() ? nullptr : sp.tri_cold.p, sp.sph_hot.p, sp.sph_cold.p,
                              sp.quad_hot.p, sp.quad_cold.p};
         HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
@@ -1004,7 +1005,7 @@ rt_status gpu_build_blas(rt_scene *s) {
     if (s->blas_builds && s->r_done) HIP_TRY(hipStreamWaitEvent(s->stream, s->r_done, 0));
     for (int q = 0; q < rt_scene::NLANE; q++)           // "overlap": the other lane's trace may still be running
         if (s->blas_builds && s->r_lane[q]) HIP_TRY(hipStreamWaitEvent(s->stream, s->r_lane[q], 0));
-    const RawPrimsGPU raw{s->raw_tris.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
+    const RawPrimsGPU raw{s->raw_tris.p, s->raw_verts.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
     const PrimOutGPU out{s->tri_hot.p, s->raw_shading() ? nullptr : s->tri_cold.p, s->sph_hot.p, s->sph_cold.p,
                          s->quad_hot.p, s->quad_cold.p};
     HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
@@ -1030,6 +1031,8 @@ rt_status gpu_setup_blas(rt_scene *s, const uint32_t *slot_count) {
     if (!ok) return fail(RT_ERR_INVALID_ARGUMENT, "primitive references a material out of range");
     rt_status st;
     if ((st = upload(s->raw_tris, s->tris)) != RT_OK) return st;
+    if ((st = alloc_buf(s->raw_verts, 9 * s->tris.size())) != RT_OK) return st;
+    HIP_TRY(extract_tri_verts(s->raw_tris.p, s->raw_verts.p, 0, s->tris.size(), s->stream));
     if ((st = upload(s->raw_sph, s->spheres)) != RT_OK) return st;
     if ((st = upload(s->raw_quad, s->quads)) != RT_OK) return st;
     if ((st = alloc_buf(s->tri_hot, slot_count[RT_PRIM_TRIANGLE])) != RT_OK) return st;
@@ -2266,6 +2269,7 @@ rt_status rt_scene_update_triangles(rt_scene *s, size_t first, size_t count, con
             if (s->r_lane[q]) HIP_TRY(hipStreamWaitEvent(s->stream, s->r_lane[q], 0));
     }
     HIP_TRY(hipMemcpyAsync(s->raw_tris.p + first, s->raw_stage, count * sizeof(rt_triangle), hipMemcpyHostToDevice, s->stream));
+    HIP_TRY(extract_tri_verts(s->raw_tris.p, s->raw_verts.p, first, count, s->stream));
     HIP_TRY(hipEventRecord(s->ev_raw_staged, s->stream));
     // instance boxes derived from the triangles (RenderPin.cu:124-139); VTK-style bounds stay as given
     for (size_t i = 0; i < s->inst.size(); i++) {
