@@ -124,7 +124,7 @@ def test_fast_kernel_on_reference_trees(gpu_lib, case, wide):
     kernel's arithmetic is the reference's wherever a value reaches a hit or a pixel; its box culls are conservative
     (RT_SLAB_CONS: never reject a box the reference's slab accepts).  What remains are hits on a box boundary that
     the reference's own slab rounding culls and the FAST kernel tests (and, with quads, a visit-order tie inside the
-    1e-6 window): measured 0 pixels on 7 of 10 C2 / C3 / C5 frames, 1 pixel on the others (C3 frame 37: 4 LSB,
+    1e-6 window): measured 0 pixels on 15 of 20 C2 / C3 / C4 / C5 frame renders, 1 pixel on the others (C3 frame 37: 4 LSB,
     C5: 25-27 LSB); held to <= 2 pixels per frame (profiles/r04/c5_compat_residual/)."""
     name, scene, W, H, cam, orc = case
     r = Renderer(scene).set_option("wide", wide).build_acceleration_structure(0, mode="compat").configure_camera(W, H, **cam)
