@@ -192,7 +192,9 @@ typedef struct rt_render_opts {
     /* Optional device outputs (hipMalloc'd / torch device memory on this scene's GPU). */
     void *rgba8_device;        /* uchar4 per pixel */
     void *rgb32_device;        /* 3 floats per pixel, linear average before gamma */
-    void *stream;              /* hipStream_t to enqueue on; NULL -> the scene's stream */
+    void *stream;              /* hipStream_t to enqueue on; NULL -> the scene's stream, and when a device
+                                * output is given the frame is ordered after the caller's null-stream work
+                                * enqueued before the call, and that null stream's later work after the frame */
 } rt_render_opts;
 
 typedef struct rt_stats {
@@ -326,7 +328,18 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "rebuild"   : RT_BUILD_LBVH only: 1 = rebuild every BLAS on the GPU every frame (default 0)
  *   "timeline"  : 1 = record a per-wave timeline of each persistent launch (debug)
  *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal steps (debug)
- *   "tlas_leaf" : instances per leaf of the per-frame TLAS (1..4, default 1; GPU-built TLASes: set before rt_scene_build)
+ *   "tlas_sah"  : RT_BUILD_SAH: 1 (default) = build the per-frame host TLAS with SAH; 0 = the reference's median split
+ *                 (TLAS.cu:4-129; "tlas_median_leaf" 1..2 = its leaf size, 0 = the reference's 2)
+ *   "tlas_leaf" : instances per leaf of an SAH or GPU-built TLAS (1..4, default 1; GPU-built TLASes: set before
+ *                 rt_scene_build)
+ *   "wide"      : FAST persistent kernel: 1 (default) = quad trees (the reference's trees and GPU-built ones: two
+ *                 binary levels per quad visited in the binary tree's order; RT_BUILD_SAH: the greedy collapse
+ *                 visited by entry t), 0 = binary node pairs
+ *   "cold_records": RT_BUILD_LBVH: 1 = the GPU builder writes TriCold records (normals, material, caller index) beside
+ *                 TriHot; 0 (default) = a hit reads the caller's triangle instead (same pixels; set before
+ *                 rt_scene_build)
+ *   "blas_sets" : RT_BUILD_LBVH rebuilds with "blas_double": BLAS sets cycled (2..3, default 3): frame k+1's rebuild
+ *                 waits only for the trace of frame k + 1 - sets (set before rt_scene_build)
  *   "blas_leaf" : RT_BUILD_SAH: primitives per BLAS leaf (1..4, default 4; set before rt_scene_build)
  *   "gpu_tlas"  : RT_BUILD_SAH: 1 = keep the host-built SAH BLASes but compute the instance records and
  *                 build the TLAS on the GPU every frame, as RT_BUILD_LBVH does (only changed instances

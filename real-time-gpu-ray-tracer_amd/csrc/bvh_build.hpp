@@ -381,10 +381,11 @@ inline FlatTree flatten_tree(const Tree &t, uint32_t pair_base, uint32_t slot_ba
     return f;
 }
 
-// Quad form of one tree (FAST kernel, option "wide").  Each quad starts from a binary interior node's
-// two children and repeatedly replaces its largest-area interior child by that child's two children
-// until it holds 4 (or only leaves are left) — the usual BVH2 -> BVH4 collapse; leaves keep their refs
-// (same leaf-ordered slots), so the quad tree holds exactly the binary tree's leaves.
+// Quad form of one tree (FAST kernel, option "wide").  The quad of a binary interior node holds its two
+// binary levels below it as two halves (layout.hpp NodeQuad): slots 0, 1 = the left child's children,
+// slots 2, 3 = the right child's, a leaf child in its half's first slot with the second empty; leaves keep
+// their refs (same leaf-ordered slots), so the quad tree holds exactly the binary tree's leaves, and the
+// kernel can visit them in the binary tree's order (BLAS.cu:186-202).
 struct FlatWide {
     std::vector<NodeQuad> quads;
     uint32_t root_ref = 0;
@@ -396,8 +397,11 @@ struct FlatWide {
 // fuller leaves mean fewer leaf rounds per ray for the same primitive tests.
 // level_order: quads numbered level by level (breadth first), so the first k quads are the tree's top
 // levels (the LDS-resident part of a group's BLAS); otherwise depth first
+// halves = false (host SAH trees): the greedy BVH2 -> BVH4 collapse instead — a quad starts from a binary node's two
+// children and repeatedly replaces its largest-area interior child by that child's two children until it holds 4
+// (fewer quads per ray; the kernel visits such quads by entry t); empty slots have every bound = +inf.
 inline FlatWide flatten_tree_wide(const Tree &t, uint32_t quad_base, uint32_t slot_base, uint32_t ptype, bool blas,
-                                  uint32_t merge_cap = 0, bool level_order = false) {
+                                  bool halves = true, uint32_t merge_cap = 0, bool level_order = false) {
     FlatWide f;
     const uint32_t n = (uint32_t)t.nodes.size();
     if (n == 0) return f;
@@ -424,41 +428,67 @@ inline FlatWide flatten_tree_wide(const Tree &t, uint32_t quad_base, uint32_t sl
             todo.pop_back();
         }
         f.height = std::max(f.height, w.depth);
-        uint32_t ch[4] = {t.nodes[w.node].index, t.nodes[w.node].index + 1, 0, 0};
-        uint32_t nc = 2;
-        while (nc < 4) {
-            int best = -1;
-            float area = -1.0f;
-            for (uint32_t k = 0; k < nc; k++)
-                if (!is_leaf(ch[k]) && half_area(t.nodes[ch[k]].box) > area) {
-                    area = half_area(t.nodes[ch[k]].box);
-                    best = (int)k;
-                }
-            if (best < 0) break;
-            const uint32_t left = t.nodes[ch[best]].index;
-            ch[best] = left;
-            ch[nc++] = left + 1;
-        }
         NodeQuad q;
-        for (uint32_t k = 0; k < 4; k++) {
+        if (!halves) {
+            uint32_t ch[4] = {t.nodes[w.node].index, t.nodes[w.node].index + 1, 0, 0};
+            uint32_t nc = 2;
+            while (nc < 4) {
+                int best = -1;
+                float area = -1.0f;
+                for (uint32_t k = 0; k < nc; k++)
+                    if (!is_leaf(ch[k]) && half_area(t.nodes[ch[k]].box) > area) {
+                        area = half_area(t.nodes[ch[k]].box);
+                        best = (int)k;
+                    }
+                if (best < 0) break;
+                const uint32_t left = t.nodes[ch[best]].index;
+                ch[best] = left;
+                ch[nc++] = left + 1;
+            }
+            for (uint32_t k = 0; k < 4; k++) {
+                float b[6];
+                uint32_t ref = REF_EMPTY;
+                if (k < nc) {
+                    t.nodes[ch[k]].box.store(b);
+                    if (is_leaf(ch[k])) {
+                        ref = leaf_ref(ch[k]);
+                    } else {
+                        const uint32_t qi = (uint32_t)f.quads.size();
+                        f.quads.emplace_back();
+                        ref = make_interior_ref(quad_base + qi, blas);
+                        todo.push_back({ch[k], qi, w.depth + 1});
+                    }
+                } else {
+                    for (float &x : b) x = std::numeric_limits<float>::infinity();   // rejected by every slab test
+                }
+                quad_set_slot(q, k, b, ref);
+            }
+            f.quads[w.quad] = q;
+            continue;
+        }
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint32_t c = t.nodes[w.node].index + h;
             float b[6];
-            if (k < nc) {
-                t.nodes[ch[k]].box.store(b);
-            } else {
-                for (float &x : b) x = std::numeric_limits<float>::infinity();   // rejected by every slab test
+            if (is_leaf(c)) {                          // a leaf half: the leaf, then an empty slot with its box
+                t.nodes[c].box.store(b);
+                quad_set_slot(q, 2 * h, b, leaf_ref(c));
+                quad_set_slot(q, 2 * h + 1, b, REF_EMPTY);
+                continue;
             }
-            q.lo_x[k] = b[0]; q.hi_x[k] = b[1]; q.lo_y[k] = b[2]; q.hi_y[k] = b[3]; q.lo_z[k] = b[4]; q.hi_z[k] = b[5];
-            if (k >= nc) {
-                q.ref[k] = REF_EMPTY;
-            } else if (is_leaf(ch[k])) {
-                q.ref[k] = leaf_ref(ch[k]);
-            } else {
-                const uint32_t qi = (uint32_t)f.quads.size();
-                f.quads.emplace_back();
-                q.ref[k] = make_interior_ref(quad_base + qi, blas);
-                todo.push_back({ch[k], qi, w.depth + 1});
+            for (uint32_t j = 0; j < 2; j++) {
+                const uint32_t g = t.nodes[c].index + j;
+                t.nodes[g].box.store(b);
+                uint32_t ref;
+                if (is_leaf(g)) {
+                    ref = leaf_ref(g);
+                } else {
+                    const uint32_t qi = (uint32_t)f.quads.size();
+                    f.quads.emplace_back();
+                    ref = make_interior_ref(quad_base + qi, blas);
+                    todo.push_back({g, qi, w.depth + 1});
+                }
+                quad_set_slot(q, 2 * h + j, b, ref);
             }
-            q.pad[k] = 0;
         }
         f.quads[w.quad] = q;
     }

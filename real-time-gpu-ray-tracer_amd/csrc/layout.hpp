@@ -75,16 +75,29 @@ struct alignas(16) NodePair {       // 64 B
 };
 static_assert(sizeof(NodePair) == 64, "NodePair must be 64 B");
 
-// FAST kernel, option "wide": the same trees collapsed to 4 children per interior node (each quad
-// absorbs the largest-area interior children of a binary node until it holds 4), so a ray descends
-// half as many dependent levels.  Child boxes are SoA (one dwordx4 per bound) so the 4 slab tests
-// share each load; an empty slot has every bound = +inf, which no slab test accepts.
+// FAST kernel, option "wide": the same trees collapsed to 4 children per interior node, so a ray
+// descends half as many dependent levels.  The quad of binary node N holds N's two binary levels below
+// it as two halves: slots 0, 1 = the left child's two children, slots 2, 3 = the right child's (a child
+// that is a leaf takes its half's first slot, and the second slot is empty).  The kernel orders the hit
+// slots exactly as the reference's stack would visit them — the halves by their boxes' entry t, then the
+// slots inside a half (push far / visit near per node pair, left on ties: BLAS.cu:186-202,
+// TLAS.cu:182-197) — and a half's box is the union of its two slots' boxes (a node's box is the union of
+// its children's, BLAS.cu:4-117), so its entry t comes from the slots' own slab planes.  Child boxes
+// are SoA (one dwordx4 per bound) so the 4 slab tests share each load; an empty slot carries a copy of
+// its sibling's box (the half's union stays exact) and ref REF_EMPTY, which the kernel never accepts.
 struct alignas(16) NodeQuad {       // 128 B
     float lo_x[4], hi_x[4], lo_y[4], hi_y[4], lo_z[4], hi_z[4];
-    uint32_t ref[4];                // child refs (interior refs index the quad array), REF_NONE = empty
+    uint32_t ref[4];                // child refs (interior refs index the quad array), REF_EMPTY = empty
     uint32_t pad[4];
 };
 static_assert(sizeof(NodeQuad) == 128, "NodeQuad must be 128 B");
+
+// slot k of a quad: box b = {xmin, xmax, ymin, ymax, zmin, zmax}
+__host__ __device__ inline void quad_set_slot(NodeQuad &q, uint32_t k, const float *b, uint32_t ref) {
+    q.lo_x[k] = b[0]; q.hi_x[k] = b[1]; q.lo_y[k] = b[2]; q.hi_y[k] = b[3]; q.lo_z[k] = b[4]; q.hi_z[k] = b[5];
+    q.ref[k] = ref;
+    q.pad[k] = 0;
+}
 
 struct alignas(16) TriHot {         // 48 B: Moller-Trumbore operands (Triangle.cu:4-44)
     float v0[3]; float pad0;            // GPU-built BLASes without cold records (SceneGPU::raw_tris): the caller's

@@ -727,18 +727,32 @@ __global__ void gather_items_kernel(const LbvhSeg *segs, const uint32_t *seg_of,
 }
 
 // ---- 4-wide collapse of a built forest (the quad form the FAST persistent kernel traverses) -------
-// Restates flatten_tree_wide (bvh_build.hpp) on the GPU: a quad starts from an interior node's two
-// children and twice replaces its largest-half-area interior child (first on ties) by that child's two
-// children, so a ray descends half as many dependent levels; leaves and boxes are the binary tree's.  Quad
-// q is the quad rooted at node pair q (pair indices are unique across the forest, so the interior refs the
-// pairs hold are also the quads' refs, and a tree's quad root ref equals its pair root ref).  One
-// workgroup per tree walks it level by level: a frontier of quad roots in LDS (global scratch, this tree's
-// pair range, for trees of more than LDS_FRONT pairs).
+// Restates flatten_tree_wide (bvh_build.hpp) on the GPU: the quad of node pair q holds q's two binary
+// levels as two halves (layout.hpp NodeQuad) — slots 0, 1 = the left child's children, slots 2, 3 = the
+// right child's, a leaf child in its half's first slot and an empty slot with a copy of its box — so a ray
+// descends half as many dependent levels and the kernel still visits the binary tree's order; leaves and
+// boxes are the binary tree's.  Quad q is the quad rooted at node pair q (pair indices are unique across
+// the forest, so the interior refs the pairs hold are also the quads' refs, and a tree's quad root ref
+// equals its pair root ref).  One workgroup per tree walks it level by level: a frontier of quad roots in
+// LDS (global scratch, this tree's pair range, for trees of more than LDS_FRONT pairs).
 constexpr uint32_t LDS_FRONT = 1024;
 
-__device__ __forceinline__ float half_area(const float *b) {
-    const float dx = b[1] - b[0], dy = b[3] - b[2], dz = b[5] - b[4];
-    return dx * dy + dy * dz + dz * dx;
+__device__ __forceinline__ NodeQuad collapse_pair(const NodePair *pairs, uint32_t q) {
+    const NodePair P = pairs[q];
+    NodeQuad Q;
+    for (uint32_t h = 0; h < 2; h++) {
+        const float *b = h ? P.c1 : P.c0;
+        const uint32_t r = h ? P.ref1 : P.ref0;
+        if (r & REF_LEAF) {
+            quad_set_slot(Q, 2 * h, b, r);
+            quad_set_slot(Q, 2 * h + 1, b, REF_EMPTY);
+        } else {
+            const NodePair C = pairs[r & REF_INDEX_MASK];
+            quad_set_slot(Q, 2 * h, C.c0, C.ref0);
+            quad_set_slot(Q, 2 * h + 1, C.c1, C.ref1);
+        }
+    }
+    return Q;
 }
 
 __global__ __launch_bounds__(BLOCK) void collapse_wide_kernel(const LbvhSeg *segs, const TreeRoot *roots, const NodePair *pairs,
@@ -751,7 +765,6 @@ __global__ __launch_bounds__(BLOCK) void collapse_wide_kernel(const LbvhSeg *seg
     if (roots_wide && t == 0) roots_wide[s] = R;              // quad root ref == pair root ref
     if ((R.ref & REF_LEAF) || R.ref == NONE) return;          // a leaf (or empty) tree has no quads
     const uint32_t root = R.ref & REF_INDEX_MASK;
-    const bool blas = (R.ref & REF_BLAS) != 0;
     const uint32_t max_pairs = segs[s].count > 1 ? segs[s].count - 1 : 1;
     uint32_t *front[2];
     if (max_pairs <= LDS_FRONT) { front[0] = lds_front[0]; front[1] = lds_front[1]; }
@@ -766,41 +779,14 @@ __global__ __launch_bounds__(BLOCK) void collapse_wide_kernel(const LbvhSeg *seg
         const uint32_t nc_level = n_cur;
         for (uint32_t i = t; i < nc_level; i += BLOCK) {
             const uint32_t q = front[cur][i];
-            float box[4][6];
-            uint32_t ref[4];
-            const NodePair P = pairs[q];
-#pragma unroll
-            for (int k = 0; k < 6; k++) { box[0][k] = P.c0[k]; box[1][k] = P.c1[k]; }
-            ref[0] = P.ref0; ref[1] = P.ref1;
-            uint32_t nc = 2;
-            while (nc < 4) {
-                int best = -1;
-                float area = -1.0f;
-                for (uint32_t k = 0; k < nc; k++)
-                    if (!(ref[k] & REF_LEAF) && half_area(box[k]) > area) { area = half_area(box[k]); best = (int)k; }
-                if (best < 0) break;
-                const NodePair C = pairs[ref[best] & REF_INDEX_MASK];
-                for (int k = 0; k < 6; k++) { box[best][k] = C.c0[k]; box[nc][k] = C.c1[k]; }
-                ref[best] = C.ref0;
-                ref[nc] = C.ref1;
-                nc++;
-            }
-            NodeQuad Q;
-            for (uint32_t k = 0; k < 4; k++) {
-                const bool used = k < nc;
-                const float inf = __builtin_huge_valf();           // empty slot: rejected by every slab test
-                Q.lo_x[k] = used ? box[k][0] : inf; Q.hi_x[k] = used ? box[k][1] : inf;
-                Q.lo_y[k] = used ? box[k][2] : inf; Q.hi_y[k] = used ? box[k][3] : inf;
-                Q.lo_z[k] = used ? box[k][4] : inf; Q.hi_z[k] = used ? box[k][5] : inf;
-                Q.ref[k] = used ? ref[k] : REF_EMPTY;
-                Q.pad[k] = 0;
-                if (used && !(ref[k] & REF_LEAF)) front[cur ^ 1][atomicAdd(&n_next, 1u)] = ref[k] & REF_INDEX_MASK;
-            }
+            const NodeQuad Q = collapse_pair(pairs, q);
+            for (uint32_t k = 0; k < 4; k++)
+                if (Q.ref[k] != REF_EMPTY && !(Q.ref[k] & REF_LEAF))
+                    front[cur ^ 1][atomicAdd(&n_next, 1u)] = Q.ref[k] & REF_INDEX_MASK;
             float4 *dst = reinterpret_cast<float4 *>(quads + q);
             const float4 *src = reinterpret_cast<const float4 *>(&Q);
 #pragma unroll
             for (int k = 0; k < 8; k++) dst[k] = src[k];
-            (void)blas;
         }
         __syncthreads();
         if (t == 0) { n_cur = n_next; n_next = 0; }
@@ -811,40 +797,12 @@ __global__ __launch_bounds__(BLOCK) void collapse_wide_kernel(const LbvhSeg *seg
 
 // The same quads for forests with a large tree (an instance group's merged BLAS: C5's 10 M triangles in one
 // tree would keep the per-tree kernel's single workgroup walking level by level for ~60 ms): quad q is a pure
-// function of node pair q (its children, the largest-half-area interior one expanded twice), so every pair gets
+// function of node pair q (its children's children, collapse_pair), so every pair gets
 // its quad, one thread each; the quads of pairs absorbed into a parent's quad are written but never reached.
 __global__ void collapse_all_kernel(const NodePair *pairs, const uint32_t *n_pairs, NodeQuad *quads) {
     const uint32_t q = blockIdx.x * BLOCK + threadIdx.x;
     if (q >= *n_pairs) return;
-    float box[4][6];
-    uint32_t ref[4];
-    const NodePair P = pairs[q];
-#pragma unroll
-    for (int k = 0; k < 6; k++) { box[0][k] = P.c0[k]; box[1][k] = P.c1[k]; }
-    ref[0] = P.ref0; ref[1] = P.ref1;
-    uint32_t nc = 2;
-    while (nc < 4) {
-        int best = -1;
-        float area = -1.0f;
-        for (uint32_t k = 0; k < nc; k++)
-            if (!(ref[k] & REF_LEAF) && half_area(box[k]) > area) { area = half_area(box[k]); best = (int)k; }
-        if (best < 0) break;
-        const NodePair C = pairs[ref[best] & REF_INDEX_MASK];
-        for (int k = 0; k < 6; k++) { box[best][k] = C.c0[k]; box[nc][k] = C.c1[k]; }
-        ref[best] = C.ref0;
-        ref[nc] = C.ref1;
-        nc++;
-    }
-    NodeQuad Q;
-    for (uint32_t k = 0; k < 4; k++) {
-        const bool used = k < nc;
-        const float inf = __builtin_huge_valf();
-        Q.lo_x[k] = used ? box[k][0] : inf; Q.hi_x[k] = used ? box[k][1] : inf;
-        Q.lo_y[k] = used ? box[k][2] : inf; Q.hi_y[k] = used ? box[k][3] : inf;
-        Q.lo_z[k] = used ? box[k][4] : inf; Q.hi_z[k] = used ? box[k][5] : inf;
-        Q.ref[k] = used ? ref[k] : REF_EMPTY;
-        Q.pad[k] = 0;
-    }
+    const NodeQuad Q = collapse_pair(pairs, q);
     float4 *dst = reinterpret_cast<float4 *>(quads + q);
     const float4 *src = reinterpret_cast<const float4 *>(&Q);
 #pragma unroll
@@ -1048,34 +1006,7 @@ __global__ __launch_bounds__(SMALL_BLOCK) void tlas_small_kernel(SmallTlasArgs a
     // 6. quads (collapse_all_kernel) and the records in leaf-slot order (slot_order_kernel)
     const uint32_t npairs = *a.pair_count;
     for (uint32_t q = t; q < npairs; q += SMALL_BLOCK) {
-        float box[4][6];
-        uint32_t ref[4];
-        const NodePair P = a.pairs[q];
-        for (int k = 0; k < 6; k++) { box[0][k] = P.c0[k]; box[1][k] = P.c1[k]; }
-        ref[0] = P.ref0; ref[1] = P.ref1;
-        uint32_t nc = 2;
-        while (nc < 4) {
-            int best = -1;
-            float area = -1.0f;
-            for (uint32_t k = 0; k < nc; k++)
-                if (!(ref[k] & REF_LEAF) && half_area(box[k]) > area) { area = half_area(box[k]); best = (int)k; }
-            if (best < 0) break;
-            const NodePair Cn = a.pairs[ref[best] & REF_INDEX_MASK];
-            for (int k = 0; k < 6; k++) { box[best][k] = Cn.c0[k]; box[nc][k] = Cn.c1[k]; }
-            ref[best] = Cn.ref0;
-            ref[nc] = Cn.ref1;
-            nc++;
-        }
-        NodeQuad Q;
-        for (uint32_t k = 0; k < 4; k++) {
-            const bool used = k < nc;
-            const float inf = __builtin_huge_valf();
-            Q.lo_x[k] = used ? box[k][0] : inf; Q.hi_x[k] = used ? box[k][1] : inf;
-            Q.lo_y[k] = used ? box[k][2] : inf; Q.hi_y[k] = used ? box[k][3] : inf;
-            Q.lo_z[k] = used ? box[k][4] : inf; Q.hi_z[k] = used ? box[k][5] : inf;
-            Q.ref[k] = used ? ref[k] : REF_EMPTY;
-            Q.pad[k] = 0;
-        }
+        const NodeQuad Q = collapse_pair(a.pairs, q);
         a.quads[q] = Q;
     }
     for (uint32_t k = t; k < m; k += SMALL_BLOCK) {

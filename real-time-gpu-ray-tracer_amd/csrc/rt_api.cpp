@@ -41,18 +41,18 @@ hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, co
 hipError_t launch_frame_copy(void *, const void *, size_t, unsigned long long *, uint32_t *, hipStream_t);
 hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t,
                            uint32_t, uint32_t, void *, const void *, size_t, unsigned long long *, hipStream_t);
-uint32_t persistent_blocks_per_cu_exact(uint32_t variant, bool wide);
+uint32_t persistent_blocks_per_cu_exact(uint32_t variant, uint32_t wide, bool raw);
 hipError_t launch_instance_slot_order(const uint32_t *, const InstHot *, const InstCold *, uint32_t, InstHot *, InstCold *,
                                       hipStream_t);
 hipError_t launch_instance_update(const InstDelta *, uint32_t, InstParams *, uint32_t, InstHot *, InstCold *, float *, float4 *,
                                   const uint32_t *, const TreeRoot *, const uint32_t *, bool, hipStream_t);
-uint32_t persistent_blocks_per_cu_fast(uint32_t variant, bool wide);
+uint32_t persistent_blocks_per_cu_fast(uint32_t variant, uint32_t wide, bool raw);
 // option "fast_math": the FAST kernels compiled with hardware reciprocals and FMA contraction (trace_fastmath.o)
 hipError_t launch_render_fastmath(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *, hipStream_t);
 hipError_t launch_trace_rays_fastmath(const SceneGPU &, const float *, uint32_t, rt_hit *, hipStream_t);
 hipError_t launch_render_persistent_fastmath(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
                                              uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
-uint32_t persistent_blocks_per_cu_fastmath(uint32_t variant, bool wide);
+uint32_t persistent_blocks_per_cu_fastmath(uint32_t variant, uint32_t wide, bool raw);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -223,6 +223,8 @@ struct rt_scene {
     static_assert(NLANE <= 8, "inst_dirty holds one bit per frame block");
     hipStream_t chain_stream[NLANE] = {};         // GPU-built frame b's records / TLAS were built on this stream
     hipEvent_t ev_blas_built = nullptr;           // the last GPU BLAS build on the scene stream finished
+    hipEvent_t ev_caller = nullptr;               // rt_render with device outputs and no stream: the null stream's
+                                                  // work before the call (the trace writes the caller's buffers after it)
     uint64_t blas_build_seq = 0;                  // BLAS builds recorded on ev_blas_built so far
     uint64_t blas_build_done = 0;                 // ... of which the host has seen the last one complete
     // pinned host staging, cycled independently of the frame blocks and twice as deep: a frame's staging is
@@ -262,7 +264,9 @@ struct rt_scene {
     uint32_t *queue[NLANE] = {};
     bool overlap = false;
     uint32_t blas_leaf = SAH_LEAF_CAP;   // option "blas_leaf": RT_BUILD_SAH BLAS leaf size (1..4), next rt_scene_build
-    uint32_t tlas_leaf = 1;   // option "tlas_leaf": RT_BUILD_SAH per-frame TLAS leaf size (1..4; 1 measured best)
+    uint32_t tlas_leaf = 1;   // option "tlas_leaf": RT_BUILD_SAH per-frame SAH TLAS leaf size (1..4; 1 measured best)
+    uint32_t tlas_median_leaf = 0;   // option "tlas_median_leaf": RT_BUILD_SAH median TLAS leaf size (0 = the reference's 2)
+    bool tlas_sah = true;     // option "tlas_sah": RT_BUILD_SAH builds its per-frame TLAS with SAH (0: the median split)
     bool inst_by_slot = true;       // option "inst_by_slot": host-built TLAS stages instance records in slot order
     bool block_by_slot[NLANE] = {};  // per frame block: staged in slot order
     uint32_t lanes = 1;
@@ -387,6 +391,9 @@ struct rt_scene {
     DevBuf<uint32_t> blas_wide_refs;    // host-built BLASes under a GPU TLAS: quad root ref per BLAS
     // instance records + TLAS built by kernels each frame: RT_BUILD_LBVH, or RT_BUILD_SAH with "gpu_tlas"
     bool gpu_tlas() const { return build_mode == RT_BUILD_LBVH || (gpu_tlas_sah && build_mode == RT_BUILD_SAH); }
+    // quads of two binary levels visited in the reference's order (layout.hpp NodeQuad): the reference's own trees and
+    // GPU-built ones; host SAH trees keep the greedy collapse visited by entry t
+    bool quad_halves() const { return build_mode != RT_BUILD_SAH; }
 
     CommState *comm = nullptr;             // multi-GPU frame (rt_scene_attach_comm)
     uint32_t comm_timeout_ms = 0;          // rt_comm_set_timeout (kept across attach / detach)
@@ -445,6 +452,7 @@ struct rt_scene {
                 if (sp.ev_lane[q]) (void)hipEventDestroy(sp.ev_lane[q]);
         }
         if (ev_render_done) (void)hipEventDestroy(ev_render_done);
+        if (ev_caller) (void)hipEventDestroy(ev_caller);
         if (ev_blas_built) (void)hipEventDestroy(ev_blas_built);
         if (ev_raw_staged) (void)hipEventDestroy(ev_raw_staged);
         if (raw_stage) (void)hipHostFree(raw_stage);
@@ -750,10 +758,21 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         if (!s->group_of[i] || !intact[s->group_of[i] - 1]) items.push_back({s->inst[i].tbox, s->inst[i].tcentroid, (uint32_t)i});
     for (size_t g = 0; g < s->groups.size(); g++)
         if (intact[g]) items.push_back({s->groups[g].st.tbox, s->groups[g].st.tcentroid, (uint32_t)(s->inst.size() + g)});
-    s->tlas = s->build_mode == RT_BUILD_SAH ? build_sah_tree(std::move(items), s->tlas_leaf)
-                                            : build_median_tree(std::move(items), TLAS_LEAF_CAP, hm::tlas_axis_state(s->build_seed, frame));
+    // RT_BUILD_SAH builds an SAH TLAS (option "tlas_sah" 0: the reference's median split, TLAS.cu:4-129).  The TLAS
+    // decides the order in which instances are visited, and with the parallelogram's q-centred box
+    // (Parallelogram.cu:48-50) that order is visible: a ray that hits the parallelogram outside its box keeps the hit
+    // only when the box is tested before a farther surface shrinks the range.  The reference's median trees test the
+    // ground sphere first for the demo's view (a subtree holding it and anything above the camera contains the camera,
+    // so its entry is t_min); an SAH TLAS isolates the ground at the root, and visited by entry t (the SAH scenes'
+    // quad order) it tests the ground first too — in the reference's pair order it would not (303 of C2's pixels at
+    // depth 1; profiles/r05/order/).
+    s->tlas = s->build_mode == RT_BUILD_SAH && s->tlas_sah
+                  ? build_sah_tree(std::move(items), s->tlas_leaf)
+                  : build_median_tree(std::move(items),
+                                      s->build_mode == RT_BUILD_SAH && s->tlas_median_leaf ? s->tlas_median_leaf : TLAS_LEAF_CAP,
+                                      hm::tlas_axis_state(s->build_seed, frame));
     s->tlas_flat = flatten_tree(s->tlas, 0, 0, 0, false);
-    s->tlas_wide = flatten_tree_wide(s->tlas, 0, 0, 0, false, s->wide_merge);
+    s->tlas_wide = flatten_tree_wide(s->tlas, 0, 0, 0, false, s->quad_halves(), s->wide_merge);
 
     TreeRoot root{};
     std::memcpy(root.box, s->tlas_flat.root_box, sizeof root.box);
@@ -807,7 +826,9 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.tlas_root_wide = reinterpret_cast<const TreeRoot *>(s->frame_dev[b] + s->off_root_wide);
     g.tlas_quads = reinterpret_cast<const NodeQuad *>(s->frame_dev[b] + s->off_quads);
     g.blas_quads = s->blas_quads.p;
-    g.wide = s->wide && s->blas_quads.p != nullptr ? 1u : 0u;   // GPU-built trees: quads from collapse_wide
+    // quad trees (GPU-built: from collapse_wide): 2 = two binary levels per quad visited in the reference's order (the
+    // reference's own trees and GPU-built ones), 1 = host SAH BLASes collapsed greedily, visited by entry t
+    g.wide = s->wide && s->blas_quads.p != nullptr ? (s->quad_halves() ? 2u : 1u) : 0u;
     g.tlas_slots = reinterpret_cast<const uint32_t *>(s->frame_dev[b] + s->off_slots);
     const bool gpu_slots = s->gpu_tlas() && s->block_by_slot[b];   // the slot-ordered copies of GPU-built frames
     g.inst_hot = reinterpret_cast<const InstHot *>(s->frame_dev[b] + (gpu_slots ? s->off_hot_s : s->off_hot));
@@ -1212,7 +1233,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             if ((uint64_t)slot_base[in.ptype] + in.pcount >= MAX_LEAF_SLOTS)
                 return fail(RT_ERR_UNSUPPORTED, "too many primitives of one type (2^26 leaf slots)");
             bh.flat = flatten_tree(bh.tree, pair_base, bh.slot_base, in.ptype, true);
-            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, in.ptype, true, s->wide_merge);
+            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, in.ptype, true, s->quad_halves(), s->wide_merge);
             quad_base += (uint32_t)bh.wide.quads.size();
             s->max_blas_height = std::max(s->max_blas_height, bh.flat.height);
             pair_base += (uint32_t)bh.flat.pairs.size();
@@ -1296,7 +1317,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             bh.pair_base = pair_base;
             bh.slot_base = slot_base[RT_PRIM_TRIANGLE];
             bh.flat = flatten_tree(bh.tree, pair_base, bh.slot_base, RT_PRIM_TRIANGLE, true);
-            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, RT_PRIM_TRIANGLE, true, s->wide_merge,
+            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, RT_PRIM_TRIANGLE, true, s->quad_halves(), s->wide_merge,
                                         /*level_order=*/true);
             quad_base += (uint32_t)bh.wide.quads.size();
             s->max_blas_height = std::max(s->max_blas_height, bh.flat.height);
@@ -1716,9 +1737,9 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         out.grab = s->grab;
         out.supertile = s->supertile;
         if (s->timeline_on) {
-            const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false)
-                                                    : (s->fast_math ? persistent_blocks_per_cu_fastmath(s->variant, g.wide != 0)
-                                                                   : persistent_blocks_per_cu_fast(s->variant, g.wide != 0)));
+            const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, 0u, false)
+                                                    : (s->fast_math ? persistent_blocks_per_cu_fastmath(s->variant, g.wide, g.raw_tris != nullptr)
+                                                                   : persistent_blocks_per_cu_fast(s->variant, g.wide, g.raw_tris != nullptr)));
             const size_t words = (size_t)blocks * 4 * TIMELINE_WORDS;
             if (s->timeline.n < words) {
                 s->timeline.release();
@@ -1743,6 +1764,16 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     s->lane = s->overlap ? (s->lane + 1) % s->lanes : 0u;
     s->last_lane = q;
     if (hipEvent_t prev = s->overlap ? s->r_lane[q] : s->r_done) HIP_TRY(hipStreamWaitEvent(stream, prev, 0));
+    // Device outputs and no stream: the trace runs on the scene's non-blocking stream, which HIP does not order with
+    // the caller's null-stream work, so it waits for what the caller enqueued there before the call (e.g. a fill of
+    // the buffer) and the null stream waits for the frame (a read of it after the call).  The reference draws into
+    // a surface it owns on its own stream (Renderer.cu:305-317), so a drop-in caller expects no ordering of its own.
+    const bool order_null = !o.stream && (o.rgba8_device || o.rgb32_device);
+    if (order_null) {
+        if (!s->ev_caller) HIP_TRY(hipEventCreateWithFlags(&s->ev_caller, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(s->ev_caller, nullptr));
+        HIP_TRY(hipStreamWaitEvent(stream, s->ev_caller, 0));
+    }
     unsigned long long *lane_counters = s->counters + (size_t)q * CNT_NUM;   // only this lane's launches add here
     if (!(o.flags & RT_RENDER_KEEP_COUNTERS)) s->cnt_epoch++;
     bool zero_lane = s->lane_epoch[q] != s->cnt_epoch;                      // cleared before this launch
@@ -1831,9 +1862,9 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     s->last_stream = stream;
     HIP_TRY(hipEventRecord(s->ring_start[slot], stream));
     if (s->use_persistent) {
-        const uint32_t cap = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, false)
-                                             : (s->fast_math ? persistent_blocks_per_cu_fastmath(s->variant, g.wide != 0)
-                                                            : persistent_blocks_per_cu_fast(s->variant, g.wide != 0)));
+        const uint32_t cap = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, 0u, false)
+                                             : (s->fast_math ? persistent_blocks_per_cu_fastmath(s->variant, g.wide, g.raw_tris != nullptr)
+                                                            : persistent_blocks_per_cu_fast(s->variant, g.wide, g.raw_tris != nullptr)));
         uint32_t blocks = s->overlap && cap > 2 * s->reserve ? cap - s->reserve : cap;
         uint32_t pct = s->grid_pct;
         if (pct == 0) {
@@ -1893,6 +1924,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     s->r_used[s->active] = s->r_done = s->r_lane[q] = done;
     if (copied_block >= 0) s->r_copied[copied_block] = s->r_staged[copied_stage] = done;
     if (s->ev_blas_lane[q]) HIP_TRY(hipEventRecord(s->ev_blas_lane[q], stream));   // "blas_double": this set's reader
+    if (order_null) HIP_TRY(hipStreamWaitEvent(nullptr, done, 0));
     if (o.flags & RT_RENDER_NO_SYNC) {
         if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; stats->update_wait_ms = s->update_wait_ms; }
         return RT_OK;
@@ -1939,7 +1971,16 @@ rt_status rt_assemble_tiles(rt_scene *s, const void *gathered, uint32_t slab_til
     if (((uintptr_t)gathered | (uintptr_t)frame) & 3u) return fail(RT_ERR_INVALID_ARGUMENT, "RGBA8 buffers must be 4-byte aligned");
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t st = stream ? static_cast<hipStream_t>(stream) : s->stream;
+    if (!stream) {                             // caller buffers on the scene's stream: ordered with the null stream
+        if (!s->ev_caller) HIP_TRY(hipEventCreateWithFlags(&s->ev_caller, hipEventDisableTiming));   // (rt_render)
+        HIP_TRY(hipEventRecord(s->ev_caller, nullptr));
+        HIP_TRY(hipStreamWaitEvent(st, s->ev_caller, 0));
+    }
     HIP_TRY(launch_assemble(gathered, slab_tiles, tw, th, tile_count, s->width, s->height, frame, st));
+    if (!stream) {
+        HIP_TRY(hipEventRecord(s->ev_caller, st));
+        HIP_TRY(hipStreamWaitEvent(nullptr, s->ev_caller, 0));
+    }
     return RT_OK;
 }
 
@@ -2067,6 +2108,11 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "blas_leaf") {
         if (value < 1 || value > (int64_t)SAH_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "blas_leaf must be in 1..4");
         s->blas_leaf = (uint32_t)value;
+    } else if (k == "tlas_median_leaf") {
+        if (value < 0 || value > (int64_t)TLAS_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_median_leaf must be 0..2");
+        s->tlas_median_leaf = (uint32_t)value;
+    } else if (k == "tlas_sah") {
+        s->tlas_sah = value != 0;                 // next frame's TLAS
     } else if (k == "tlas_leaf") {
         if (value < 1 || value > (int64_t)SAH_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_leaf must be in 1..4");
         s->tlas_leaf = (uint32_t)value;          // next frame's TLAS

@@ -606,9 +606,13 @@ __device__ __forceinline__ void pop_next(Trav &T, const SEnt *spill) {
 
 // One interior-loop step of a lane whose cur is an interior node, or a leaf to postpone.
 #if !RT_EXACT
-// Quad node (option "wide"): 4 slab tests on SoA bounds, hits sorted by entry t; the nearest is visited
-// next and the others are pushed farthest first (popped nearest first).  Not the reference's visit
-// order (FAST tolerance): the closest hit only differs on ties within the 1e-6 window.
+// Quad node (option "wide", layout.hpp NodeQuad): 4 slab tests on SoA bounds; the hit slots are visited
+//   PAIR (quads of two binary levels: the reference's trees, GPU-built trees): in the reference's order — the two
+//     halves (binary children) by their boxes' entry t, then the slots of a half by theirs, the nearer first and the
+//     left one on ties (BLAS.cu:186-202, TLAS.cu:182-197) — so the closest hit is the reference's, ties included;
+//   else (host SAH trees, collapsed greedily): by entry t, nearest first (measured against the oracle: DESIGN §3.4).
+// The first is visited next and the others pushed last-first, each with its own entry t for the pop re-test (a
+// half's box holds its slots' boxes, so its re-test passes whenever one of theirs does).
 // Option "lds_scene" (SceneGPU::lds_quads / lds_insts): the frame's TLAS quads and instance hot records,
 // copied into LDS by every workgroup of the persistent quad-tree kernel at its start.  On C2 an average
 // ray visits ~1.6 quads (mostly TLAS) and enters ~1 instance, so most of its dependent loads are these.
@@ -670,13 +674,23 @@ __device__ __forceinline__ R lds_or_global(uint32_t at, const R *g, uint32_t k) 
     return r;
 }
 
-__device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float oinv, float4 &tn, float4 &tf) {
+// one axis of the 4 slot slab tests; pa / pb: that axis's contribution to the entry t of the halves' boxes (a
+// half's box is the union of its two slots' boxes, and the plane distances are monotone in the bound, so its near
+// plane is the nearer of its slots' near planes)
+template <bool PAIR>
+__device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float oinv, float4 &tn, float4 &tf,
+                                      float &pa, float &pb) {
     const float a0 = fmaf(lo.x, inv, -oinv), b0 = fmaf(hi.x, inv, -oinv);
     const float a1 = fmaf(lo.y, inv, -oinv), b1 = fmaf(hi.y, inv, -oinv);
     const float a2 = fmaf(lo.z, inv, -oinv), b2 = fmaf(hi.z, inv, -oinv);
     const float a3 = fmaf(lo.w, inv, -oinv), b3 = fmaf(hi.w, inv, -oinv);
-    tn = make_float4(fmaxf(tn.x, fminf(a0, b0)), fmaxf(tn.y, fminf(a1, b1)), fmaxf(tn.z, fminf(a2, b2)), fmaxf(tn.w, fminf(a3, b3)));
+    const float n0 = fminf(a0, b0), n1 = fminf(a1, b1), n2 = fminf(a2, b2), n3 = fminf(a3, b3);
+    tn = make_float4(fmaxf(tn.x, n0), fmaxf(tn.y, n1), fmaxf(tn.z, n2), fmaxf(tn.w, n3));
     tf = make_float4(fminf(tf.x, fmaxf(a0, b0)), fminf(tf.y, fmaxf(a1, b1)), fminf(tf.z, fmaxf(a2, b2)), fminf(tf.w, fmaxf(a3, b3)));
+    if (PAIR) {
+        pa = fmaxf(pa, fminf(n0, n1));
+        pb = fmaxf(pb, fminf(n2, n3));
+    }
 }
 __device__ __forceinline__ void cswap(float &ta, uint32_t &ra, float &tb, uint32_t &rb) {
     const bool sw = tb < ta;
@@ -684,7 +698,7 @@ __device__ __forceinline__ void cswap(float &ta, uint32_t &ra, float &tb, uint32
     const uint32_t r = sw ? rb : ra, q = sw ? ra : rb;
     ta = t; tb = u; ra = r; rb = q;
 }
-template <bool COUNT>
+template <bool COUNT, bool PAIR>
 __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
     const uint32_t cur = T.cur;
     const bool blas = (cur & REF_BLAS) != 0;
@@ -708,11 +722,12 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
     const RayP &r = blas ? T.lr : T.wr;
     float t[4];
     bool h[4];
+    float pa = TMIN, pb = TMIN;                      // entry t of the two halves' boxes
     {
         float4 tn = make_float4(TMIN, TMIN, TMIN, TMIN), tf = make_float4(T.tmax, T.tmax, T.tmax, T.tmax);
-        slab4(lx, hx, r.inv.x, r.oinv.x, tn, tf);
-        slab4(ly, hy, r.inv.y, r.oinv.y, tn, tf);
-        slab4(lz, hz, r.inv.z, r.oinv.z, tn, tf);
+        slab4<PAIR>(lx, hx, r.inv.x, r.oinv.x, tn, tf, pa, pb);
+        slab4<PAIR>(ly, hy, r.inv.y, r.oinv.y, tn, tf, pa, pb);
+        slab4<PAIR>(lz, hz, r.inv.z, r.oinv.z, tn, tf, pa, pb);
         t[0] = tn.x; t[1] = tn.y; t[2] = tn.z; t[3] = tn.w;
 #if RT_SLAB_CONS
         h[0] = cons_lo(tn.x, r.pad) < cons_hi(tf.x, r.pad); h[1] = cons_lo(tn.y, r.pad) < cons_hi(tf.y, r.pad);
@@ -721,40 +736,79 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
         h[0] = tn.x < tf.x; h[1] = tn.y < tf.y; h[2] = tn.z < tf.z; h[3] = tn.w < tf.w;
 #endif
     }
-    float t0 = h[0] ? t[0] : __builtin_huge_valf(), t1 = h[1] ? t[1] : __builtin_huge_valf();
-    float t2 = h[2] ? t[2] : __builtin_huge_valf(), t3 = h[3] ? t[3] : __builtin_huge_valf();
-    uint32_t r0 = R.x, r1 = R.y, r2 = R.z, r3 = R.w;
-    const uint32_t nh = (uint32_t)h[0] + (uint32_t)h[1] + (uint32_t)h[2] + (uint32_t)h[3];
-    if (nh == 0) { pop_next(T, spill); return; }
-    // sort the 4 (t, ref) ascending; misses (t = inf) sink to the end
-    cswap(t0, r0, t1, r1); cswap(t2, r2, t3, r3); cswap(t0, r0, t2, r2); cswap(t1, r1, t3, r3); cswap(t1, r1, t2, r2);
-    // the 1..3 far hits go to the three LDS slots above the top without branching on their count
-    // (farthest first; the slots past the new top are free space), after one page-out check
-    if (nh > 1) {
+    // an empty slot repeats its sibling's box (the half's union stays exact) and is never accepted
+    h[1] = h[1] && R.y != REF_EMPTY;
+    h[3] = h[3] && R.w != REF_EMPTY;
+    const float inf = __builtin_huge_valf();
+    if (!PAIR) {
+        float t0 = h[0] ? t[0] : inf, t1 = h[1] ? t[1] : inf, t2 = h[2] ? t[2] : inf, t3 = h[3] ? t[3] : inf;
+        uint32_t r0 = R.x, r1 = R.y, r2 = R.z, r3 = R.w;
+        const uint32_t nh = (uint32_t)h[0] + (uint32_t)h[1] + (uint32_t)h[2] + (uint32_t)h[3];
+        if (nh == 0) { pop_next(T, spill); return; }
+        // sort the 4 (t, ref) ascending; misses (t = inf) sink to the end
+        cswap(t0, r0, t1, r1); cswap(t2, r2, t3, r3); cswap(t0, r0, t2, r2); cswap(t1, r1, t3, r3); cswap(t1, r1, t2, r2);
+        // the 1..3 far hits go to the three LDS slots above the top without branching on their count (farthest
+        // first; the slots past the new top are free space), after one page-out check
+        if (nh > 1) {
+            if (T.stk.sp > LDS_DEPTH - 3) stack_page_out3(T.stk, spill, cnt);
+            SEnt a, b, c;
+            a.ref = nh == 4 ? r3 : (nh == 3 ? r2 : r1);
+            a.tn = __float_as_uint(nh == 4 ? t3 : (nh == 3 ? t2 : t1));
+            b.ref = nh == 4 ? r2 : r1;
+            b.tn = __float_as_uint(nh == 4 ? t2 : t1);
+            c.ref = r1;
+            c.tn = __float_as_uint(t1);
+            T.stk.lds[T.stk.sp * BLOCK] = pack(a);
+            T.stk.lds[(T.stk.sp + 1) * BLOCK] = pack(b);
+            T.stk.lds[(T.stk.sp + 2) * BLOCK] = pack(c);
+            T.stk.sp += (int)nh - 1;
+        }
+        T.cur = r0;
+        T.curT = t0;
+        return;
+    }
+    const uint32_t na = (uint32_t)h[0] + (uint32_t)h[1], nb = (uint32_t)h[2] + (uint32_t)h[3];
+    if (na + nb == 0) { pop_next(T, spill); return; }
+    // The reference's visit order (BLAS.cu:186-202: push far, visit near, the right child first iff tLeft > tRight):
+    // inside each half its two slots, then the halves by their boxes' entry t.  A missed slot counts as t = +inf, so
+    // it is second in its half, and a half without hits goes second; the hits then come first in each half.
+    const float u0 = h[0] ? t[0] : inf, u1 = h[1] ? t[1] : inf, u2 = h[2] ? t[2] : inf, u3 = h[3] ? t[3] : inf;
+    const bool sa = u0 > u1, sb = u2 > u3;
+    const float a0t = sa ? u1 : u0, a1t = sa ? u0 : u1, b0t = sb ? u3 : u2, b1t = sb ? u2 : u3;
+    const uint32_t a0r = sa ? R.y : R.x, a1r = sa ? R.x : R.y, b0r = sb ? R.w : R.z, b1r = sb ? R.z : R.w;
+    const bool sr = na == 0 || (nb != 0 && pa > pb);                 // the right half first
+    const float n0t = sr ? b0t : a0t, n1t = sr ? b1t : a1t, f0t = sr ? a0t : b0t, f1t = sr ? a1t : b1t;
+    const uint32_t n0r = sr ? b0r : a0r, n1r = sr ? b1r : a1r, f0r = sr ? a0r : b0r, f1r = sr ? a1r : b1r;
+    const uint32_t nn = sr ? nb : na, nf = sr ? na : nb;             // hits in the near / far half (nn >= 1)
+    // the near half's first hit is visited next; the rest go to the three LDS slots above the top, deepest first
+    // (far half's second, its first, the near half's second), without branching on their count, after one
+    // page-out check
+    const uint32_t npush = nn - 1u + nf;
+    if (npush > 0) {
         if (T.stk.sp > LDS_DEPTH - 3) stack_page_out3(T.stk, spill, cnt);
         SEnt a, b, c;
-        a.ref = nh == 4 ? r3 : (nh == 3 ? r2 : r1);
-        a.tn = __float_as_uint(nh == 4 ? t3 : (nh == 3 ? t2 : t1));
-        b.ref = nh == 4 ? r2 : r1;
-        b.tn = __float_as_uint(nh == 4 ? t2 : t1);
-        c.ref = r1;
-        c.tn = __float_as_uint(t1);
+        a.ref = nf == 2 ? f1r : (nf == 1 ? f0r : n1r);
+        a.tn = __float_as_uint(nf == 2 ? f1t : (nf == 1 ? f0t : n1t));
+        b.ref = nf == 2 ? f0r : n1r;
+        b.tn = __float_as_uint(nf == 2 ? f0t : n1t);
+        c.ref = n1r;
+        c.tn = __float_as_uint(n1t);
         T.stk.lds[T.stk.sp * BLOCK] = pack(a);
         T.stk.lds[(T.stk.sp + 1) * BLOCK] = pack(b);
         T.stk.lds[(T.stk.sp + 2) * BLOCK] = pack(c);
-        T.stk.sp += (int)nh - 1;
+        T.stk.sp += (int)npush;
     }
-    T.cur = r0;
-    T.curT = t0;
+    T.cur = n0r;
+    T.curT = n0t;
 }
 #endif
 
-template <bool COUNT, bool WIDE = false>
+template <bool COUNT, int WIDE = 0>
 __device__ __forceinline__ void spec_interior_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
     const uint32_t cur = T.cur;
 #if !RT_EXACT
     if (WIDE) {
-        if (!(cur & REF_LEAF)) wide_interior_step<COUNT>(T, sc, spill, cnt);
+        if (!(cur & REF_LEAF)) wide_interior_step<COUNT, WIDE == 2>(T, sc, spill, cnt);
         else { T.pleaf = cur; pop_next(T, spill); }        // postpone, keep walking
         return;
     }
@@ -804,7 +858,7 @@ __device__ __forceinline__ void spec_interior_step(Trav &T, const SceneGPU &sc, 
 // after the tests.  A segment against the demo's spheres / parallelogram then takes one round, not two.
 // Returns 1 when a root leaf was chained (it counts as a step of its own in the unit costs, so the
 // claim order's cost classes keep the scale they were tuned on).
-template <bool COUNT, bool WIDE = false>
+template <bool COUNT, int WIDE = 0>
 __device__ __forceinline__ uint32_t spec_leaf_phase(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
     uint32_t leaf = T.pleaf;
     bool chained = false;
@@ -928,7 +982,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 
 // One round: interior loop until every traversing lane holds a leaf, then the leaf phase.
 // steps (when `track`): the lane's interior steps + leaf phases, the pixel's cost for the work order
-template <bool COUNT, bool WIDE = false>
+template <bool COUNT, int WIDE = 0>
 __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt,
                                            PhaseCycles &pc, uint32_t &steps, bool track) {
     DIAG_T(t0);
@@ -1281,7 +1335,7 @@ __device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t
     }
 }
 
-template <bool COUNT, bool WIDE, int RAW>
+template <bool COUNT, int WIDE, int RAW>
 __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out,
                                                        uint32_t *queue, uint32_t threshold, unsigned long long *counters) {
     __shared__ unsigned long long lds_stack[LDS_DEPTH][BLOCK];
@@ -1294,7 +1348,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     if constexpr (WIDE) lds_scene_fill(sc);
 #endif
     __syncthreads();                              // once, before any wave leaves for the queue
-    const TreeRoot root = uniform_root<WIDE>(sc);
+    const TreeRoot root = uniform_root<WIDE != 0>(sc);
 
     Trav T;
     T.stk.lds = (LdsU2 *)&lds_stack[0][tid];
@@ -1445,7 +1499,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             f3 no = T.wr.o, nd = T.wr.d;                                     // next segment
             if (T.found) {
                 if (COUNT) cnt.hits++;
-                const Surface s = finalize<WIDE, RAW>(sc, T.wr.o, T.wr.d, T.hit);
+                const Surface s = finalize<WIDE != 0, RAW>(sc, T.wr.o, T.wr.d, T.hit);
                 DIAG_WAIT_VM();
                 DIAG_T(t_hit);
                 const uint32_t mi = s.material & ~MAT_METAL_BIT;
@@ -1550,7 +1604,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
 }
 
 // Register budget variants: WPE = minimum waves per SIMD the compiler must allow (0 = its choice).
-template <bool COUNT, int WPE, bool WIDE = false, int RAW = 2>
+template <bool COUNT, int WPE, int WIDE = 0, int RAW = 2>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(WPE > 0 ? WPE : 1)))
 void render_persistent_kernel(SceneGPU sc, CameraGPU cam, OutputGPU out, uint32_t *queue, uint32_t threshold,
                               unsigned long long *counters) {
@@ -1600,7 +1654,7 @@ hipError_t RT_SUFFIX(launch_render)(const SceneGPU &sc, const CameraGPU &cam, co
 }
 
 namespace {
-template <int WPE, bool WIDE = false, int RAW = 2>
+template <int WPE, int WIDE = 0, int RAW = 2>
 hipError_t launch_persistent_wpe(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
                                  unsigned long long *counters, uint32_t *queue, uint32_t blocks_per_cu_cus,
                                  uint32_t threshold, hipStream_t stream) {
@@ -1613,11 +1667,11 @@ hipError_t launch_persistent_wpe(const SceneGPU &sc, const CameraGPU &cam, const
         hipLaunchKernelGGL((render_persistent_kernel<false, WPE, WIDE, RAW>), grid, dim3(BLOCK), 0, stream, sc, cam, out, queue, threshold, counters);
     return hipGetLastError();
 }
-template <int WPE, bool WIDE = false>
+template <int WPE, int WIDE = 0, int RAW = 2>
 uint32_t blocks_per_cu_wpe() {
     using namespace RT_SUFFIX(dev);
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false, WPE, WIDE, (WIDE ? 0 : 2)>, BLOCK, 0) != hipSuccess) return 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, render_persistent_kernel<false, WPE, WIDE, RAW>, BLOCK, 0) != hipSuccess) return 1;
     return n > 0 ? (uint32_t)n : 1u;
 }
 #if RT_EXACT
@@ -1636,10 +1690,16 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
         const hipError_t e = hipMemsetAsync(queue, 0, QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
     }
-    if (sc.wide && HAS_WIDE) {              // quad trees: one instance per scene kind (finalize's RAW)
+    // quad trees: one instance per scene kind — visit order (SceneGPU::wide 1 = by entry t, 2 = the binary tree's)
+    // and where a hit triangle's shading data lives (finalize's RAW; GPU-built trees are always in pair order)
+    if (sc.wide && HAS_WIDE) {
         if (sc.raw_tris) {
-            if (variant == 4) return launch_persistent_wpe<4, HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-            return launch_persistent_wpe<3, HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+            if (variant == 4) return launch_persistent_wpe<4, 2 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+            return launch_persistent_wpe<3, 2 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+        }
+        if (sc.wide == 2) {
+            if (variant == 4) return launch_persistent_wpe<4, 2 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+            return launch_persistent_wpe<3, 2 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
         }
         if (variant == 4) return launch_persistent_wpe<4, HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
         return launch_persistent_wpe<3, HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
@@ -1648,12 +1708,16 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
     return launch_persistent_wpe<0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
 }
 
-uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, bool wide) {
-    if (wide && HAS_WIDE) return variant == 4 ? blocks_per_cu_wpe<4, HAS_WIDE>() : blocks_per_cu_wpe<3, HAS_WIDE>();   // (RAW 0; 1 has the same budget)
+// the occupancy of the instance launch_render_persistent runs for (wide, raw): the persistent grid is sized from it
+uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, uint32_t wide, bool raw) {
+    if (wide && HAS_WIDE) {
+        if (raw) return variant == 4 ? blocks_per_cu_wpe<4, 2 * HAS_WIDE, 1>() : blocks_per_cu_wpe<3, 2 * HAS_WIDE, 1>();
+        if (wide == 2) return variant == 4 ? blocks_per_cu_wpe<4, 2 * HAS_WIDE, 0>() : blocks_per_cu_wpe<3, 2 * HAS_WIDE, 0>();
+        return variant == 4 ? blocks_per_cu_wpe<4, HAS_WIDE, 0>() : blocks_per_cu_wpe<3, HAS_WIDE, 0>();
+    }
     if (variant == 4) return blocks_per_cu_wpe<4>();
     return blocks_per_cu_wpe<0>();
 }
-
 hipError_t RT_SUFFIX(launch_trace_rays)(const SceneGPU &sc, const float *rays, uint32_t n, rt_hit *hits,
                                         hipStream_t stream) {
     using namespace RT_SUFFIX(dev);

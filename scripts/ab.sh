@@ -1,7 +1,8 @@
 #!/bin/bash
 # A/B of one scene option on bench lines (interleaved runs in one call).
-# usage: OPT=name [VALS="0 1"] scripts/r04_ab.sh OUTNAME   (runs each case with --opt $OPT=v for v in VALS, REPS times)
+# usage: OPT=name [VALS="0 1"] scripts/ab.sh OUTNAME   (runs each case with --opt $OPT=v for v in VALS, REPS times)
 #        OPT=lib VALS="default nocons" ...                  (library A/B: RTAMD_LIB=lib/librtamd_$v.so, "default" = the build)
+#        OPT=opts VALS="base wide_order=0 wide_order=0,tlas_sah=1"   (option sets: comma-separated k=v, "base" = none)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=gpurun_out/$1
 mkdir -p $OUT
@@ -22,6 +23,9 @@ for rep in $(seq 1 $REPS); do
       if [ "$OPT" = lib ]; then
         if [ "$v" = default ]; then lib=""; else lib=$PWD/real-time-gpu-ray-tracer_amd/lib/librtamd_$v.so; fi
         RTAMD_LIB=$lib timeout -k 10 300 python3 bench.py $args --no-cpu-baseline > $OUT/${name}_${v}_$rep.log 2>&1
+      elif [ "$OPT" = opts ]; then
+        oa=""; [ "$v" != base ] && for kv in ${v//,/ }; do oa="$oa --opt $kv"; done
+        timeout -k 10 300 python3 bench.py $args --no-cpu-baseline $oa > $OUT/${name}_${v}_$rep.log 2>&1
       else
         timeout -k 10 300 python3 bench.py $args --no-cpu-baseline --opt $OPT=$v > $OUT/${name}_${v}_$rep.log 2>&1
       fi

@@ -97,17 +97,13 @@ def test_c4_eight_tile_shards_assemble_to_the_frame(gpu_lib, c3_scene):
             assert slab_tiles == -(-((W + T - 1) // T) * ((H + T - 1) // T) // N)
             slab_px = slab_tiles * T * T
             gathered = torch.zeros(N * slab_px * 4, dtype=torch.uint8, device="cuda")
-            torch.cuda.synchronize()              # torch's fill runs on its stream, not the scene's
             rays = 0
             for k in range(N):
                 _, _, sk = r.render(0, exact=exact, tiles=(T, T, k, N), rgba8_device=gathered.data_ptr() + k * slab_px * 4,
                                     skip_update=True, want_rgba=False)
                 rays += sk["rays"]
             frame = torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda")
-            torch.cuda.synchronize()
             r.assemble_tiles(gathered.data_ptr(), slab_tiles, T, T, N, frame.data_ptr())
-            r.synchronize()
-            torch.cuda.synchronize()
             assert np.array_equal(frame.cpu().numpy().reshape(H, W, 4), full), mode
             assert rays == st["rays"], (rays, st["rays"])
 

@@ -367,31 +367,25 @@ ROOT_DT = np.dtype([("box", np.float32, 6), ("ref", np.uint32), ("height", np.ui
 REF_LEAF, REF_INDEX = 1 << 31, (1 << 30) - 1
 
 
-def _half_area(b):
-    f = np.float32
-    dx, dy, dz = f(b[1]) - f(b[0]), f(b[3]) - f(b[2]), f(b[5]) - f(b[4])
-    return f(f(dx * dy) + f(dy * dz)) + f(dz * dx)
-
-
 def _expected_quads(pairs, root_ref):
-    """csrc/bvh_build.hpp flatten_tree_wide restated on the GPU's own node pairs: quad q rooted at pair q
-    holds q's two children, twice expanding the largest-half-area interior child (first on ties)."""
+    """csrc/bvh_build.hpp flatten_tree_wide restated on the GPU's own node pairs: quad q rooted at pair q holds q's
+    two binary levels as two halves — slots 0, 1 = the left child's children, 2, 3 = the right child's; a leaf child
+    takes its half's first slot and the second is empty (REF_EMPTY) with a copy of its box."""
     out, todo = {}, ([root_ref & REF_INDEX] if not root_ref & REF_LEAF else [])
     while todo:
         q = todo.pop()
         p = pairs[q]
-        box, ref = [p["c0"].copy(), p["c1"].copy()], [int(p["ref0"]), int(p["ref1"])]
-        while len(ref) < 4:
-            cand = [(k, _half_area(box[k])) for k in range(len(ref)) if not ref[k] & REF_LEAF]
-            if not cand:
-                break
-            best = max(cand, key=lambda kv: (kv[1], -kv[0]))[0]     # largest area, first on ties
-            c = pairs[ref[best] & REF_INDEX]
-            box[best], ref[best] = c["c0"].copy(), int(c["ref0"])
-            box.append(c["c1"].copy())
-            ref.append(int(c["ref1"]))
+        box, ref = [], []
+        for c, r in ((p["c0"], int(p["ref0"])), (p["c1"], int(p["ref1"]))):
+            if r & REF_LEAF:
+                box += [c.copy(), c.copy()]
+                ref += [r, 0xFFFFFFFF]
+            else:
+                g = pairs[r & REF_INDEX]
+                box += [g["c0"].copy(), g["c1"].copy()]
+                ref += [int(g["ref0"]), int(g["ref1"])]
         out[q] = (box, ref)
-        todo += [r & REF_INDEX for r in ref if not r & REF_LEAF]
+        todo += [r & REF_INDEX for r in ref if r != 0xFFFFFFFF and not r & REF_LEAF]
     return out
 
 
@@ -399,7 +393,8 @@ def _expected_quads(pairs, root_ref):
 def test_gpu_quad_collapse_equals_restatement(gpu_lib, mode):
     """RT_BUILD_LBVH trees get the 4-wide form on the GPU (collapse_wide_kernel, lbvh.hip): every quad equals
     the host collapse rule applied to the GPU's binary tree (bit for bit, slot order included), and the quad
-    traversal renders the binary traversal's frame within the FAST tolerance with the same ray count."""
+    traversal — which visits the binary tree's order — renders the binary traversal's frame within the FAST
+    tolerance, with the same ray count."""
     if mode == "particles":
         s = scenes.demo_with_particles(12)
     elif mode == "group80":  # one 81,920-triangle group BLAS (> 65,536 items): collapsed one pair per thread
@@ -421,12 +416,10 @@ def test_gpu_quad_collapse_equals_restatement(gpu_lib, mode):
     for b in range(len(roots)):
         for q, (box, ref) in _expected_quads(pairs, int(roots[b]["ref"])).items():
             g = quads[q]
-            n = len(ref)
-            assert list(g["ref"][:n]) == ref and (g["ref"][n:] == 0xFFFFFFFF).all(), (b, q)
-            for k in range(n):
+            assert list(g["ref"]) == ref, (b, q)
+            for k in range(4):
                 got = [g["lo_x"][k], g["hi_x"][k], g["lo_y"][k], g["hi_y"][k], g["lo_z"][k], g["hi_z"][k]]
                 assert np.array_equal(np.asarray(got, np.float32), box[k]), (b, q, k)
-            assert np.isinf(g["lo_x"][n:]).all()
             n_quads += 1
     assert n_quads > 0
     out = {}

@@ -201,15 +201,11 @@ def test_tile_shards_assemble_to_full_frame(gpu_lib):
         slab_tiles = max(r.tiles_for_rank(tw, th, k, count) for k in range(count))
         slab_px = slab_tiles * tw * th
         gathered = torch.zeros(count * slab_px * 4, dtype=torch.uint8, device="cuda")
-        torch.cuda.synchronize()                  # torch's fill runs on its stream, not the scene's
         for k in range(count):
             r.render(0, tiles=(tw, th, k, count), rgba8_device=gathered.data_ptr() + k * slab_px * 4,
                      skip_update=True, want_rgba=False)
         frame = torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda")
-        torch.cuda.synchronize()
         r.assemble_tiles(gathered.data_ptr(), slab_tiles, tw, th, count, frame.data_ptr())
-        r.synchronize()
-        torch.cuda.synchronize()
         assert np.array_equal(frame.cpu().numpy().reshape(H, W, 4), full), (count, tw, th)
 
 

@@ -9,10 +9,12 @@ Bars (measured basis: the oracle against itself on different rand
     of pixels.
 The benched configuration is bench.py's: FAST persistent kernel, SAH trees, instance groups, quad traversal, LDS
 scene region, 4 overlapped lanes on new streams, frames pipelined without waiting (RT_RENDER_NO_SYNC) into device
-buffers; frames 0 and 37 of the animation.  Measured on MI355X (scripts/parity_report.py):
+buffers; frames 0 and 37 of the animation (C5: GPU LBVH trees rebuilt every frame, 2 lanes).  Measured on MI355X
+(scripts/parity_report.py):
   C2 depth 1: 0 outliers, float |d| 0 on both frames;  C2 depth 2: 34 / 4 outliers (0.0016 %);
-  C3 (4 spp, depth 4): 122 / 3 outliers (0.0059 %); C5 (GPU LBVH rebuilt per frame, 2 lanes): 1 304 / 1 544 (0.016 /
-  0.019 %, over the bar: the quad visit order, see BENCH_BAR); FAST on the reference's trees: <= 1 pixel per frame.
+  C3 (4 spp, depth 4): 122 / 3 outliers (0.0059 %); C4: 33 / 0;  C5: 4 / 255 (0.0031 %) — since round 5 the quads of
+  GPU-built (and the reference's own) trees hold two binary levels visited in the reference's pair order (round 4's
+  entry-t order: 1 304 / 1 544, over the bar); FAST on the reference's trees: <= 1 pixel per frame.
 Option "fast_math" (hardware reciprocals + FMA contraction, ~8 % faster) is held to its own measured bar: it moves
 0.008-0.09 % of pixels even on identical trees (ground-sphere cancellation in Sphere.cu:4-28 and bounce origins).
 Reference: src/Global/Kernel.cu:105-147 (render), src/AS/BoundingBox.cu:34-72 (the slab the FAST kernel culls with).
@@ -55,15 +57,6 @@ CASES = {
 # bench.py's configuration per case: the builder, the per-frame BLAS rebuild, the overlap lanes, lane 0 = the current
 # stream (bench.py "classic": a rebuild on a small frame) or every lane a new stream
 BENCH = {"C5": ("lbvh", True, 2, False)}
-# C5 (10 M triangles in 9 766 particle meshes) misses SURVEY's 0.01 % at depth 2 in the benched configuration:
-# measured 0.0157 % / 0.0186 % (frames 0 / 37).  The cause is the quad traversal's visit order, not the kernel's
-# arithmetic or the GPU trees: a ray through a mesh edge hits both triangles within the 1e-6 window and the later-
-# tested one wins (Range.cuh:33-43); the EXACT kernel on the same LBVH trees gives 3 / 255 outliers and the FAST
-# kernel with the reference's binary visit order 4 / 255 (test_c5_reference_order_on_bench_trees), while the quad
-# order, 1.66x faster on C5, sorts four children by entry where the reference orders two levels of pairs
-# (profiles/r04/slab_cons/parity_c5_trees.json, parity_c5_binary.json).  Held here to its measured level.
-BENCH_BAR = {"C5": 0.00025}
-
 
 @pytest.fixture(scope="module", params=list(CASES))
 def case(request):
@@ -105,7 +98,7 @@ def test_bench_configuration_full_frame_within_survey_bars(gpu_lib, case):
     name, scene, W, H, cam, orc = case
     got = bench_frames(scene, W, H, cam, name)
     depth = cam["ray_trace_depth"]
-    bar = BENCH_BAR.get(name, 0.0001 if depth <= 2 else 0.0005)
+    bar = 0.0001 if depth <= 2 else 0.0005
     for f in FRAMES:
         rgba, rgb = got[f]
         orgb, orgba = orc[f]
@@ -120,12 +113,13 @@ def test_bench_configuration_full_frame_within_survey_bars(gpu_lib, case):
 @pytest.mark.parametrize("wide", [0, 1])
 def test_fast_kernel_on_reference_trees(gpu_lib, case, wide):
     """Identical trees (the reference's median split), FAST kernel (persistent waves, reciprocal-slab culls, LDS
-    scene) with the reference's visit order (binary node pairs, "wide" 0) and with the default quad traversal.  The
+    scene) with the reference's visit order on binary node pairs ("wide" 0) and on the default quads (two binary
+    levels per quad, visited in the same pair order).  The
     kernel's arithmetic is the reference's wherever a value reaches a hit or a pixel; its box culls are conservative
     (RT_SLAB_CONS: never reject a box the reference's slab accepts).  What remains are hits on a box boundary that
-    the reference's own slab rounding culls and the FAST kernel tests (and, with quads, a visit-order tie inside the
-    1e-6 window): measured 0 pixels on 15 of 20 C2 / C3 / C4 / C5 frame renders, 1 pixel on the others (C3 frame 37: 4 LSB,
-    C5: 25-27 LSB); held to <= 2 pixels per frame (profiles/r04/c5_compat_residual/)."""
+    the reference's own slab rounding culls and the FAST kernel tests: measured 0 pixels on 18 of 20 C2 / C3 / C4 / C5
+    frame renders, 1 pixel on the others (C3 frame 37: 3 LSB, C5 frame 0: 0.19 float); held to <= 2 pixels per frame
+    (profiles/r04/c5_compat_residual/)."""
     name, scene, W, H, cam, orc = case
     r = Renderer(scene).set_option("wide", wide).build_acceleration_structure(0, mode="compat").configure_camera(W, H, **cam)
     for f in FRAMES:

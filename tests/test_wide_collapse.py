@@ -1,6 +1,7 @@
-"""CPU check of the BVH2 -> BVH4 collapse (csrc/bvh_build.hpp flatten_tree_wide, option "wide"):
-the quad form holds exactly the binary tree's leaves, every quad child box is a node box of the
-binary tree, quads hold 2-4 children, and the tree is about half as deep."""
+"""CPU check of the BVH2 -> BVH4 collapse (csrc/bvh_build.hpp flatten_tree_wide, option "wide"), in both forms —
+two binary levels per quad (halves: the reference's trees, visited in its pair order) and the greedy collapse (host
+SAH trees): the quad form holds exactly the binary tree's leaves, every quad child box (and with halves every half's
+union box) is a node box of the binary tree, quads hold 2-4 children, and the tree is about half as deep."""
 import json
 import os
 import subprocess
@@ -18,11 +19,12 @@ def checker(tmp_path_factory):
     return exe
 
 
+@pytest.mark.parametrize("halves", [1, 0])
 @pytest.mark.parametrize("merge", [0, 4])
 @pytest.mark.parametrize("n,sah", [(1, 1), (3, 1), (5, 0), (17, 1), (1000, 1), (1000, 0), (20000, 1)])
-def test_quad_form_preserves_leaves_and_boxes(checker, n, sah, merge):
+def test_quad_form_preserves_leaves_and_boxes(checker, n, sah, merge, halves):
     """merge = 4: binary subtrees of <= 4 items become one leaf (option "wide_merge")."""
-    r = json.loads(subprocess.run([checker, str(n), str(sah), str(merge)], check=True, capture_output=True,
+    r = json.loads(subprocess.run([checker, str(n), str(sah), str(merge), str(halves)], check=True, capture_output=True,
                                   text=True).stdout)
     assert r["slots_equal"] == 1 and r["bad_boxes"] == 0, r
     if r["quads"]:
