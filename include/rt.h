@@ -172,7 +172,9 @@ typedef enum rt_render_flags {
     RT_RENDER_NO_SYNC = 1u << 2,      /* return after enqueue (device outputs only)        */
     RT_RENDER_SKIP_UPDATE = 1u << 3,  /* do not run the instance update / TLAS rebuild (with
                                          "overlap": the frame waits for the whole launch that
-                                         uploaded its frame block, i.e. it serialises with it) */
+                                         uploaded its frame block, i.e. it serialises with it);
+                                         RT_ERR_STATE after rt_scene_update_triangles until a
+                                         frame has run its update (which rebuilds the BLASes) */
     RT_RENDER_KEEP_COUNTERS = 1u << 4 /* accumulate device counters (see rt_scene_collect); a
                                          synchronous frame with "overlap" then waits for every lane
                                          and reports the totals over all lanes                 */
@@ -300,7 +302,8 @@ rt_status rt_tile_pixels(uint32_t width, uint32_t height, uint32_t tile_w, uint3
                          uint32_t tile_count, uint64_t first, uint64_t n, int32_t *xy);
 
 /* Trace arbitrary world rays (origin xyz, direction xyz per ray) against the current TLAS
- * with t in [0.001, inf) and return the closest hit (TLAS::hit, src/AS/TLAS.cu:131-201). */
+ * with t in [0.001, inf) and return the closest hit (TLAS::hit, src/AS/TLAS.cu:131-201).
+ * RT_ERR_STATE after rt_scene_update_triangles until a frame has run its update. */
 rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_count,
                         uint32_t flags, rt_hit *hits_host);
 
@@ -409,8 +412,10 @@ rt_status rt_scene_collect(rt_scene *scene, rt_stats *accumulated, float *kernel
 
 /* Replace triangles [first, first + count) of the scene's triangle array (deforming geometry,
  * e.g. the next frame of a VTK series, Renderer.cu:394-443).  RT_BUILD_LBVH scenes only: the
- * BLASes are rebuilt on the GPU before the next frame traces.  Instances keep the local bounds
- * their description supplied (has_local_bounds), as the reference keeps the VTK reader's. */
+ * BLASes are rebuilt on the GPU by the next frame update, before that frame traces; until then a
+ * trace that skips the update (RT_RENDER_SKIP_UPDATE, rt_trace_rays) returns RT_ERR_STATE, since it
+ * would traverse the old trees while its hits read the new triangles.  Instances keep the local
+ * bounds their description supplied (has_local_bounds), as the reference keeps the VTK reader's. */
 rt_status rt_scene_update_triangles(rt_scene *scene, size_t first, size_t count, const rt_triangle *triangles);
 
 /* Replace instance descriptions [first, first + count) — local bounds / centroid and the transform

@@ -180,7 +180,7 @@ struct SceneGPU {
     const NodeQuad *blas_quads;     // option "wide" (host-built trees): quad forms of the BLASes / TLAS
     const NodeQuad *tlas_quads;
     const TreeRoot *tlas_root_wide;
-    uint32_t wide;                  // 1: the FAST persistent kernel traverses the quad trees
+    uint32_t wide;                  // FAST persistent kernel: 0 binary node pairs, 1..3 quad trees (trace_kernel.hip XBOX)
     uint32_t inst_by_slot;          // 1 (host-built TLAS): inst_hot / inst_cold are stored in TLAS leaf-slot
                                     // order, so entering an instance needs no tlas_slots load (the slot
                                     // is the record index; tlas_slots maps it back to the instance id)

@@ -826,9 +826,11 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.tlas_root_wide = reinterpret_cast<const TreeRoot *>(s->frame_dev[b] + s->off_root_wide);
     g.tlas_quads = reinterpret_cast<const NodeQuad *>(s->frame_dev[b] + s->off_quads);
     g.blas_quads = s->blas_quads.p;
-    // quad trees (GPU-built: from collapse_wide): 2 = two binary levels per quad visited in the reference's order (the
-    // reference's own trees and GPU-built ones), 1 = host SAH BLASes collapsed greedily, visited by entry t
-    g.wide = s->wide && s->blas_quads.p != nullptr ? (s->quad_halves() ? 2u : 1u) : 0u;
+    // quad trees (GPU-built: from collapse_wide): 1 = host SAH BLASes collapsed greedily, visited by entry t; 2 = two
+    // binary levels per quad visited in the reference's order (GPU-built trees); 3 = the same on the reference's own
+    // trees, with every box decision inside the FAST slab's error margin re-taken with the reference's slab
+    g.wide = s->wide && s->blas_quads.p != nullptr
+                 ? (s->quad_halves() ? (s->build_mode == RT_BUILD_COMPAT_MEDIAN ? 3u : 2u) : 1u) : 0u;
     g.tlas_slots = reinterpret_cast<const uint32_t *>(s->frame_dev[b] + s->off_slots);
     const bool gpu_slots = s->gpu_tlas() && s->block_by_slot[b];   // the slot-ordered copies of GPU-built frames
     g.inst_hot = reinterpret_cast<const InstHot *>(s->frame_dev[b] + (gpu_slots ? s->off_hot_s : s->off_hot));
@@ -1636,6 +1638,10 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         o.tile_w = cm->tile_w; o.tile_h = cm->tile_h;
         o.tile_rank = (uint32_t)cm->rank; o.tile_count = (uint32_t)cm->world;
     }
+    // a trace that skips the frame update after rt_scene_update_triangles would traverse the old trees while its hits
+    // read the new triangles (raw_tris): the next frame update rebuilds the BLASes first
+    if ((o.flags & RT_RENDER_SKIP_UPDATE) && s->blas_dirty)
+        return fail(RT_ERR_STATE, "triangles were updated since the last frame update: render a frame with the update first");
     HIP_TRY(hipSetDevice(s->device));
     hipStream_t stream = o.stream ? static_cast<hipStream_t>(o.stream) : s->stream;
     double update_ms = 0.0;
@@ -1989,6 +1995,8 @@ rt_status rt_trace_rays(rt_scene *s, const float *rays, size_t n, uint32_t flags
     if (!s->built) return fail(RT_ERR_STATE, "rt_scene_build has not been called");
     if (n == 0) return RT_OK;
     if (n > 0xFFFFFFFFull) return fail(RT_ERR_INVALID_ARGUMENT, "too many rays");
+    if (s->blas_dirty)
+        return fail(RT_ERR_STATE, "triangles were updated since the last frame update: render a frame with the update first");
     HIP_TRY(hipSetDevice(s->device));
     float *d_rays = nullptr;
     rt_hit *d_hits = nullptr;

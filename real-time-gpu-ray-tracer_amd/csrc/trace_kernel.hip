@@ -75,9 +75,22 @@ static_assert(LDS_DEPTH % 4 == 0, "half-pages move as 16 B pieces");
                                         // reciprocal-FMA planes is widened by a bound on its distance from the
                                         // reference's (mn - q) / d interval before the lo < hi test (and a popped entry's
                                         // lo before its lo < tmax re-test), so a FAST cull never rejects a box the
-                                        // reference's slab accepts; entries keep the unwidened lo, so children are still
-                                        // ordered by it
+                                        // reference's slab accepts — except on a parallel axis (|d| < 1e-6) when the origin
+                                        // lies exactly on a face of the slab: the reference keeps q == min / max
+                                        // (BoundingBox.cu:47), the FAST planes there are the rounding residual of o / d and
+                                        // may reject; the exact-decision instances (XBOX) re-test every box of such a ray.
+                                        // Entries keep the unwidened lo, so children are still ordered by it
 #endif
+#ifndef RT_BOX_EXACT
+#define RT_BOX_EXACT 1                  // FAST box decisions that lie inside the slabs' error margin (and every box test of a
+                                        // ray with a parallel axis) are re-taken with the reference's division slab, as
+                                        // are the pair-order comparisons of two entry t's inside the margin: on the
+                                        // reference's trees the traversal takes the reference's decisions
+#endif
+// the persistent kernel's traversal modes (SceneGPU::wide): 0 binary node pairs, 1 greedy quads by entry t (host SAH
+// trees), 2 two-level quads in pair order (GPU-built trees), 3 the same with exact box decisions (the reference's trees);
+// the binary pairs (an A/B path) take exact decisions too
+#define XBOX(W) (RT_BOX_EXACT && ((W) == 0 || (W) == 3))
 #ifndef RT_NZ_MIN
 #define RT_NZ_MIN FZERO                 // |d_axis| below this is clamped to +-1e-20 for the slab reciprocals (prep)
 #endif
@@ -187,10 +200,12 @@ struct RayP {
 #if !RT_EXACT
     f3 inv, oinv;      // 1/d and o/d for one-FMA slab planes
 #if RT_SLAB_CONS
-    float pad;         // the absolute part of the plane-distance bound: 2^-22 max |o/d| over the non-parallel axes
+    float pad;         // the absolute part of a plane distance's error bound: 2^-22 max |o/d| over the non-parallel
+                       // axes; negative (sign bit set) when an axis is parallel (|d| < 1e-6)
 #endif
 #endif
 };
+template <bool XB = false>
 __device__ __forceinline__ void prep(RayP &r) {
 #if !RT_EXACT
     // |d| < 1e-6 (the reference's parallel-axis threshold, BoundingBox.cu:44-50) -> +-1e-20: the plane distances
@@ -205,7 +220,12 @@ __device__ __forceinline__ void prep(RayP &r) {
         const float px = fabsf(r.d.x) < RT_NZ_MIN ? 0.0f : fabsf(r.oinv.x);
         const float py = fabsf(r.d.y) < RT_NZ_MIN ? 0.0f : fabsf(r.oinv.y);
         const float pz = fabsf(r.d.z) < RT_NZ_MIN ? 0.0f : fabsf(r.oinv.z);
-        r.pad = 0x1p-22f * fmaxf(px, fmaxf(py, pz));
+        const float pad = 0x1p-22f * fmaxf(px, fmaxf(py, pz));
+        r.pad = pad;
+        if (XB) {       // the exact-decision instances re-take every box test of a ray with a parallel axis
+            const bool par = fabsf(r.d.x) < RT_NZ_MIN || fabsf(r.d.y) < RT_NZ_MIN || fabsf(r.d.z) < RT_NZ_MIN;
+            r.pad = par ? -pad : pad;
+        }
     }
 #endif
 #else
@@ -238,11 +258,26 @@ __device__ __forceinline__ bool slab_ref(const float *b, const f3 &o, const f3 &
     return true;
 }
 
-#if RT_SLAB_CONS
-// a box's entry / exit distance widened by the bound above (lo, hi >= TMIN > 0 wherever lo < hi can hold)
-__device__ __forceinline__ float cons_lo(float lo, float pad) { return fmaf(lo, 1.0f - 0x1p-20f, -pad); }
-__device__ __forceinline__ float cons_hi(float hi, float pad) { return fmaf(hi, 1.0f + 0x1p-20f, pad); }
+#if RT_SLAB_CONS && !RT_EXACT
+// The reference's slab as one out-of-line copy for the FAST kernels' rare exact re-tests (inlined at every box test it
+// would add its divisions to the hot loop's code and registers).  Returns the entry t, or NaN for a miss.
+struct BoxArgs { float b[6]; f3 o, d; float tmax; };
+__device__ __attribute__((noinline)) float slab_ref_entry(BoxArgs a) {
+    float te = 0.0f;
+    return slab_ref(a.b, a.o, a.d, TMIN, a.tmax, te) ? te : __builtin_nanf("");
+}
+// A FAST box decision: each end of the interval [lo, hi] (hi includes tmax) is within |pad| + 2^-20 |t| of the
+// reference's (lo, hi >= TMIN > 0 wherever lo < hi can hold), so the widened test cons_lo(lo) < cons_hi(hi) keeps every
+// box the reference's slab accepts (a cull is never wrong), and hi - lo > box_margin is an accept the reference shares;
+// in between, the XB instances re-take the decision with the reference's slab (RT_BOX_EXACT)
+__device__ __forceinline__ float cons_lo(float lo, float pad) { return fmaf(lo, 1.0f - 0x1p-20f, -fabsf(pad)); }
+__device__ __forceinline__ float cons_hi(float hi, float pad) { return fmaf(hi, 1.0f + 0x1p-20f, fabsf(pad)); }
+__device__ __forceinline__ float box_margin(float lo, float hi, float pad) { return fmaf(lo + hi, 0x1p-20f, 2.0f * fabsf(pad)); }
+__device__ __forceinline__ bool ray_parallel(const RayP &r) { return __builtin_signbit(r.pad) != 0; }
 #endif
+// XB: decisions inside the margin re-taken with the reference's slab (RT_BOX_EXACT: the quad instance for the reference's
+// own trees and the binary-pair one, where the traversal then takes exactly the reference's decisions)
+template <bool XB = false>
 __device__ __forceinline__ bool slab(const float *b, const RayP &r, float tmin, float tmax, float &te) {
 #if RT_EXACT
     return slab_ref(b, r.o, r.d, tmin, tmax, te);
@@ -254,7 +289,18 @@ __device__ __forceinline__ bool slab(const float *b, const RayP &r, float tmin, 
     const float hi = fminf(fminf(tmax, fmaxf(tx1, tx2)), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
     te = lo;
 #if RT_SLAB_CONS
-    return cons_lo(lo, r.pad) < cons_hi(hi, r.pad);
+    bool h = cons_lo(lo, r.pad) < cons_hi(hi, r.pad);
+#if RT_BOX_EXACT
+    if (XB && ((h && !(hi - lo > box_margin(lo, hi, r.pad))) || ray_parallel(r))) {   // rare: the reference's decision
+        BoxArgs a;
+        for (int c = 0; c < 6; c++) a.b[c] = b[c];
+        a.o = r.o; a.d = r.d; a.tmax = tmax;
+        const float e = slab_ref_entry(a);            // (tmin is TMIN at every call site)
+        h = e == e;
+        if (h) te = e;
+    }
+#endif
+    return h;
 #else
     return lo < hi;
 #endif
@@ -477,8 +523,9 @@ __device__ __forceinline__ bool pop_keep(const Trav &T, float tn, uint32_t ref) 
 }
 
 // R: this frame's TLAS root (the persistent kernel holds it in SGPRs, loaded once per wave)
+template <bool XB = false>
 __device__ __forceinline__ void trav_init(Trav &T, const TreeRoot &R, const f3 &o, const f3 &d) {
-    T.wr.o = o; T.wr.d = d; prep(T.wr);
+    T.wr.o = o; T.wr.d = d; prep<XB>(T.wr);
     T.lr = T.wr;
     T.tmax = __builtin_huge_valf();
     T.found = false;
@@ -488,7 +535,7 @@ __device__ __forceinline__ void trav_init(Trav &T, const TreeRoot &R, const f3 &
     T.cur_inst = 0;
     T.pleaf = REF_NONE;
     float te = 0.0f;
-    T.tracing = slab(R.box, T.wr, TMIN, T.tmax, te);                     // root pop test (TLAS.cu:150)
+    T.tracing = slab<XB>(R.box, T.wr, TMIN, T.tmax, te);                 // root pop test (TLAS.cu:150)
     T.curT = te;
 }
 __device__ __forceinline__ void trav_init(Trav &T, const SceneGPU &sc, const f3 &o, const f3 &d) {
@@ -692,25 +739,27 @@ __device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float 
         pb = fmaxf(pb, fminf(n2, n3));
     }
 }
+__device__ __forceinline__ float comp4(const float4 &v, int k) { return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w)); }
 __device__ __forceinline__ void cswap(float &ta, uint32_t &ra, float &tb, uint32_t &rb) {
     const bool sw = tb < ta;
     const float t = sw ? tb : ta, u = sw ? ta : tb;
     const uint32_t r = sw ? rb : ra, q = sw ? ra : rb;
     ta = t; tb = u; ra = r; rb = q;
 }
-template <bool COUNT, bool PAIR>
+template <bool COUNT, bool PAIR, bool XB>
 __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
     const uint32_t cur = T.cur;
     const bool blas = (cur & REF_BLAS) != 0;
     float4 lx, hx, ly, hy, lz, hz;
     uint4 R;
     // one code path: a generic pointer into the LDS scene region or HBM (flat loads serve both)
+    const float4 *Q;
     {
         const uint32_t qi = cur & REF_INDEX_MASK, qb = qi - sc.lds_bq0;
         const bool in_lds = blas ? qb < sc.lds_bqn : sc.lds_quads != 0;
         const uint32_t at = blas ? sc.lds_bq_at + qb * LDS_QUAD_F4 : qi * LDS_QUAD_F4;
-        const float4 *Q = in_lds ? static_cast<const float4 *>(lds_scene + at)
-                                 : reinterpret_cast<const float4 *>((blas ? sc.blas_quads : sc.tlas_quads) + qi);
+        Q = in_lds ? static_cast<const float4 *>(lds_scene + at)
+                   : reinterpret_cast<const float4 *>((blas ? sc.blas_quads : sc.tlas_quads) + qi);
         lx = Q[0]; hx = Q[1]; ly = Q[2]; hy = Q[3]; lz = Q[4]; hz = Q[5];
         R = reinterpret_cast<const uint4 *>(Q)[6];
     }
@@ -721,7 +770,7 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
     if (COUNT) cnt.pairs += 2;                       // 4 child boxes = 2 node-pair equivalents
     const RayP &r = blas ? T.lr : T.wr;
     float t[4];
-    bool h[4];
+    bool h[4], und[4] = {false, false, false, false};   // und: hit decision inside the error margin
     float pa = TMIN, pb = TMIN;                      // entry t of the two halves' boxes
     {
         float4 tn = make_float4(TMIN, TMIN, TMIN, TMIN), tf = make_float4(T.tmax, T.tmax, T.tmax, T.tmax);
@@ -732,6 +781,10 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
 #if RT_SLAB_CONS
         h[0] = cons_lo(tn.x, r.pad) < cons_hi(tf.x, r.pad); h[1] = cons_lo(tn.y, r.pad) < cons_hi(tf.y, r.pad);
         h[2] = cons_lo(tn.z, r.pad) < cons_hi(tf.z, r.pad); h[3] = cons_lo(tn.w, r.pad) < cons_hi(tf.w, r.pad);
+        if (XB) {
+            und[0] = !(tf.x - tn.x > box_margin(tn.x, tf.x, r.pad)); und[1] = !(tf.y - tn.y > box_margin(tn.y, tf.y, r.pad));
+            und[2] = !(tf.z - tn.z > box_margin(tn.z, tf.z, r.pad)); und[3] = !(tf.w - tn.w > box_margin(tn.w, tf.w, r.pad));
+        }
 #else
         h[0] = tn.x < tf.x; h[1] = tn.y < tf.y; h[2] = tn.z < tf.z; h[3] = tn.w < tf.w;
 #endif
@@ -739,6 +792,47 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
     // an empty slot repeats its sibling's box (the half's union stays exact) and is never accepted
     h[1] = h[1] && R.y != REF_EMPTY;
     h[3] = h[3] && R.w != REF_EMPTY;
+#if RT_SLAB_CONS && RT_BOX_EXACT
+    if (XB) {   // Rare: a hit decision inside the error margin, a ray with a parallel axis, or (pair order) two entry t's the order
+        // compares inside the margin — then every box of the node is re-tested with the reference's slab (the halves'
+        // boxes too: unions of their slots' boxes), on the node's bounds read again (keeping the 24 bounds live through
+        // the step would cost registers on the hot path), one box per iteration so that one copy of the division slab
+        // serves all six
+        const auto close = [&](float a, float b) { return fabsf(a - b) <= box_margin(a, b, r.pad); };
+        bool need = ray_parallel(r) || (h[0] && und[0]) || (h[1] && und[1]) || (h[2] && und[2]) || (h[3] && und[3]);
+        if (PAIR)
+            need = need || (h[0] && h[1] && close(t[0], t[1])) || (h[2] && h[3] && close(t[2], t[3])) ||
+                   ((h[0] || h[1]) && (h[2] || h[3]) && close(pa, pb));
+        if (need) {
+            const float4 L[6] = {Q[0], Q[1], Q[2], Q[3], Q[4], Q[5]};
+#pragma unroll 1
+            for (int j = 0; j < (PAIR ? 6 : 4); j++) {
+                const int k0 = j < 4 ? j : 2 * (j - 4), k1 = j < 4 ? j : k0 + 1;     // a slot, or a half's two slots
+                float b[6];
+#pragma unroll
+                for (int c = 0; c < 6; c++) {
+                    const float u = comp4(L[c], k0), v = comp4(L[c], k1);
+                    b[c] = (c & 1) ? fmaxf(u, v) : fminf(u, v);
+                }
+                BoxArgs ba;
+                for (int c = 0; c < 6; c++) ba.b[c] = b[c];
+                ba.o = r.o; ba.d = r.d; ba.tmax = T.tmax;
+                const float te = slab_ref_entry(ba);
+                const bool hh = te == te;
+                if (j < 4) {
+                    const uint32_t rk = j == 0 ? R.x : (j == 1 ? R.y : (j == 2 ? R.z : R.w));
+                    const bool live = rk != REF_EMPTY;
+                    const bool hk = hh && live;
+                    h[0] = j == 0 ? hk : h[0]; h[1] = j == 1 ? hk : h[1]; h[2] = j == 2 ? hk : h[2]; h[3] = j == 3 ? hk : h[3];
+                    if (hk) { t[0] = j == 0 ? te : t[0]; t[1] = j == 1 ? te : t[1]; t[2] = j == 2 ? te : t[2]; t[3] = j == 3 ? te : t[3]; }
+                } else if (hh) {
+                    pa = j == 4 ? te : pa;
+                    pb = j == 5 ? te : pb;
+                }
+            }
+        }
+    }
+#endif
     const float inf = __builtin_huge_valf();
     if (!PAIR) {
         float t0 = h[0] ? t[0] : inf, t1 = h[1] ? t[1] : inf, t2 = h[2] ? t[2] : inf, t3 = h[3] ? t[3] : inf;
@@ -808,7 +902,7 @@ __device__ __forceinline__ void spec_interior_step(Trav &T, const SceneGPU &sc, 
     const uint32_t cur = T.cur;
 #if !RT_EXACT
     if (WIDE) {
-        if (!(cur & REF_LEAF)) wide_interior_step<COUNT, WIDE == 2>(T, sc, spill, cnt);
+        if (!(cur & REF_LEAF)) wide_interior_step<COUNT, (WIDE >= 2), (WIDE == 3)>(T, sc, spill, cnt);
         else { T.pleaf = cur; pop_next(T, spill); }        // postpone, keep walking
         return;
     }
@@ -824,8 +918,8 @@ __device__ __forceinline__ void spec_interior_step(Trav &T, const SceneGPU &sc, 
         if (COUNT) cnt.pairs++;
         float e0 = 0.0f, e1 = 0.0f;
         const RayP &r = blas ? T.lr : T.wr;
-        const bool h0 = slab(b0, r, TMIN, T.tmax, e0);
-        const bool h1 = slab(b1, r, TMIN, T.tmax, e1);
+        const bool h0 = slab<XBOX(WIDE)>(b0, r, TMIN, T.tmax, e0);
+        const bool h1 = slab<XBOX(WIDE)>(b1, r, TMIN, T.tmax, e1);
         if (h0 && h1) {
             const bool right_near = e0 > e1;          // TLAS.cu:185-192 ordering
             stack_push(T.stk, spill, right_near ? D.x : D.y, right_near ? e0 : e1, cnt);
@@ -883,8 +977,8 @@ __device__ __forceinline__ uint32_t spec_leaf_phase(Trav &T, const SceneGPU &sc,
             const float box[6] = {I.box01.x, I.box01.y, I.box01.z, I.box01.w, I.box2ref.x, I.box2ref.y};
             T.lr.o = xf_point(inv, T.wr.o);                    // Instance.cu:26-27
             T.lr.d = xf_vector(inv, T.wr.d);
-            prep(T.lr);
-            if (slab(box, T.lr, TMIN, T.tmax, te)) {
+            prep<XBOX(WIDE)>(T.lr);
+            if (slab<XBOX(WIDE)>(box, T.lr, TMIN, T.tmax, te)) {
                 T.cur = __float_as_uint(I.box2ref.w);
                 T.curT = te;
                 if (RT_CHAIN_ROOT_LEAF && (T.cur & REF_LEAF)) { leaf = T.cur; chained = true; }
@@ -897,8 +991,8 @@ __device__ __forceinline__ uint32_t spec_leaf_phase(Trav &T, const SceneGPU &sc,
             const InstHot &I = sc.inst_hot[T.cur_inst];
             T.lr.o = xf_point(I.inv, T.wr.o);                      // Instance.cu:26-27
             T.lr.d = xf_vector(I.inv, T.wr.d);
-            prep(T.lr);
-            if (slab(I.root_box, T.lr, TMIN, T.tmax, te)) { T.cur = WIDE ? I.root_ref_wide : I.root_ref; T.curT = te; }
+            prep<XBOX(WIDE)>(T.lr);
+            if (slab<XBOX(WIDE)>(I.root_box, T.lr, TMIN, T.tmax, te)) { T.cur = WIDE ? I.root_ref_wide : I.root_ref; T.curT = te; }
             else pop_next(T, spill);
         }
     }
@@ -1467,7 +1561,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     px_steps = 0;
                     f3 o, d;
                     camera_ray(cam, px, py, 0, rng, o, d);
-                    trav_init(T, root, o, d);
+                    trav_init<XBOX(WIDE)>(T, root, o, d);
                     pixels++;
                 }
             }
@@ -1546,7 +1640,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                     fin = true;
                 }
             }
-            if (has) trav_init(T, root, no, nd);
+            if (has) trav_init<XBOX(WIDE)>(T, root, no, nd);
         }
         if (track && fin) {
             const uint32_t u = item >> 6;
@@ -1690,12 +1784,16 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
         const hipError_t e = hipMemsetAsync(queue, 0, QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
     }
-    // quad trees: one instance per scene kind — visit order (SceneGPU::wide 1 = by entry t, 2 = the binary tree's)
-    // and where a hit triangle's shading data lives (finalize's RAW; GPU-built trees are always in pair order)
+    // quad trees: one instance per scene kind — traversal mode (SceneGPU::wide, XBOX) and where a hit triangle's shading
+    // data lives (finalize's RAW; GPU-built trees are always in pair order)
     if (sc.wide && HAS_WIDE) {
         if (sc.raw_tris) {
             if (variant == 4) return launch_persistent_wpe<4, 2 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
             return launch_persistent_wpe<3, 2 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+        }
+        if (sc.wide == 3) {
+            if (variant == 4) return launch_persistent_wpe<4, 3 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+            return launch_persistent_wpe<3, 3 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
         }
         if (sc.wide == 2) {
             if (variant == 4) return launch_persistent_wpe<4, 2 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
@@ -1712,6 +1810,7 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
 uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, uint32_t wide, bool raw) {
     if (wide && HAS_WIDE) {
         if (raw) return variant == 4 ? blocks_per_cu_wpe<4, 2 * HAS_WIDE, 1>() : blocks_per_cu_wpe<3, 2 * HAS_WIDE, 1>();
+        if (wide == 3) return variant == 4 ? blocks_per_cu_wpe<4, 3 * HAS_WIDE, 0>() : blocks_per_cu_wpe<3, 3 * HAS_WIDE, 0>();
         if (wide == 2) return variant == 4 ? blocks_per_cu_wpe<4, 2 * HAS_WIDE, 0>() : blocks_per_cu_wpe<3, 2 * HAS_WIDE, 0>();
         return variant == 4 ? blocks_per_cu_wpe<4, HAS_WIDE, 0>() : blocks_per_cu_wpe<3, HAS_WIDE, 0>();
     }

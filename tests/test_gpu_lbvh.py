@@ -211,12 +211,13 @@ def test_update_triangles_pipelined_frames(gpu_lib, group):
     r.cleanup()
 
 
-@pytest.mark.parametrize("double", [1, 0])
-def test_update_triangles_once_then_pipelined_frames(gpu_lib, double):
+@pytest.mark.parametrize("double,sets,cold", [(1, 3, 0), (1, 2, 0), (1, 3, 1), (1, 2, 1), (0, 3, 0), (0, 3, 1)])
+def test_update_triangles_once_then_pipelined_frames(gpu_lib, double, sets, cold):
     """One rt_scene_update_triangles, then frames on three overlapped lanes without waiting: only the first frame
     enqueues the BLAS rebuild (on the scene stream); the frames after it on the other lanes build nothing and must
     still wait for it before their instance records, TLAS and trace read the new BLAS set.  Every
-    frame equals the synchronous render of the same frame; both BLAS-set policies ("blas_double")."""
+    frame equals the synchronous render of the same frame by a default scene (one set in place or 2 / 3 sets in
+    rotation, "blas_double" / "blas_sets"; with or without TriCold records, "cold_records" — same pixels)."""
     import torch
     P = 200                                            # ~205 k triangles: a rebuild long enough to race with
     s = scenes.demo_with_particles(P)
@@ -224,12 +225,13 @@ def test_update_triangles_once_then_pipelined_frames(gpu_lib, double):
     W, H, F, L = 256, 144, 9, 3
     moved = s.triangles[:n_p].copy()
     moved["vertex"] += np.asarray([0.04, -0.02, 0.03], np.float32)
-    ref_r = Renderer(s).set_option("blas_double", double).build_acceleration_structure(0, mode="lbvh")
+    ref_r = Renderer(s).build_acceleration_structure(0, mode="lbvh")
     ref_r.configure_camera(W, H, ray_trace_depth=2)
     ref_r.update_triangles(0, moved)
     ref = [ref_r.render(f)[0] for f in range(F)]
     ref_r.cleanup()
-    r = Renderer(s).set_option("blas_double", double).build_acceleration_structure(0, mode="lbvh")
+    r = Renderer(s).set_option("blas_double", double).set_option("blas_sets", sets).set_option("cold_records", cold)
+    r.build_acceleration_structure(0, mode="lbvh")
     r.configure_camera(W, H, ray_trace_depth=2)
     r.set_option("overlap", L)
     lanes = [torch.cuda.Stream() for _ in range(L)]
@@ -246,6 +248,26 @@ def test_update_triangles_once_then_pipelined_frames(gpu_lib, double):
     torch.cuda.synchronize()
     for f in range(F):
         assert np.array_equal(bufs[f].cpu().numpy().reshape(H, W, 4), ref[f]), f
+    r.cleanup()
+
+
+def test_trace_after_triangle_update_needs_a_frame_update(gpu_lib):
+    """After rt_scene_update_triangles the BLASes are rebuilt by the next frame update; a trace that skips it
+    (RT_RENDER_SKIP_UPDATE, rt_trace_rays) would mix the old trees with the new triangles a hit reads
+    (raw_tris), so it is refused with RT_ERR_STATE until a frame has run its update (include/rt.h)."""
+    s = scenes.demo_with_particles(4)
+    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(64, 48, ray_trace_depth=2)
+    a = r.render(0)[0]
+    assert np.array_equal(r.render(0, skip_update=True)[0], a)
+    moved = s.triangles[:1024].copy()
+    moved["vertex"] += np.asarray([0.01, 0.0, 0.0], np.float32)
+    r.update_triangles(0, moved)
+    with pytest.raises(abi.RtError, match="RT_ERR_STATE"):
+        r.render(0, skip_update=True)
+    with pytest.raises(abi.RtError, match="RT_ERR_STATE"):
+        r.trace_rays(np.asarray([[0.0, 2.0, 10.0, 0.0, 0.0, -1.0]], np.float32))
+    b = r.render(0)[0]                                 # the update rebuilds the BLASes
+    assert np.array_equal(r.render(0, skip_update=True)[0], b)
     r.cleanup()
 
 

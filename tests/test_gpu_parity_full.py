@@ -14,7 +14,7 @@ buffers; frames 0 and 37 of the animation (C5: GPU LBVH trees rebuilt every fram
   C2 depth 1: 0 outliers, float |d| 0 on both frames;  C2 depth 2: 34 / 4 outliers (0.0016 %);
   C3 (4 spp, depth 4): 122 / 3 outliers (0.0059 %); C4: 33 / 0;  C5: 4 / 255 (0.0031 %) — since round 5 the quads of
   GPU-built (and the reference's own) trees hold two binary levels visited in the reference's pair order (round 4's
-  entry-t order: 1 304 / 1 544, over the bar); FAST on the reference's trees: <= 1 pixel per frame.
+  entry-t order: 1 304 / 1 544, over the bar); FAST on the reference's trees: bit-identical float frames.
 Option "fast_math" (hardware reciprocals + FMA contraction, ~8 % faster) is held to its own measured bar: it moves
 0.008-0.09 % of pixels even on identical trees (ground-sphere cancellation in Sphere.cu:4-28 and bounce origins).
 Reference: src/Global/Kernel.cu:105-147 (render), src/AS/BoundingBox.cu:34-72 (the slab the FAST kernel culls with).
@@ -114,12 +114,12 @@ def test_bench_configuration_full_frame_within_survey_bars(gpu_lib, case):
 def test_fast_kernel_on_reference_trees(gpu_lib, case, wide):
     """Identical trees (the reference's median split), FAST kernel (persistent waves, reciprocal-slab culls, LDS
     scene) with the reference's visit order on binary node pairs ("wide" 0) and on the default quads (two binary
-    levels per quad, visited in the same pair order).  The
-    kernel's arithmetic is the reference's wherever a value reaches a hit or a pixel; its box culls are conservative
-    (RT_SLAB_CONS: never reject a box the reference's slab accepts).  What remains are hits on a box boundary that
-    the reference's own slab rounding culls and the FAST kernel tests: measured 0 pixels on 18 of 20 C2 / C3 / C4 / C5
-    frame renders, 1 pixel on the others (C3 frame 37: 3 LSB, C5 frame 0: 0.19 float); held to <= 2 pixels per frame
-    (profiles/r04/c5_compat_residual/)."""
+    levels per quad, visited in the same pair order).  The kernel's arithmetic is the reference's wherever a value
+    reaches a hit or a pixel; its box culls are conservative (RT_SLAB_CONS), and on these trees every box decision —
+    and every pair-order comparison — that lies inside the reciprocal slab's error margin is re-taken with the
+    reference's division slab (RT_BOX_EXACT, XBOX instances), so the traversal takes the reference's decisions: the
+    float frame is bit-identical (round 4, without the re-test: 1 pixel on 5 of 20 renders, a hit on a box boundary
+    the reference's own slab rounding culls; profiles/r04/c5_compat_residual/, profiles/r05/exact_box/)."""
     name, scene, W, H, cam, orc = case
     r = Renderer(scene).set_option("wide", wide).build_acceleration_structure(0, mode="compat").configure_camera(W, H, **cam)
     for f in FRAMES:
@@ -127,8 +127,8 @@ def test_fast_kernel_on_reference_trees(gpu_lib, case, wide):
         orgb, orgba = orc[f]
         mism = int((rgb != orgb).any(axis=-1).sum())
         print(f"{name} frame {f} wide {wide}: {mism} pixels differ, max {float(np.abs(rgb - orgb).max()):.4f}")
-        assert mism <= 2, (name, f, mism, float(np.abs(rgb - orgb).max()))
-        assert outliers(rgba, orgba)[0] <= 2
+        assert mism == 0, (name, f, mism, float(np.abs(rgb - orgb).max()))
+        assert outliers(rgba, orgba)[0] == 0
     r.cleanup()
 
 
