@@ -61,6 +61,9 @@ def parse():
     p.add_argument("--overlap", type=int, default=None,
                    help="L >= 2: consecutive frames cycle L streams / library lanes so frame k+1 fills the CUs "
                         "frame k's tail leaves idle; 0 or 1: frames are serialised (default 3)")
+    p.add_argument("--lanes", default="library", choices=("library", "caller"),
+                   help="library: frames without a stream on lanes the scene owns (option overlap -1 picks the lane "
+                        "count and staging depth; --overlap L sets L); caller: bench creates the lane streams")
     p.add_argument("--lane-priority", type=int, default=None,
                    help="overlap lanes on new HIP streams of this priority (torch: -1 high, 0 normal); default: "
                         "new normal-priority streams, except the current stream + new ones with a per-frame rebuild")
@@ -199,6 +202,9 @@ def load_traffic(tag):
     return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO), "tagged PMC summary"
 
 
+rt_scene_lanes_max = 8                                     # rt.h: "overlap" lanes 2..8
+
+
 def main():
     args = parse()
     if args.print_pmc_tag:
@@ -235,7 +241,12 @@ def main():
     # with a communicator attached (N > 1, --attach-comm) RCCL's own streams take hardware queues as well: at 12
     # two of three lanes shared one queue and ran back to back (world-1 comm path 0.29 ms/frame, 0.22 at 16-24;
     # 1/8 shares 0.045 -> 0.043; profiles/r03_session2/comm_world1_hwq.jsonl)
-    want_q = 24 if (n > 1 or args.attach_comm) else (0 if classic else 12)
+    # library lanes (the default, below) are high-priority streams with hardware queues of their own: one GPU needs no
+    # more than the default 4 (C2 0.180 ms/frame at 4 and at 12 queues, profiles/r05/lanes/)
+    lib_lane_run = args.lanes == "library" and not classic and args.lane_priority is None
+    # (a rank's share runs 8 lanes: more than the high-priority queues HIP hands out at 4, 0.046 against 0.038
+    # ms/frame at 12-24 queues, profiles/r05/lanes/)
+    want_q = 24 if (n > 1 or args.attach_comm) else (12 if share else (0 if (classic or lib_lane_run) else 12))
     if os.environ.get("RTAMD_HWQ"):                    # A/B studies: an explicit queue count
         os.environ["GPU_MAX_HW_QUEUES"] = os.environ["RTAMD_HWQ"]
     elif want_q and int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < want_q:
@@ -272,12 +283,18 @@ def main():
     # a per-frame rebuild of a >= 16 M-path frame (C5): 2 lanes (the rebuild kernels then find slots between two
     # traces instead of three or four: 9.78 / 9.76 -> 8.82 ms/frame; 1 lane 13.7; profiles/r04/c5_rebuild/r04s17_*,
     # r04s18_*); trees built once keep 4 (5.46 against 5.86 with 3, 6.43 with 2)
+    # library lanes (default): the scene picks the lanes ("overlap" -1, rt_api.cpp auto_lanes: the counts below) and
+    # runs frames rendered without a stream on streams of its own; a C2-LBVH-style rebuild of a small frame ("classic")
+    # keeps the caller's null stream as lane 0, which only a caller can hand it
+    lib_lanes = args.lanes == "library" and not classic and args.lane_priority is None
     L = max(1, args.overlap if args.overlap is not None else
             (8 if share else (3 if classic else (2 if args.rebuild and big else 4))))
     overlap = L > 1
-    if overlap:
+    if lib_lanes and args.overlap is None:
+        r.set_option("overlap", -1)
+    elif overlap:
         r.set_option("overlap", L)
-    if share:
+    if share and not (lib_lanes and args.overlap is None):
         # the host stages frame k once frame k - depth's trace is done: 64 lets it run 8 frames ahead per lane
         # (C2 1/8 share 0.0446 -> 0.0432 ms/frame, C4 equal; profiles/r03_session2/stage_depth.jsonl)
         r.set_option("stage_depth", 64)
@@ -288,7 +305,7 @@ def main():
     # every lane on a new stream, none on the null stream (C2 1/8 share 0.0437 -> 0.0416 ms/frame, world-1 comm
     # path 0.212 -> 0.191, the whole frame with 4 lanes above; profiles/r03_session2/lane_streams_*.txt)
     prio = args.lane_priority if args.lane_priority is not None else (None if classic else 0)
-    if overlap and prio is not None:
+    if overlap and prio is not None and not lib_lanes:
         lanes = [torch.cuda.Stream(priority=prio) for _ in range(L)]
     shard = tuple(int(v) for v in args.shard.split("/")) if args.shard else None
     if shard and (n > 1 or args.attach_comm):
@@ -305,8 +322,10 @@ def main():
     elif shard:
         tiles = (TILE, TILE, shard[0], shard[1])
     frame_buf = torch.zeros(cfg.width * cfg.height * 4, dtype=torch.uint8, device="cuda") if rank == 0 else None
-    frame_bufs = ([frame_buf] + [torch.zeros_like(frame_buf) if overlap else frame_buf for _ in range(L - 1)]
-                  if rank == 0 else [None] * L)
+    nbuf = rt_scene_lanes_max if overlap else 1
+    serial_stream = torch.cuda.Stream()                    # the roofline's serialised launches (a non-null stream)
+    frame_bufs = ([frame_buf] + [torch.zeros_like(frame_buf) if overlap else frame_buf for _ in range(nbuf - 1)]
+                  if rank == 0 else [None] * nbuf)
 
     host_update = []                                       # (update_ms, part of it waiting on the GPU) per call
 
@@ -314,8 +333,11 @@ def main():
         """One frame; sync=False pipelines it (host TLAS build of the next frame overlaps the GPU).
         With "overlap", frame k runs on lanes[k % L] (its own trace -> gather -> assemble chain);
         one_stream: every frame on the first lane's stream (launches serialised back to back)."""
-        b = frame % L if overlap else 0
-        st = lanes[0 if one_stream else b].cuda_stream if overlap else stream
+        b = frame % nbuf if overlap else 0
+        if lib_lanes and overlap:
+            st = serial_stream.cuda_stream if one_stream else None   # None: the scene's own lane streams
+        else:
+            st = lanes[0 if one_stream else frame % L].cuda_stream if overlap else stream
         fb = frame_bufs[b]
         t_call = time.perf_counter()
         _, _, sts = r.render(frame, exact=args.exact, want_rgba=False, rgba8_device=fb.data_ptr() if fb is not None else None,
@@ -364,6 +386,8 @@ def main():
     if args.launch_times and rank == 0:                    # before collect() empties the library's ring
         np.save(args.launch_times, r.debug_read("launch_times").view(np.float32).reshape(-1, 2))
     acc, kernel_ms = r.collect()                           # device counters + HIP-event kernel times
+    if lib_lanes and args.overlap is None:
+        L = int(r.info()["overlap_lanes"])                 # the library's pick for this frame kind
     rays = int(acc["rays"])
     assert len(kernel_ms) == args.steps, (len(kernel_ms), args.steps)
 
@@ -464,8 +488,11 @@ def main():
                                                ("single-gpu through the world-1 comm path" if args.attach_comm
                                                 else "single-gpu"))),
                 "overlap_lanes": L,
-                "lane_streams": (None if not overlap else ("current stream + new streams" if prio is None
-                                                           else f"new streams, priority {prio}")),
+                "lane_streams": (None if not overlap else
+                                 ("the scene's own (overlap -1: lanes and staging picked by the library)"
+                                  if lib_lanes and args.overlap is None else
+                                  ("the scene's own" if lib_lanes else
+                                   ("current stream + new streams" if prio is None else f"new streams, priority {prio}")))),
                 "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4),
                 "tile": TILE,
                 "threshold": args.threshold if args.threshold is not None else "auto (64 at depth x spp <= 2, else 40)",

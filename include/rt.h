@@ -29,8 +29,9 @@ extern "C" {
 #endif
 
 /* 2: rt_stats gained update_wait_ms; rt_comm_* / rt_slab_tiles / rt_tile_pixels / rt_scene_detach_comm;
- *    rt_camera_move / rt_frame_pacer_* / rt_comm_set_timeout (round 3) */
-#define RT_ABI_VERSION 2u
+ *    rt_camera_move / rt_frame_pacer_* / rt_comm_set_timeout (round 3)
+ * 3: rt_scene_info gained overlap_lanes / stage_depth; "overlap" -1 = library-picked lanes on library streams */
+#define RT_ABI_VERSION 3u
 
 typedef enum rt_status {
     RT_OK = 0,
@@ -331,6 +332,12 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "rebuild"   : RT_BUILD_LBVH only: 1 = rebuild every BLAS on the GPU every frame (default 0)
  *   "timeline"  : 1 = record a per-wave timeline of each persistent launch (debug)
  *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal steps (debug)
+ *   "leaf_early": persistent kernel: a round's interior loop also ends once no more than this many lanes are still
+ *                 looking for a leaf (0..64; 0 = when every traversing lane holds one); -1 (default) = auto: 0 for
+ *                 paths of <= 2 segments (depth x samples), else 12.  Results are identical for every value
+ *   "lane_priority": the lane streams the scene creates for "overlap" frames without a caller stream: 1 (default) =
+ *                 the device's highest stream priority (hardware queues of their own: full overlap at the default
+ *                 GPU_MAX_HW_QUEUES of 4), 0 = normal priority
  *   "tlas_sah"  : RT_BUILD_SAH: 1 (default) = build the per-frame host TLAS with SAH; 0 = the reference's median split
  *                 (TLAS.cu:4-129; "tlas_median_leaf" 1..2 = its leaf size, 0 = the reference's 2)
  *   "tlas_leaf" : instances per leaf of an SAH or GPU-built TLAS (1..4, default 1; GPU-built TLASes: set before
@@ -377,9 +384,13 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 shape: inactive records are left out instead of sorted into a subtree no ray enters)
  *   "overlap"   : L = consecutive rt_render calls cycle through L (2..8) internal lanes (work-queue
  *                 heads, unit costs, schedule); a launch waits only for the previous launch of its own
- *                 lane and for its frame block, so a caller that cycles L streams runs frame
- *                 k+1's launch in the CUs frame k's tail leaves idle.  The caller orders its own output
- *                 buffers (default 0 = 1 lane: every launch of the scene is serialised)                    */
+ *                 lane and for its frame block, so frame k+1's launch runs in the CUs frame k's tail
+ *                 leaves idle.  Frames with opts.stream NULL run on lane streams the scene creates; a
+ *                 caller that passes streams cycles its own.  -1 = auto: the scene also picks L and the
+ *                 staging depth per frame kind (8 lanes / 64 buffers for a rank's tile share, 2 lanes for
+ *                 a >= 16 M-path frame with a per-frame rebuild, else 4).  With lanes the caller orders
+ *                 its own output buffers: device outputs of NO_SYNC frames without a stream are complete
+ *                 once rt_synchronize returns (default 0 = 1 lane: every launch of the scene is serialised) */
 rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
 
 /* Debug buffers of the last launch that recorded them (synchronises the scene's stream):
@@ -505,6 +516,9 @@ typedef struct rt_scene_info {
     uint32_t ray_trace_depth;
     uint32_t tlas_height;          /* interior levels on the longest TLAS root-to-leaf path */
     uint32_t blas_height_max;      /* the same, deepest BLAS */
+    uint32_t overlap_lanes;        /* lanes consecutive frames cycle through (option "overlap"; -1 = auto, resolved
+                                    * by the last rt_render) */
+    uint32_t stage_depth;          /* pinned staging buffers of the per-frame upload */
 } rt_scene_info;
 
 rt_status rt_scene_get_info(const rt_scene *scene, rt_scene_info *info);

@@ -260,6 +260,7 @@ struct OutputGPU {
     const uint32_t *order;
     uint32_t *unit_cost;
     uint32_t cost_max;              // 1: a unit's cost is 64 x its longest path (atomicMax), not the sum of its paths
+    uint32_t leaf_early;            // option "leaf_early": interior loop ends with <= this many lanes still descending
 };
 constexpr uint32_t QUEUE_STRIDE = 32;         // u32 words between partition heads (128 B lines)
 constexpr uint32_t QUEUE_MAX_PARTS = 8;
@@ -281,7 +282,7 @@ __host__ __device__ inline uint32_t split_log2(uint32_t cls, uint32_t k_half, ui
     const uint32_t k = (SCHED_CLASSES - 1) - cls;
     return k >= k_quarter ? 2u : (k >= k_half ? 1u : 0u);
 }
-constexpr uint32_t TIMELINE_WORDS = 16;
+constexpr uint32_t TIMELINE_WORDS = 20;
 
 // Counter slots (device uint64 array)
 enum CounterSlot : uint32_t {

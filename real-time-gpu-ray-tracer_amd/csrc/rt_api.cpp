@@ -277,6 +277,21 @@ struct rt_scene {
     uint32_t reserve = 16;
     uint32_t lane = 0;              // lane of the next rt_render (overlap)
     int last_lane = 0;              // lane of the last rt_render
+    // "overlap" frames rendered without a caller stream (opts.stream NULL) run on lane streams the scene owns; with
+    // option "overlap" -1 (overlap_auto) the scene also picks the lane count and the staging depth per frame kind
+    // (auto_lanes: the settings bench.py measured best), so a drop-in caller passes no streams at all
+    hipStream_t lane_st[NLANE] = {};
+    bool overlap_auto = false;
+    // option "leaf_early" (OutputGPU::leaf_early): -1 = auto, 0 for paths of <= 2 segments (depth x samples; C2, C4),
+    // else LEAF_EARLY_AUTO (C3 1.54 -> 1.25, C5 5.79 -> 4.97 ms/frame; C2 0.181 -> 0.185 with it,
+    // profiles/r05/leaf_early/)
+    int leaf_early = -1;
+    static constexpr uint32_t LEAF_EARLY_AUTO = 12;
+    // option "lane_priority": the scene's own lane streams at the device's highest priority (default 1): HIP gives them
+    // hardware queues of their own, so 4 lanes run side by side at the default GPU_MAX_HW_QUEUES (4) — C2 0.256 ->
+    // 0.180 ms/frame, C3 2.15 -> 1.54, a 1/8 share 0.064 -> 0.046 — as at 12 queues (profiles/r05/lanes/)
+    bool lane_priority = true;
+    bool stage_depth_set = false;   // option "stage_depth" given explicitly (auto lanes leave it alone)
     hipEvent_t ev_lane_done[NLANE] = {};   // last trace launch of each lane finished
     uint32_t cus = 0;
     // option "threshold" (lanes waiting before a wave leaves traversal to shade and refill); 0 = auto: 64 when
@@ -475,6 +490,8 @@ struct rt_scene {
             if (ring_post[i]) (void)hipEventDestroy(ring_post[i]);
         }
         if (stream) (void)hipStreamDestroy(stream);
+        for (hipStream_t &l : lane_st)
+            if (l) (void)hipStreamDestroy(l);
     }
 };
 
@@ -1591,7 +1608,8 @@ rt_status rt_scene_attach_comm(rt_scene *s, const rt_comm_id *id, int rank, int 
     auto *cm = new (std::nothrow) CommState();
     if (!cm) return fail(RT_ERR_OUT_OF_MEMORY, "host allocation failed");
     cm->rank = rank; cm->world = world; cm->tile_w = tw; cm->tile_h = th;
-    cm->ncomm = (int)std::max<uint32_t>(1u, s->overlap ? s->lanes : 1u);   // one per lane in use
+    // one per lane in use (auto lanes: the 8 a rank's share runs on, auto_lanes)
+    cm->ncomm = (int)std::max<uint32_t>(1u, s->overlap_auto && world > 1 ? 8u : (s->overlap ? s->lanes : 1u));
     cm->timeout_ms = s->comm_timeout_ms;
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
@@ -1622,6 +1640,28 @@ rt_status rt_scene_detach_comm(rt_scene *s) {
     return RT_OK;
 }
 
+// Option "overlap" -1: the lane count (and staging depth) bench.py measured best per frame kind:
+// a rank's share of a multi-GPU frame (tiles, or a communicator of world > 1) 8 lanes and 64 staging buffers; a
+// launch of >= BIG_LAUNCH_PATHS camera paths with a per-frame BLAS rebuild 2 lanes (the rebuild finds slots between
+// two traces); any other frame 4 lanes.  Changing the count drains the scene (a new frame kind, e.g. attaching a
+// communicator).
+rt_status auto_lanes(rt_scene *s, const rt_render_opts &o) {
+    const bool share = o.tile_count > 0 || (s->comm && s->comm->world > 1);
+    const uint64_t paths = (uint64_t)s->width * s->height * s->cam.sqrt_s * s->cam.sqrt_s;
+    const uint32_t L = share ? 8u : (s->rebuild_blas && paths >= rt_scene::BIG_LAUNCH_PATHS ? 2u : 4u);
+    const int depth = share ? rt_scene::NSTAGE : 2 * rt_scene::NLANE;
+    if (L == s->lanes && (s->stage_depth_set || depth == s->stage_depth)) return RT_OK;
+    RT_TRY(drain(s));
+    s->lanes = L;
+    s->overlap = L > 1;
+    s->lane = 0;
+    if (!s->stage_depth_set) {
+        s->stage_depth = depth;
+        s->stage_next = 0;
+    }
+    return RT_OK;
+}
+
 rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uint8_t *rgba_host, float *rgb_host,
                     rt_stats *stats) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -1643,7 +1683,22 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     if ((o.flags & RT_RENDER_SKIP_UPDATE) && s->blas_dirty)
         return fail(RT_ERR_STATE, "triangles were updated since the last frame update: render a frame with the update first");
     HIP_TRY(hipSetDevice(s->device));
-    hipStream_t stream = o.stream ? static_cast<hipStream_t>(o.stream) : s->stream;
+    if (s->overlap_auto) RT_TRY(auto_lanes(s, o));
+    // the frame's stream: the caller's; else, with "overlap", the lane's own stream (created on first use), else the
+    // scene's stream (every frame of the scene in order)
+    hipStream_t stream = static_cast<hipStream_t>(o.stream);
+    const bool lib_lane = !stream && s->overlap;
+    if (lib_lane) {
+        hipStream_t &ls = s->lane_st[s->lane];
+        if (!ls) {
+            int lo = 0, hi = 0;                    // option "lane_priority": 1 = the device's highest stream priority
+            HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIP_TRY(hipStreamCreateWithPriority(&ls, hipStreamNonBlocking, s->lane_priority ? hi : 0));
+        }
+        stream = ls;
+    } else if (!stream) {
+        stream = s->stream;
+    }
     double update_ms = 0.0;
     if (!(o.flags & RT_RENDER_SKIP_UPDATE)) {
         const auto u0 = std::chrono::steady_clock::now();
@@ -1659,6 +1714,8 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     const int q = s->overlap ? (int)s->lane : 0;
     OutputGPU out{};
     out.nt_store = s->nt_store;
+    out.leaf_early = s->leaf_early >= 0 ? (uint32_t)s->leaf_early
+                                        : (s->cam.depth * s->cam.sqrt_s * s->cam.sqrt_s <= 2u ? 0u : rt_scene::LEAF_EARLY_AUTO);
     const uint32_t W = s->width, H = s->height;
     size_t npix;
     if (o.tile_count == 0) {
@@ -1770,12 +1827,16 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     s->lane = s->overlap ? (s->lane + 1) % s->lanes : 0u;
     s->last_lane = q;
     if (hipEvent_t prev = s->overlap ? s->r_lane[q] : s->r_done) HIP_TRY(hipStreamWaitEvent(stream, prev, 0));
-    // Device outputs and no stream: the trace runs on the scene's non-blocking stream, which HIP does not order with
-    // the caller's null-stream work, so it waits for what the caller enqueued there before the call (e.g. a fill of
-    // the buffer) and the null stream waits for the frame (a read of it after the call).  The reference draws into
-    // a surface it owns on its own stream (Renderer.cu:305-317), so a drop-in caller expects no ordering of its own.
+    // Device outputs and no stream: the trace runs on a non-blocking stream of the scene, which HIP does not order
+    // with the caller's null-stream work, so it waits for what the caller enqueued there before the call (e.g. a fill
+    // of the buffer), and — without "overlap" — the null stream waits for the frame (a read of it after the call).  The
+    // reference draws into a surface it owns on its own stream (Renderer.cu:305-317), so a drop-in caller expects no
+    // ordering of its own.  With "overlap" the frames run side by side on the scene's lanes; a null-stream wait per
+    // frame would serialise them, so their device outputs are complete once rt_synchronize returns.
+    // (A null stream with nothing pending needs no wait: one host query instead of a cross-queue wait, ~5 us of GPU
+    // idle time per frame, profiles/r02_gaps.txt.)
     const bool order_null = !o.stream && (o.rgba8_device || o.rgb32_device);
-    if (order_null) {
+    if (order_null && hipStreamQuery(nullptr) == hipErrorNotReady) {
         if (!s->ev_caller) HIP_TRY(hipEventCreateWithFlags(&s->ev_caller, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(s->ev_caller, nullptr));
         HIP_TRY(hipStreamWaitEvent(stream, s->ev_caller, 0));
@@ -1930,7 +1991,7 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     s->r_used[s->active] = s->r_done = s->r_lane[q] = done;
     if (copied_block >= 0) s->r_copied[copied_block] = s->r_staged[copied_stage] = done;
     if (s->ev_blas_lane[q]) HIP_TRY(hipEventRecord(s->ev_blas_lane[q], stream));   // "blas_double": this set's reader
-    if (order_null) HIP_TRY(hipStreamWaitEvent(nullptr, done, 0));
+    if (order_null && !lib_lane) HIP_TRY(hipStreamWaitEvent(nullptr, done, 0));
     if (o.flags & RT_RENDER_NO_SYNC) {
         if (stats) { std::memset(stats, 0, sizeof *stats); stats->update_ms = update_ms; stats->update_wait_ms = s->update_wait_ms; }
         return RT_OK;
@@ -2044,6 +2105,7 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         RT_TRY(drain(s));
         s->stage_depth = (int)value;
         s->stage_next = 0;
+        s->stage_depth_set = true;
     } else if (k == "nt_store") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "nt_store must be 0 or 1");
         s->nt_store = (uint32_t)value;
@@ -2116,6 +2178,15 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "blas_leaf") {
         if (value < 1 || value > (int64_t)SAH_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "blas_leaf must be in 1..4");
         s->blas_leaf = (uint32_t)value;
+    } else if (k == "leaf_early") {
+        if (value < -1 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "leaf_early must be -1 (auto) or 0..64");
+        s->leaf_early = (int)value;
+    } else if (k == "lane_priority") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "lane_priority must be 0 or 1");
+        RT_TRY(drain(s));
+        for (hipStream_t &l : s->lane_st)
+            if (l) { (void)hipStreamDestroy(l); l = nullptr; }          // recreated at the next frame
+        s->lane_priority = value == 1;
     } else if (k == "tlas_median_leaf") {
         if (value < 0 || value > (int64_t)TLAS_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_median_leaf must be 0..2");
         s->tlas_median_leaf = (uint32_t)value;
@@ -2129,9 +2200,10 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         RT_TRY(drain(s));
         s->inst_by_slot = value == 1;            // takes effect with the next frame's staging
     } else if (k == "overlap") {
-        if (value < 0 || value > rt_scene::NLANE) return fail(RT_ERR_INVALID_ARGUMENT, "overlap must be 0..8 lanes");
+        if (value < -1 || value > rt_scene::NLANE) return fail(RT_ERR_INVALID_ARGUMENT, "overlap must be -1 (auto) or 0..8 lanes");
         RT_TRY(drain(s));
-        s->lanes = value < 1 ? 1u : (uint32_t)value;
+        s->overlap_auto = value == -1;
+        s->lanes = value < 1 ? (value == -1 ? 4u : 1u) : (uint32_t)value;      // auto: resolved per frame (auto_lanes)
         s->overlap = s->lanes > 1;
         s->lane = 0;
     } else if (k == "reserve") {
@@ -2401,6 +2473,8 @@ rt_status rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
     if (!s || !info) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
     std::memset(info, 0, sizeof *info);
     info->blas_count = s->blas_own;     // per-instance BLASes (the groups' merged ones are not counted)
+    info->overlap_lanes = s->lanes;
+    info->stage_depth = (uint32_t)s->stage_depth;
     info->blas_node_pairs = s->blas_pair_count;
     info->blas_leaves = s->blas_leaf_count;
     info->tlas_node_pairs = s->tlas_flat.pairs.size();

@@ -1058,7 +1058,12 @@ __device__ __forceinline__ uint32_t spec_leaf_phase(Trav &T, const SceneGPU &sc,
 // Diagnostic builds (make diag -> librtamd_diag.so): wave-uniform cycle stamps per phase.
 // claim / hit (diagnostic builds): cycles giving idle lanes their pixels (map, RNG, camera ray, traversal
 // init) and sampling scatter directions after the hit records arrived
-struct PhaseCycles { unsigned long long refill, interior, leaf, shade, iters, refill_iters, claim, hit; };
+struct PhaseCycles {
+    unsigned long long refill, interior, leaf, shade, iters, refill_iters, claim, hit;
+    // lane occupancy (diagnostic builds): lanes stepping per interior iteration, lanes holding a TLAS / BLAS leaf per
+    // leaf phase, lanes shaded per shade step (sums; the timeline divides by iters / rounds / shades)
+    unsigned long long lanes_interior, lanes_leaf_tlas, lanes_leaf_blas, lanes_shade;
+};
 __device__ __forceinline__ unsigned long long stamp() {
     unsigned long long t;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
@@ -1076,14 +1081,19 @@ __device__ __forceinline__ unsigned long long stamp() {
 
 // One round: interior loop until every traversing lane holds a leaf, then the leaf phase.
 // steps (when `track`): the lane's interior steps + leaf phases, the pixel's cost for the work order
+// leaf_early (option "leaf_early"): the interior loop also ends once no more than this many lanes are still looking
+// for a leaf while some hold one; the lanes without a leaf skip the leaf phase and go on descending next round
 template <bool COUNT, int WIDE = 0>
 __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt,
-                                           PhaseCycles &pc, uint32_t &steps, bool track) {
+                                           PhaseCycles &pc, uint32_t &steps, bool track, uint32_t leaf_early) {
     DIAG_T(t0);
     for (;;) {
         if (T.tracing && T.pleaf == REF_NONE && T.cur == REF_NONE) T.tracing = false;   // done, no leaf left
-        if (!__any(T.tracing && T.pleaf == REF_NONE)) break;
+        const uint64_t looking = __ballot(T.tracing && T.pleaf == REF_NONE);
+        if (!looking) break;
+        if (leaf_early && (uint32_t)__popcll(looking) <= leaf_early && __any(T.tracing && T.pleaf != REF_NONE)) break;
         const bool active = T.tracing && T.cur != REF_NONE && (!(T.cur & REF_LEAF) || T.pleaf == REF_NONE);
+        if (RT_DIAG) pc.lanes_interior += (unsigned long long)__popcll(__ballot(active));
         if (active) {
             spec_interior_step<COUNT, WIDE>(T, sc, spill, cnt);
             if (track) steps++;
@@ -1091,8 +1101,12 @@ __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *sp
         if (RT_DIAG) pc.iters++;
     }
     DIAG_ADD(pc.interior, t0);
+    if (RT_DIAG) {
+        pc.lanes_leaf_tlas += (unsigned long long)__popcll(__ballot(T.tracing && T.pleaf != REF_NONE && !(T.pleaf & REF_BLAS)));
+        pc.lanes_leaf_blas += (unsigned long long)__popcll(__ballot(T.tracing && T.pleaf != REF_NONE && (T.pleaf & REF_BLAS)));
+    }
     DIAG_T(t1);
-    if (T.tracing) {
+    if (T.tracing && T.pleaf != REF_NONE) {
         const uint32_t chained = spec_leaf_phase<COUNT, WIDE>(T, sc, spill, cnt);
         if (track) steps += 1u + chained;
     }
@@ -1472,7 +1486,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
     uint32_t pend_unit = 0, pend_cost = 0;          // the lane's unflushed unit cost (flushed before a claim)
     unsigned long long t_start = 0, t_exhaust = 0;
     uint32_t n_rounds = 0, n_shades = 0, n_grabs = 0;      // wave-uniform (timeline)
-    PhaseCycles pc = {0, 0, 0, 0, 0, 0, 0, 0};
+    PhaseCycles pc = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     if (out.timeline) t_start = __builtin_amdgcn_s_memrealtime();
 
     for (;;) {
@@ -1580,13 +1594,14 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             if (tr == 0) break;
             const uint64_t want = __ballot(!T.tracing && (has || !exhausted));
             if ((uint32_t)__popcll(want) >= threshold) break;
-            spec_round<COUNT, WIDE>(T, sc, spill, cnt, pc, px_steps, COUNT || track);
+            spec_round<COUNT, WIDE>(T, sc, spill, cnt, pc, px_steps, COUNT || track, out.leaf_early);
             n_rounds++;
         }
         // ---- shade lanes whose segment finished (rayColor body, Kernel.cu:64-100)
         n_shades++;
         DIAG_T(t_shade);
         bool fin = false;                    // lane wrote its pixel in this step
+        if (RT_DIAG) pc.lanes_shade += (unsigned long long)__popcll(__ballot(has && !T.tracing));
         if (has && !T.tracing) {
             rays++;
             bool path_done;
@@ -1693,6 +1708,10 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
             w[13] = pc.refill_iters;
             w[14] = pc.claim;
             w[15] = pc.hit;
+            w[16] = pc.lanes_interior;
+            w[17] = pc.lanes_leaf_tlas;
+            w[18] = pc.lanes_leaf_blas;
+            w[19] = pc.lanes_shade;
         }
     }
 }

@@ -8,7 +8,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 
-RT_ABI_VERSION = 2
+RT_ABI_VERSION = 3
 
 RT_OK = 0
 RT_STATUS_NAMES = {
@@ -124,7 +124,8 @@ class SceneInfo(C.Structure):
                 ("blas_leaves", C.c_uint64), ("tlas_node_pairs", C.c_uint64),
                 ("device_bytes", C.c_uint64), ("width", C.c_uint32), ("height", C.c_uint32),
                 ("sqrt_sample_count", C.c_uint32), ("ray_trace_depth", C.c_uint32),
-                ("tlas_height", C.c_uint32), ("blas_height_max", C.c_uint32)]
+                ("tlas_height", C.c_uint32), ("blas_height_max", C.c_uint32), ("overlap_lanes", C.c_uint32),
+                ("stage_depth", C.c_uint32)]
 
 
 class CommId(C.Structure):

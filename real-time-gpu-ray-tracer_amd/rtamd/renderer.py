@@ -138,19 +138,23 @@ class Renderer:
     def timeline(self):
         """Per-wave timeline of the last persistent launch (set_option("timeline", 1) first).
         Structured array: start/end in s_memrealtime ticks (100 MHz), xcc, hw_id, pixels."""
-        w = self.debug_read("timeline").view(np.uint64).reshape(-1, 16)
+        w = self.debug_read("timeline").view(np.uint64).reshape(-1, 20)
         out = np.zeros(len(w), dtype=[("start", np.uint64), ("end", np.uint64), ("xcc", np.uint32),
                                       ("hw_id", np.uint32), ("pixels", np.uint32), ("exhaust", np.uint64),
                                       ("rounds", np.uint32), ("shades", np.uint32), ("grabs", np.uint32),
                                       ("cyc_refill", np.uint64), ("cyc_interior", np.uint64), ("cyc_leaf", np.uint64),
                                       ("cyc_shade", np.uint64), ("iters", np.uint64), ("refill_iters", np.uint64),
-                                      ("cyc_lanes", np.uint64), ("cyc_scatter", np.uint64)])
+                                      ("cyc_lanes", np.uint64), ("cyc_scatter", np.uint64),
+                                      ("lanes_interior", np.uint64), ("lanes_leaf_tlas", np.uint64),
+                                      ("lanes_leaf_blas", np.uint64), ("lanes_shade", np.uint64)])
         out["start"], out["end"], out["exhaust"] = w[:, 0], w[:, 1], w[:, 4]
         out["xcc"], out["hw_id"], out["pixels"] = w[:, 2] & 0xFFFFFFFF, w[:, 2] >> 32, w[:, 3]
         out["rounds"], out["shades"], out["grabs"] = w[:, 5], w[:, 6], w[:, 7]
         out["cyc_refill"], out["cyc_interior"], out["cyc_leaf"], out["cyc_shade"] = w[:, 8], w[:, 9], w[:, 10], w[:, 11]
         out["iters"], out["refill_iters"] = w[:, 12], w[:, 13]
         out["cyc_lanes"], out["cyc_scatter"] = w[:, 14], w[:, 15]       # diagnostic builds only: lane refill work, scatter sampling
+        # diagnostic builds only: lane sums per interior iteration / leaf phase (TLAS, BLAS leaves) / shade step
+        out["lanes_interior"], out["lanes_leaf_tlas"], out["lanes_leaf_blas"], out["lanes_shade"] = w[:, 16], w[:, 17], w[:, 18], w[:, 19]
         return out
 
     def costmap(self):

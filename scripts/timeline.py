@@ -49,6 +49,12 @@ def summarize(tl, tag):
             "refill_iters_per_shade": round(float(tl["refill_iters"].sum() / max(1, tl["shades"].sum())), 2),
             "us_per_round_plus_shade_p50": round(float(np.median(life / (tl["rounds"] + tl["shades"]))), 3),
             "mean_life_frac": round(float(life.mean() / span), 3),
+            # diagnostic builds: mean lanes at work (of 64) per interior iteration, per leaf phase (TLAS + BLAS leaves,
+            # which run as two divergent code paths) and per shade step
+            "lanes_per_interior_iter": round(float(tl["lanes_interior"].sum() / max(1, tl["iters"].sum())), 2),
+            "lanes_per_leaf_phase_tlas_blas": [round(float(tl["lanes_leaf_tlas"].sum() / max(1, tl["rounds"].sum())), 2),
+                                               round(float(tl["lanes_leaf_blas"].sum() / max(1, tl["rounds"].sum())), 2)],
+            "lanes_per_shade": round(float(tl["lanes_shade"].sum() / max(1, tl["shades"].sum())), 2),
             "start_us_p50_p99_max": [round(float(np.percentile(st, q)), 1) for q in (50, 99, 100)],
             "end_us_p1_p50_p99": [round(float(np.percentile(en, q)), 1) for q in (1, 50, 99)],
             "pixels": int(tl["pixels"].sum()), "per_xcc": per_xcc}

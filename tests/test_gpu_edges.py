@@ -128,12 +128,13 @@ def test_tiny_frames_on_overlapped_lanes(gpu_lib, w, h):
 
 @pytest.mark.parametrize("lanes", [0, 3])
 def test_null_stream_device_outputs_ordered(gpu_lib, lanes):
-    """rt_render with device outputs and no stream (opts.stream NULL) runs on the scene's non-blocking stream; it
-    is ordered after the caller's null-stream work enqueued before the call and before the null stream's work after
-    it (rt_api.cpp order_null), as a drop-in caller of the reference's render-into-my-surface loop
-    (Renderer.cu:305-317) expects.  Each iteration queues a long fill on torch's default (null) stream, a fill of
-    the output with junk, the frame with RT_RENDER_NO_SYNC and no stream, and a copy of the output — no host
-    synchronisation anywhere — and every copy equals the synchronously rendered frame byte for byte."""
+    """rt_render with device outputs and no stream (opts.stream NULL) runs on a non-blocking stream of the scene; it
+    is ordered after the caller's null-stream work enqueued before the call and, without "overlap", before the null
+    stream's work after it (rt_api.cpp order_null), as a drop-in caller of the reference's render-into-my-surface
+    loop (Renderer.cu:305-317) expects.  Each iteration queues a long fill on torch's default (null) stream, a fill
+    of the output with junk, the frame with RT_RENDER_NO_SYNC and no stream, and a copy of the output — no host
+    synchronisation anywhere — and every copy equals the synchronously rendered frame byte for byte.  With
+    "overlap" the frames run side by side on the scene's own lanes and are read after rt_synchronize."""
     import torch
     s = scenes.demo_with_particles(10)
     W, H = 320, 184
@@ -146,9 +147,19 @@ def test_null_stream_device_outputs_ordered(gpu_lib, lanes):
     copies = []
     for it in range(24):
         big.fill_(float(it))                         # keeps the null stream busy for a while
-        out.fill_(0x5A)
-        r.render(it % 4, want_rgba=False, rgba8_device=out.data_ptr(), sync=False)
-        copies.append(out.clone())
+        if lanes:
+            # frames on the scene's own lane streams run side by side: each waits for the caller's null-stream work
+            # before the call (the junk fill), and its output is complete once rt_synchronize returns
+            o = torch.empty(W * H * 4, dtype=torch.uint8, device="cuda")
+            o.fill_(0x5A)
+            r.render(it % 4, want_rgba=False, rgba8_device=o.data_ptr(), sync=False)
+            copies.append(o)
+        else:
+            out.fill_(0x5A)
+            r.render(it % 4, want_rgba=False, rgba8_device=out.data_ptr(), sync=False)
+            copies.append(out.clone())
+    if lanes:
+        r.synchronize()
     for it, c in enumerate(copies):
         assert np.array_equal(c.cpu().numpy().reshape(H, W, 4), ref[it % 4]), it
     r.cleanup()

@@ -437,7 +437,8 @@ def test_reorder_period_byte_identical(gpu_lib, period, lanes):
 
 @pytest.mark.parametrize("opts", [{"grid_pct": 30}, {"merge": 8}, {"merge": 16}, {"merge": 0}, {"split": 0xFFFF},
                                   {"split": 4 | 8 << 8}, {"cost_max": 1}, {"lds_blas": 0}, {"stage_depth": 2},
-                                  {"stage_depth": 64}])
+                                  {"stage_depth": 64}, {"leaf_early": 0}, {"leaf_early": 1}, {"leaf_early": 12},
+                                  {"leaf_early": 64}, {"lane_priority": 0}])
 def test_claim_options_byte_identical(gpu_lib, opts):
     """Claim-order options of the persistent kernel (light units merged into 128-pixel items, heavy units
     split in halves / quarters, costs as the longest path, a 30 % grid): which wave traces a pixel changes,
