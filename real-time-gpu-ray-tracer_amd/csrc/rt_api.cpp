@@ -291,6 +291,7 @@ struct rt_scene {
     // hardware queues of their own, so 4 lanes run side by side at the default GPU_MAX_HW_QUEUES (4) — C2 0.256 ->
     // 0.180 ms/frame, C3 2.15 -> 1.54, a 1/8 share 0.064 -> 0.046 — as at 12 queues (profiles/r05/lanes/)
     bool lane_priority = true;
+    bool scene_priority = false;    // option "scene_priority" (set before rt_scene_build): the scene stream at the highest
     bool stage_depth_set = false;   // option "stage_depth" given explicitly (auto lanes leave it alone)
     hipEvent_t ev_lane_done[NLANE] = {};   // last trace launch of each lane finished
     uint32_t cus = 0;
@@ -1353,7 +1354,11 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     for (const auto &r : s->roughs) { mats.push_back(r.albedo.x); mats.push_back(r.albedo.y); mats.push_back(r.albedo.z); mats.push_back(0.0f); }
     for (const auto &m : s->metals) { mats.push_back(m.albedo.x); mats.push_back(m.albedo.y); mats.push_back(m.albedo.z); mats.push_back(m.fuzz); }
     rt_status st;
-    if (!s->stream) HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
+    if (!s->stream) {
+        int lo = 0, hi = 0;                        // option "scene_priority": the scene stream (uploads, GPU BLAS builds)
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIP_TRY(hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, s->scene_priority ? hi : 0));
+    }
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
     if (!s->r_done) s->r_done = s->ev_render_done;
     for (bool &v : s->sched_valid) v = false;
@@ -2181,6 +2186,10 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "leaf_early") {
         if (value < -1 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "leaf_early must be -1 (auto) or 0..64");
         s->leaf_early = (int)value;
+    } else if (k == "scene_priority") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "scene_priority must be 0 or 1");
+        if (s->stream) return fail(RT_ERR_STATE, "scene_priority is set before rt_scene_build");
+        s->scene_priority = value == 1;
     } else if (k == "lane_priority") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "lane_priority must be 0 or 1");
         RT_TRY(drain(s));

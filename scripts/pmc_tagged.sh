@@ -9,6 +9,12 @@ export TMPDIR=/tmp
 mkdir -p "$OUT"
 python3 bench.py "$@" --print-pmc-tag > "$OUT/tag.json" || exit 1
 PASSES=("FETCH_SIZE" "WRITE_SIZE" ${PMC_EXTRA:+"$PMC_EXTRA"})
+if [ "${PMC_SET:-}" = "deep" ]; then   # occupancy, lane utilisation, L2 / L1 behaviour of the same workload (verdict r4 3)
+  PASSES+=("SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE"
+           "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VMEM"
+           "TCC_HIT_sum TCC_MISS_sum SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"
+           "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum TCP_PENDING_STALL_CYCLES_sum")
+fi
 dirs=()
 i=0
 for p in "${PASSES[@]}"; do
