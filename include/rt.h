@@ -338,6 +338,8 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *   "lane_priority": the lane streams the scene creates for "overlap" frames without a caller stream: 1 (default) =
  *                 the device's highest stream priority (hardware queues of their own: full overlap at the default
  *                 GPU_MAX_HW_QUEUES of 4), 0 = normal priority
+ *   "scene_priority": 1 = create the scene stream (uploads, GPU tree builds) at the device's highest priority;
+ *                 0 (default).  Set before rt_scene_build (RT_ERR_STATE after)
  *   "tlas_sah"  : RT_BUILD_SAH: 1 (default) = build the per-frame host TLAS with SAH; 0 = the reference's median split
  *                 (TLAS.cu:4-129; "tlas_median_leaf" 1..2 = its leaf size, 0 = the reference's 2)
  *   "tlas_leaf" : instances per leaf of an SAH or GPU-built TLAS (1..4, default 1; GPU-built TLASes: set before
