@@ -163,3 +163,22 @@ def test_null_stream_device_outputs_ordered(gpu_lib, lanes):
     for it, c in enumerate(copies):
         assert np.array_equal(c.cpu().numpy().reshape(H, W, 4), ref[it % 4]), it
     r.cleanup()
+
+
+def test_synchronous_frame_after_pipelined_frames(gpu_lib):
+    """A synchronous call behind NO_SYNC frames still in flight on the scene's own lanes (auto overlap): every frame
+    equals its single-launch render, three bursts in a row."""
+    import torch
+    s = scenes.demo_with_particles(10)
+    W, H = 320, 184
+    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(W, H, ray_trace_depth=2)
+    ref = [r.render(f)[0] for f in range(6)]
+    r.set_option("overlap", -1)
+    outs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(6)]
+    for it in range(3):
+        for f in range(6):
+            r.render(f, want_rgba=False, rgba8_device=outs[f].data_ptr(), sync=(f == 5))
+        r.synchronize()
+        for f in range(6):
+            assert np.array_equal(outs[f].cpu().numpy().reshape(H, W, 4), ref[f]), (it, f)
+    r.cleanup()
