@@ -4,9 +4,10 @@ Tolerances:
   * EXACT mode (IEEE division, no FMA contraction) on identical trees: float RGB bit-identical,
     RGBA8 within 1 LSB (the GPU applies gamma with sqrtf, the reference with powf(x, 0.5)),
     identical work counters (rays, instance visits, primitive tests).
-  * FAST mode (default: quad traversal with reciprocal slab culls, the reference's arithmetic for every value
-    that reaches a hit or a pixel): on identical trees bit-identical like EXACT (full C2 / C3 frames:
-    tests/test_gpu_parity_full.py); on other trees (SAH / LBVH: ties in the 1e-6 window) RGBA8 |d| <= 1 on
+  * FAST mode (default: quad traversal with reciprocal slab culls whose marginal decisions are re-taken with the
+    reference's slab, the reference's arithmetic for every value that reaches a hit or a pixel): on identical trees
+    bit-identical like EXACT (full frames: tests/test_gpu_parity_full.py; the crops, the C3-settings frame and the
+    20k closest hits below); on other trees (SAH / LBVH: ties in the 1e-6 window) RGBA8 |d| <= 1 on
     >= 99.9 % of pixels at depth 1-2 and >= 99.5 % at depth >= 4 on these small scenes; per-ray closest hit
     identical on >= 99.9 % of rays with |dt| <= 1e-4 * t.  Option "fast_math" (hardware reciprocals, FMA) is
     held to the same small-scene tolerance.
@@ -112,8 +113,8 @@ def test_fast_mode_within_tolerance_demo(gpu_lib, depth, need):
 
 
 def test_fast_mode_c2_crop(gpu_lib):
-    """C2 (1080p, 1 spp, depth 2, 68 particles): full GPU frame vs oracle on the particle crop
-    and a ground/sky crop."""
+    """C2 (1080p, 1 spp, depth 2, 68 particles) on the reference's trees: the FAST frame's float RGB equals the
+    oracle's on the particle crop and a ground/sky crop (round 5: marginal box decisions re-taken exactly)."""
     cfg = scenes.CONFIGS["C2"]
     s = scenes.config_scene(cfg)
     r, o = pair(s, 0, cfg.width, cfg.height)
@@ -121,8 +122,9 @@ def test_fast_mode_c2_crop(gpu_lib):
     assert st["pixels"] == cfg.width * cfg.height
     for x0, y0, w, h in ((800, 620, 320, 160), (0, 0, 256, 128)):
         orgb, orgba, _ = o.render(region=(x0, y0, w, h), threads=THREADS)
-        f, mx = frac_within(rgba[y0:y0 + h, x0:x0 + w], orgba)
-        assert f >= 0.999, (f, mx)
+        crop = rgb[y0:y0 + h, x0:x0 + w]
+        assert (crop != orgb).any(axis=2).sum() == 0, float(np.abs(crop - orgb).max())
+        assert frac_within(rgba[y0:y0 + h, x0:x0 + w], orgba)[0] == 1.0
 
 
 def test_c3_settings_spp4_depth4_crop(gpu_lib):
@@ -130,8 +132,8 @@ def test_c3_settings_spp4_depth4_crop(gpu_lib):
     r, o = pair(s, 1, 320, 180, sample_count=4, ray_trace_depth=4)
     rgba, rgb, st = r.render(0, want_rgb=True)
     orgb, orgba, ocnt = o.render(threads=THREADS)
-    f, mx = frac_within(rgba, orgba)
-    assert f >= 0.995, (f, mx)
+    assert (rgb != orgb).any(axis=2).sum() == 0, float(np.abs(rgb - orgb).max())   # FAST on the reference's trees
+    assert frac_within(rgba, orgba)[0] == 1.0
     rgba_e, rgb_e, st_e = r.render(0, exact=True, want_rgb=True)
     assert (rgb_e != orgb).any(axis=2).sum() == 0
     assert st_e["rays"] == ocnt["rays"]
@@ -180,11 +182,10 @@ def test_trace_rays_exact_and_fast(gpu_lib):
     for k in ("t", "instance", "pindex", "ptype", "mtype", "midx"):
         assert np.array_equal(eh[k], oh[k]), k
     assert np.array_equal(eh["point"], oh["point"]) and np.array_equal(eh["normal"], oh["normal"])
-    fh = r.trace_rays(rays)
-    same = (fh["instance"] == oh["instance"]) & (fh["pindex"] == oh["pindex"])
-    assert same.mean() >= 0.999
-    hit = same & (oh["instance"] != 0xFFFFFFFF)
-    assert np.all(np.abs(fh["t"][hit] - oh["t"][hit]) <= 1e-4 * oh["t"][hit])
+    fh = r.trace_rays(rays)                   # FAST on the reference's trees: the same closest hits, bit for bit
+    for k in ("t", "instance", "pindex", "ptype", "mtype", "midx"):
+        assert np.array_equal(fh[k], oh[k]), k
+    assert np.array_equal(fh["point"], oh["point"]) and np.array_equal(fh["normal"], oh["normal"])
 
 
 def test_tile_shards_assemble_to_full_frame(gpu_lib):
