@@ -268,12 +268,12 @@ def main():
     for kv in args.pre_opt:
         k, v = kv.split("=")
         r.set_option(k, int(v, 0))
+    if args.rebuild:                  # before the build: the build then leaves out the cold triangle records (auto)
+        r.set_option("rebuild", 1)
     r.build_acceleration_structure(0, mode=args.build).configure_camera(cfg.width, cfg.height)
     r.set_option("kernel", args.kernel)
     if args.threshold is not None:
         r.set_option("threshold", args.threshold)
-    if args.rebuild:
-        r.set_option("rebuild", 1)
     for kv in args.opt:
         k, v = kv.split("=")
         r.set_option(k, int(v, 0))

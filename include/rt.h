@@ -348,8 +348,8 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 binary levels per quad visited in the binary tree's order; RT_BUILD_SAH: the greedy collapse
  *                 visited by entry t), 0 = binary node pairs
  *   "cold_records": RT_BUILD_LBVH: 1 = the GPU builder writes TriCold records (normals, material, caller index) beside
- *                 TriHot; 0 (default) = a hit reads the caller's triangle instead (same pixels; set before
- *                 rt_scene_build)
+ *                 TriHot; 0 = a hit reads the caller's triangle instead; -1 (default) = 1 unless "rebuild" is 1 at
+ *                 rt_scene_build (same pixels either way; set before rt_scene_build, as is "rebuild" to take effect)
  *   "blas_sets" : RT_BUILD_LBVH rebuilds with "blas_double": BLAS sets cycled (2..3, default 3): frame k+1's rebuild
  *                 waits only for the trace of frame k + 1 - sets (set before rt_scene_build)
  *   "blas_leaf" : RT_BUILD_SAH: primitives per BLAS leaf (1..4, default 4; set before rt_scene_build)

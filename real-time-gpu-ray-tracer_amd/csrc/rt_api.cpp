@@ -194,8 +194,13 @@ struct rt_scene {
     // records (normals, material, caller index) as the host builders do; 0 = they write TriHot only, with the caller's
     // triangle index and group member in its pads, and a hit reads normals and material from the caller's triangle
     // (SceneGPU::raw_tris) — a C5 rebuild's leaf-ordered gather then moves about half the bytes
-    bool cold_records = false;
-    bool raw_shading() const { return build_mode == RT_BUILD_LBVH && !cold_records; }
+    // -1 (auto, default): 1 when the BLASes are built once (option "rebuild" 0 at rt_scene_build: a hit's normals and
+    // material are then one dependent HBM round trip nearer — C5 static 4.97 -> 4.80 ms/frame, C2-LBVH -1 %), 0 when
+    // they are rebuilt every frame (the rebuild's gather moves half the bytes: C5 8.36 against 8.52;
+    // profiles/r05/cold_records/)
+    int cold_records = -1;
+    bool cold_eff = false;          // the build's choice (rt_scene_build)
+    bool raw_shading() const { return build_mode == RT_BUILD_LBVH && !cold_eff; }
     uint32_t wide_merge = 0;        // quad trees: binary subtrees of <= wide_merge items become one leaf (set before build)
     DevBuf<TriHot> tri_hot;
     DevBuf<TriCold> tri_cold;
@@ -1077,7 +1082,7 @@ rt_status gpu_setup_blas(rt_scene *s, const uint32_t *slot_count) {
     if ((st = upload(s->raw_sph, s->spheres)) != RT_OK) return st;
     if ((st = upload(s->raw_quad, s->quads)) != RT_OK) return st;
     if ((st = alloc_buf(s->tri_hot, slot_count[RT_PRIM_TRIANGLE])) != RT_OK) return st;
-    if (s->cold_records) {
+    if (s->cold_eff) {
         if ((st = alloc_buf(s->tri_cold, slot_count[RT_PRIM_TRIANGLE])) != RT_OK) return st;
     } else {
         s->tri_cold.release();                          // raw_shading(): no TriCold records
@@ -1182,6 +1187,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     if (s->built) RT_TRY(drain(s));              // a rebuild frees buffers earlier frames may still read
     s->build_seed = seed;
     s->build_mode = mode;
+    s->cold_eff = s->cold_records == 1 || (s->cold_records < 0 && !s->rebuild_blas);
     s->inst.clear();
     s->blas.clear();
     s->groups.clear();
@@ -2132,9 +2138,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
         s->costmap_on = value == 1;
     } else if (k == "cold_records") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "cold_records must be 0 or 1");
+        if (value < -1 || value > 1) return fail(RT_ERR_INVALID_ARGUMENT, "cold_records must be -1, 0 or 1");
         if (s->built) return fail(RT_ERR_STATE, "cold_records must be set before rt_scene_build");
-        s->cold_records = value == 1;
+        s->cold_records = (int)value;
     } else if (k == "blas_sets") {
         if (value != 2 && value != 3) return fail(RT_ERR_INVALID_ARGUMENT, "blas_sets must be 2 or 3");
         RT_TRY(drain(s));

@@ -25,9 +25,9 @@ def main():
     for kv in a.pre_opt:
         k, v = kv.split("=")
         r.set_option(k, int(v))
+    r.set_option("rebuild", 1)                           # before the build (no cold records, as bench.py)
     r.build_acceleration_structure(0, mode="lbvh")
     r.configure_camera(cfg.width, cfg.height, sample_count=cfg.spp, ray_trace_depth=cfg.depth)
-    r.set_option("rebuild", 1)
     for kv in a.opt:
         k, v = kv.split("=")
         r.set_option(k, int(v))

@@ -117,8 +117,8 @@ def test_c5_lbvh_per_frame_rebuild(gpu_lib):
     assert n_tris == P * 1024 + 1
     W, H = cfg.width, cfg.height
     x0, y0, w, h = 1600, 1240, 512, 256                                 # over the particle cluster
-    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(W, H)
-    r.set_option("rebuild", 1)
+    r = Renderer(s).set_option("rebuild", 1)            # before the build, as bench.py: no cold triangle records
+    r.build_acceleration_structure(0, mode="lbvh").configure_camera(W, H)
     info = r.info()
     assert info["sqrt_sample_count"] == 2                                # 8 requested -> 4 traced (RenderPin.cu:93)
     assert info["blas_count"] == 4 + P                                   # 2 spheres, quad, demo triangle + particles
@@ -138,7 +138,7 @@ def test_c5_lbvh_per_frame_rebuild(gpu_lib):
     assert np.array_equal(orig1, orig)                                   # the rebuild is deterministic
     assert st0["pixels"] == W * H
     r.cleanup()
-    # a scene built once (no per-frame rebuild) traces the same trees: same frame bytes
+    # a scene built once (no per-frame rebuild: cold triangle records by default) traces the same trees: same bytes
     r2 = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(W, H)
     g1, _, _ = r2.render(1)
     assert np.array_equal(f1, g1)

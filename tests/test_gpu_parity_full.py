@@ -71,9 +71,10 @@ def bench_frames(scene, W, H, cam, name="C2", **opts):
     (C5: GPU LBVH with every BLAS rebuilt each frame, 2 lanes on new streams)."""
     import torch
     build, rebuild, L, classic = BENCH.get(name, ("sah", False, 4, False))
-    r = Renderer(scene).build_acceleration_structure(0, mode=build).configure_camera(W, H, **cam)
-    if rebuild:
+    r = Renderer(scene)
+    if rebuild:                       # set before the build, as bench.py does (the build then leaves out cold records)
         r.set_option("rebuild", 1)
+    r.build_acceleration_structure(0, mode=build).configure_camera(W, H, **cam)
     for k, v in opts.items():
         r.set_option(k, v)
     r.set_option("overlap", L)
