@@ -497,3 +497,24 @@ def test_small_tlas_equals_multi_kernel_tlas(gpu_lib, group):
             assert live == list(range(n - 12)) + [n], live         # the demo instances and the group record
     a.cleanup()
     b.cleanup()
+
+
+@pytest.mark.parametrize("rebuild", [0, 1])
+def test_cold_records_auto_same_frames(gpu_lib, rebuild):
+    """Option "cold_records" auto (-1): cold triangle records when the GPU-built BLASes are built once, none with a
+    per-frame rebuild ("rebuild" set before the build).  Every policy renders the same bytes, FAST and EXACT, and the
+    auto build holds TriCold records exactly when it should (device_bytes)."""
+    s = scenes.demo_with_particles(6)
+    frames = {}
+    dev = {}
+    for cold in (-1, 0, 1):
+        r = Renderer(s).set_option("cold_records", cold).set_option("rebuild", rebuild)
+        r.build_acceleration_structure(0, mode="lbvh").configure_camera(96, 64, ray_trace_depth=2)
+        frames[cold] = [r.render(f, exact=e)[0] for f in (0, 37) for e in (False, True)]
+        dev[cold] = r.info()["device_bytes"]
+        r.cleanup()
+    for cold in (0, 1):
+        for a, b in zip(frames[-1], frames[cold]):
+            assert np.array_equal(a, b), cold
+    assert dev[-1] == (dev[0] if rebuild else dev[1]), dev
+    assert dev[1] > dev[0], dev
