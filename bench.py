@@ -237,7 +237,7 @@ def main():
     # (profiles/r04/c5_rebuild/r04s16_*)
     w, h, spp = FRAME_DIMS[args.config]
     big = w * h * int(spp ** 0.5) ** 2 >= (16 << 20)
-    classic = not share and not args.attach_comm and args.rebuild and not big
+    classic = args.lanes == "caller" and not share and not args.attach_comm and args.rebuild and not big
     # with a communicator attached (N > 1, --attach-comm) RCCL's own streams take hardware queues as well: at 12
     # two of three lanes shared one queue and ran back to back (world-1 comm path 0.29 ms/frame, 0.22 at 16-24;
     # 1/8 shares 0.045 -> 0.043; profiles/r03_session2/comm_world1_hwq.jsonl)
@@ -287,8 +287,8 @@ def main():
     # runs frames rendered without a stream on streams of its own; a C2-LBVH-style rebuild of a small frame ("classic")
     # keeps the caller's null stream as lane 0, which only a caller can hand it
     lib_lanes = args.lanes == "library" and not classic and args.lane_priority is None
-    L = max(1, args.overlap if args.overlap is not None else
-            (8 if share else (3 if classic else (2 if args.rebuild and big else 4))))
+    # (round 5: any per-frame rebuild, 2 — C5 1/8 share 5.5 -> 4.1 ms/frame, C2-LBVH 1.04 -> 0.38; profiles/r05/c5_rebuild/)
+    L = max(1, args.overlap if args.overlap is not None else (2 if args.rebuild else (8 if share else 4)))
     overlap = L > 1
     if lib_lanes and args.overlap is None:
         r.set_option("overlap", -1)

@@ -1652,14 +1652,14 @@ rt_status rt_scene_detach_comm(rt_scene *s) {
 }
 
 // Option "overlap" -1: the lane count (and staging depth) bench.py measured best per frame kind:
-// a rank's share of a multi-GPU frame (tiles, or a communicator of world > 1) 8 lanes and 64 staging buffers; a
-// launch of >= BIG_LAUNCH_PATHS camera paths with a per-frame BLAS rebuild 2 lanes (the rebuild finds slots between
-// two traces); any other frame 4 lanes.  Changing the count drains the scene (a new frame kind, e.g. attaching a
-// communicator).
+// with a per-frame BLAS rebuild 2 lanes (the rebuild is the frame's critical path and starves behind traces in
+// flight: C5 8.8 against 9.8 ms/frame with 4 lanes; a C5 1/8 share 4.1 against 5.5 with 8; C2-LBVH 0.38 against 1.04
+// with 3; profiles/r04/c5_rebuild/, profiles/r05/c5_rebuild/); else a rank's share of a multi-GPU frame (tiles, or a
+// communicator of world > 1) 8 lanes and 64 staging buffers, any other frame 4 lanes.  Changing the count drains the
+// scene (a new frame kind, e.g. attaching a communicator).
 rt_status auto_lanes(rt_scene *s, const rt_render_opts &o) {
     const bool share = o.tile_count > 0 || (s->comm && s->comm->world > 1);
-    const uint64_t paths = (uint64_t)s->width * s->height * s->cam.sqrt_s * s->cam.sqrt_s;
-    const uint32_t L = share ? 8u : (s->rebuild_blas && paths >= rt_scene::BIG_LAUNCH_PATHS ? 2u : 4u);
+    const uint32_t L = s->rebuild_blas ? 2u : (share ? 8u : 4u);
     const int depth = share ? rt_scene::NSTAGE : 2 * rt_scene::NLANE;
     if (L == s->lanes && (s->stage_depth_set || depth == s->stage_depth)) return RT_OK;
     RT_TRY(drain(s));
