@@ -389,8 +389,8 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  *                 lane and for its frame block, so frame k+1's launch runs in the CUs frame k's tail
  *                 leaves idle.  Frames with opts.stream NULL run on lane streams the scene creates; a
  *                 caller that passes streams cycles its own.  -1 = auto: the scene also picks L and the
- *                 staging depth per frame kind (8 lanes / 64 buffers for a rank's tile share, 2 lanes for
- *                 a >= 16 M-path frame with a per-frame rebuild, else 4).  With lanes the caller orders
+ *                 staging depth per frame kind (2 lanes with a per-frame rebuild, else 8 lanes / 64
+ *                 buffers for a rank's tile share, else 4).  With lanes the caller orders
  *                 its own output buffers: device outputs of NO_SYNC frames without a stream are complete
  *                 once rt_synchronize returns (default 0 = 1 lane: every launch of the scene is serialised) */
 rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
