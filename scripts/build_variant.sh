@@ -9,7 +9,7 @@ make -s
 NAME=$1; FLAGS=$2
 HIPCC=/opt/rocm/bin/hipcc
 $HIPCC -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -DRT_EXACT=0 -DRT_FAST_IEEE=1 -ffp-contract=off $FLAGS \
-  -I. -c ${SRC:-trace_kernel.hip} -o ../build/trace_fast_$NAME.o
+  -I. -I$PWD -c ${SRC:-trace_kernel.hip} -o ../build/trace_fast_$NAME.o
 objs=""
 for o in rt_api trace_exact trace_fastmath assemble schedule lbvh vtk_reader comm instances interactive; do objs="$objs ../build/$o.o"; done
 $HIPCC -shared -fPIC --offload-arch=gfx950 -o ../lib/librtamd_$NAME.so $objs ../build/trace_fast_$NAME.o -ldl
