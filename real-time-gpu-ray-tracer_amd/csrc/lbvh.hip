@@ -286,13 +286,81 @@ __global__ __launch_bounds__(BLOCK) void local_sort_kernel(const LbvhSeg *segs, 
     }
 }
 
+// Leaf-ordered BLAS records (rt_api.cpp builds the same records on the host: Triangle.cuh:26-46,
+// Parallelogram.cuh:26-39).
+__device__ __forceinline__ uint32_t material_slot(uint32_t type, uint32_t index, uint32_t rough_count) {
+    return type == RT_MAT_ROUGH ? index : ((rough_count + index) | MAT_METAL_BIT);
+}
+
+__device__ __forceinline__ void gather_item(const LbvhSeg &S, uint32_t p, const uint32_t *vals, const RawPrimsGPU &raw,
+                                            const PrimOutGPU &out, const uint32_t *item_member) {
+    const uint32_t slot = S.slot_base + (p - S.item_base);
+    const uint32_t prim = S.prim_base + (vals[p] - S.item_base);
+    if (S.ptype == RT_PRIM_TRIANGLE) {
+        const float *tv = raw.tri_verts + 9 * (size_t)prim;
+        const V3 v0 = v3(tv[0], tv[1], tv[2]);
+        const V3 e1 = v3(tv[3], tv[4], tv[5]) - v0, e2 = v3(tv[6], tv[7], tv[8]) - v0;
+        const uint32_t member = S.member_count ? item_member[vals[p]] : 0u;   // a group's BLAS: member instance + 1
+        TriHot H;
+        H.v0[0] = v0.x; H.v0[1] = v0.y; H.v0[2] = v0.z; H.pad0 = 0.0f;
+        H.e1[0] = e1.x; H.e1[1] = e1.y; H.e1[2] = e1.z; H.pad1 = 0.0f;
+        H.e2[0] = e2.x; H.e2[1] = e2.y; H.e2[2] = e2.z; H.pad2 = 0.0f;
+        if (!out.tri_cold) {                          // no cold records: the index and member ride in the pads
+            H.pad0 = __uint_as_float(prim);
+            H.pad1 = __uint_as_float(member);
+            out.tri_hot[slot] = H;
+            return;
+        }
+        const rt_triangle &t = raw.tris[prim];
+        V3 nn[3];
+        if (t.has_normals) { nn[0] = of(t.normal[0]); nn[1] = of(t.normal[1]); nn[2] = of(t.normal[2]); }
+        else { const V3 u = unit(cross(e1, e2)); nn[0] = u; nn[1] = u; nn[2] = u; }
+        TriCold C;
+        C.n0[0] = nn[0].x; C.n0[1] = nn[0].y; C.n0[2] = nn[0].z;
+        C.n1[0] = nn[1].x; C.n1[1] = nn[1].y; C.n1[2] = nn[1].z;
+        C.n2[0] = nn[2].x; C.n2[1] = nn[2].y; C.n2[2] = nn[2].z;
+        C.material = material_slot(t.material_type, t.material_index, raw.rough_count);
+        C.orig_index = prim;
+        C.pad = member;
+        out.tri_hot[slot] = H;
+        out.tri_cold[slot] = C;
+    } else if (S.ptype == RT_PRIM_SPHERE) {
+        const rt_sphere sp = raw.spheres[prim];
+        SphereHot H;
+        H.center[0] = sp.center.x; H.center[1] = sp.center.y; H.center[2] = sp.center.z; H.radius = sp.radius;
+        PrimCold C;
+        C.material = material_slot(sp.material_type, sp.material_index, raw.rough_count);
+        C.orig_index = prim; C.pad0 = 0; C.pad1 = 0;
+        out.sph_hot[slot] = H;
+        out.sph_cold[slot] = C;
+    } else {
+        const rt_parallelogram q = raw.quads[prim];
+        const V3 nx = cross(of(q.u), of(q.v));
+        const V3 nn = unit(nx);
+        float d = 0.0f;
+        d += nn.x * q.q.x; d += nn.y * q.q.y; d += nn.z * q.q.z;
+        QuadHot H;
+        H.n[0] = nn.x; H.n[1] = nn.y; H.n[2] = nn.z; H.d = d;
+        H.q[0] = q.q.x; H.q[1] = q.q.y; H.q[2] = q.q.z; H.den = dot(nx, nx);
+        H.u[0] = q.u.x; H.u[1] = q.u.y; H.u[2] = q.u.z; H.pad0 = 0.0f;
+        H.v[0] = q.v.x; H.v[1] = q.v.y; H.v[2] = q.v.z; H.pad1 = 0.0f;
+        H.nx[0] = nx.x; H.nx[1] = nx.y; H.nx[2] = nx.z; H.pad2 = 0.0f;
+        PrimCold C;
+        C.material = material_slot(q.material_type, q.material_index, raw.rough_count);
+        C.orig_index = prim; C.pad0 = 0; C.pad1 = 0;
+        out.quad_hot[slot] = H;
+        out.quad_cold[slot] = C;
+    }
+}
+
 // Karras 2012, one thread per interior node.  Local indices are positions inside the segment.  The sorted codes
 // within KWIN positions of the workgroup's own are staged in LDS first: nearly every node's searches stay inside
 // that window (a range of <= KWIN / 2 items), so a search step is an LDS read, not a dependent global load.
 constexpr int KWIN = 256;
 __global__ __launch_bounds__(BLOCK) void karras_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *keys,
                                                        uint32_t n, uint32_t *child, uint32_t *parent, uint32_t *parent_leaf,
-                                                       uint32_t *range, uint32_t *flag) {
+                                                       uint32_t *range, uint32_t *flag, const uint32_t *vals, RawPrimsGPU raw,
+                                                       PrimOutGPU out, const uint32_t *item_member, uint32_t gather) {
     __shared__ uint32_t skey[BLOCK + 2 * KWIN];
     const int64_t w0 = (int64_t)blockIdx.x * BLOCK - KWIN;       // position of skey[0]
     for (int k = threadIdx.x; k < BLOCK + 2 * KWIN; k += BLOCK) {
@@ -303,6 +371,8 @@ __global__ __launch_bounds__(BLOCK) void karras_kernel(const LbvhSeg *segs, cons
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
     if (p >= n) return;
     const LbvhSeg S = segs[seg_of[p]];
+    // fused BLAS gather (build() with raw / out): item p's leaf-ordered record; its loads overlap the searches below
+    if (gather) gather_item(S, p, vals, raw, out, item_member);
     const int m = (int)S.count;
     const int i = (int)(p - S.item_base);
     if (m == 1) { parent_leaf[p] = NONE; return; }
@@ -648,75 +718,7 @@ __global__ void roots_kernel(const LbvhSeg *segs, uint32_t n_segs, const uint32_
     roots[s] = R;
 }
 
-// Leaf-ordered BLAS records (rt_api.cpp builds the same records on the host: Triangle.cuh:26-46,
-// Parallelogram.cuh:26-39).
-__device__ __forceinline__ uint32_t material_slot(uint32_t type, uint32_t index, uint32_t rough_count) {
-    return type == RT_MAT_ROUGH ? index : ((rough_count + index) | MAT_METAL_BIT);
-}
 
-__global__ void gather_blas_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *vals, uint32_t n,
-                                   RawPrimsGPU raw, PrimOutGPU out, const uint32_t *item_member) {
-    const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
-    if (p >= n) return;
-    const LbvhSeg S = segs[seg_of[p]];
-    const uint32_t slot = S.slot_base + (p - S.item_base);
-    const uint32_t prim = S.prim_base + (vals[p] - S.item_base);
-    if (S.ptype == RT_PRIM_TRIANGLE) {
-        const float *tv = raw.tri_verts + 9 * (size_t)prim;
-        const V3 v0 = v3(tv[0], tv[1], tv[2]);
-        const V3 e1 = v3(tv[3], tv[4], tv[5]) - v0, e2 = v3(tv[6], tv[7], tv[8]) - v0;
-        const uint32_t member = S.member_count ? item_member[vals[p]] : 0u;   // a group's BLAS: member instance + 1
-        TriHot H;
-        H.v0[0] = v0.x; H.v0[1] = v0.y; H.v0[2] = v0.z; H.pad0 = 0.0f;
-        H.e1[0] = e1.x; H.e1[1] = e1.y; H.e1[2] = e1.z; H.pad1 = 0.0f;
-        H.e2[0] = e2.x; H.e2[1] = e2.y; H.e2[2] = e2.z; H.pad2 = 0.0f;
-        if (!out.tri_cold) {                          // no cold records: the index and member ride in the pads
-            H.pad0 = __uint_as_float(prim);
-            H.pad1 = __uint_as_float(member);
-            out.tri_hot[slot] = H;
-            return;
-        }
-        const rt_triangle &t = raw.tris[prim];
-        V3 nn[3];
-        if (t.has_normals) { nn[0] = of(t.normal[0]); nn[1] = of(t.normal[1]); nn[2] = of(t.normal[2]); }
-        else { const V3 u = unit(cross(e1, e2)); nn[0] = u; nn[1] = u; nn[2] = u; }
-        TriCold C;
-        C.n0[0] = nn[0].x; C.n0[1] = nn[0].y; C.n0[2] = nn[0].z;
-        C.n1[0] = nn[1].x; C.n1[1] = nn[1].y; C.n1[2] = nn[1].z;
-        C.n2[0] = nn[2].x; C.n2[1] = nn[2].y; C.n2[2] = nn[2].z;
-        C.material = material_slot(t.material_type, t.material_index, raw.rough_count);
-        C.orig_index = prim;
-        C.pad = member;
-        out.tri_hot[slot] = H;
-        out.tri_cold[slot] = C;
-    } else if (S.ptype == RT_PRIM_SPHERE) {
-        const rt_sphere sp = raw.spheres[prim];
-        SphereHot H;
-        H.center[0] = sp.center.x; H.center[1] = sp.center.y; H.center[2] = sp.center.z; H.radius = sp.radius;
-        PrimCold C;
-        C.material = material_slot(sp.material_type, sp.material_index, raw.rough_count);
-        C.orig_index = prim; C.pad0 = 0; C.pad1 = 0;
-        out.sph_hot[slot] = H;
-        out.sph_cold[slot] = C;
-    } else {
-        const rt_parallelogram q = raw.quads[prim];
-        const V3 nx = cross(of(q.u), of(q.v));
-        const V3 nn = unit(nx);
-        float d = 0.0f;
-        d += nn.x * q.q.x; d += nn.y * q.q.y; d += nn.z * q.q.z;
-        QuadHot H;
-        H.n[0] = nn.x; H.n[1] = nn.y; H.n[2] = nn.z; H.d = d;
-        H.q[0] = q.q.x; H.q[1] = q.q.y; H.q[2] = q.q.z; H.den = dot(nx, nx);
-        H.u[0] = q.u.x; H.u[1] = q.u.y; H.u[2] = q.u.z; H.pad0 = 0.0f;
-        H.v[0] = q.v.x; H.v[1] = q.v.y; H.v[2] = q.v.z; H.pad1 = 0.0f;
-        H.nx[0] = nx.x; H.nx[1] = nx.y; H.nx[2] = nx.z; H.pad2 = 0.0f;
-        PrimCold C;
-        C.material = material_slot(q.material_type, q.material_index, raw.rough_count);
-        C.orig_index = prim; C.pad0 = 0; C.pad1 = 0;
-        out.quad_hot[slot] = H;
-        out.quad_cold[slot] = C;
-    }
-}
 
 __global__ void gather_items_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *vals, uint32_t n,
                                     uint32_t *slots) {
@@ -1161,7 +1163,8 @@ hipError_t LbvhBuilder::set_items(const float *boxes, const float4 *centroids) {
     return hipSuccess;
 }
 
-hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_count, hipStream_t stream) {
+hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_count, hipStream_t stream,
+                              const RawPrimsGPU *raw, const PrimOutGPU *out) {
     if (!box_ || !cent_ || n_items_ == 0) return hipErrorInvalidValue;
     const uint32_t N = n_items_, NI = n_items_ - n_segs_;
     hipLaunchKernelGGL(init_bounds_kernel, dim3(blocks_for(6ull * n_segs_)), dim3(BLOCK), 0, stream, bounds_, n_segs_);
@@ -1184,7 +1187,8 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
                                          end_bit, stream));
     }
     hipLaunchKernelGGL(karras_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, seg_of_, k1_, N, child_, parent_,
-                       parent_leaf_, range_, flag_);
+                       parent_leaf_, range_, flag_, v1_, raw ? *raw : RawPrimsGPU{}, out ? *out : PrimOutGPU{}, item_member_,
+                       (uint32_t)(raw && out));
     hipLaunchKernelGGL(bottom_up_local_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, v1_, box_, child_, parent_,
                        parent_leaf_, range_, nbox_, height_, kept_);
     if (max_count_ > LOCAL_MAX) {
@@ -1211,12 +1215,6 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
     }
     hipLaunchKernelGGL(roots_kernel, dim3(blocks_for(n_segs_)), dim3(BLOCK), 0, stream, segs_, n_segs_, v1_, box_, nbox_,
                        height_, pidx_, roots);
-    return hipGetLastError();
-}
-
-hipError_t LbvhBuilder::gather_blas(const RawPrimsGPU &raw, const PrimOutGPU &out, hipStream_t stream) {
-    hipLaunchKernelGGL(gather_blas_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, seg_of_, v1_, n_items_,
-                       raw, out, item_member_);
     return hipGetLastError();
 }
 

@@ -102,10 +102,11 @@ public:
 
     // Builds every segment: pairs written from index 0 of `pairs` (capacity max_pairs()),
     // roots[s] receives segment s's root; `pair_count` (device, may be null) the pairs written.
-    hipError_t build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_count, hipStream_t stream);
+    // With `raw` / `out` (BLAS builds), the leaf-ordered primitive records are written by the Karras kernel as well
+    // (one launch and one pass over the sorted items fewer than a separate gather).
+    hipError_t build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_count, hipStream_t stream,
+                     const RawPrimsGPU *raw = nullptr, const PrimOutGPU *out = nullptr);
 
-    // After build(): leaf-ordered BLAS primitive records.
-    hipError_t gather_blas(const RawPrimsGPU &raw, const PrimOutGPU &out, hipStream_t stream);
     // After build(): the 4-wide form of every tree (quads[q] = the quad rooted at node pair q, capacity
     // max_pairs()); roots_wide (may be null) receives each tree's root for the quad traversal.
     hipError_t collapse_wide(const NodePair *pairs, const TreeRoot *roots, NodeQuad *quads, TreeRoot *roots_wide,

@@ -1035,9 +1035,8 @@ rt_status gpu_build_blas(rt_scene *s) {
         const PrimOutGPU out{sp.tri_hot.p, s->raw_shading() ? nullptr : sp.tri_cold.p, sp.sph_hot.p, sp.sph_cold.p,
                              sp.quad_hot.p, sp.quad_cold.p};
         HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
-        HIP_TRY(s->blas_builder->build(sp.pairs.p, sp.roots.p, s->gpu_counts.p, s->stream));
+        HIP_TRY(s->blas_builder->build(sp.pairs.p, sp.roots.p, s->gpu_counts.p, s->stream, &raw, &out));   // + gather
         HIP_TRY(s->blas_builder->collapse_wide(sp.pairs.p, sp.roots.p, sp.quads.p, nullptr, s->stream));
-        HIP_TRY(s->blas_builder->gather_blas(raw, out, s->stream));
         std::swap(s->blas_pairs, sp.pairs); std::swap(s->blas_quads, sp.quads); std::swap(s->blas_roots, sp.roots);
         std::swap(s->tri_hot, sp.tri_hot); std::swap(s->tri_cold, sp.tri_cold);
         std::swap(s->sph_hot, sp.sph_hot); std::swap(s->sph_cold, sp.sph_cold);
@@ -1055,9 +1054,8 @@ rt_status gpu_build_blas(rt_scene *s) {
     const PrimOutGPU out{s->tri_hot.p, s->raw_shading() ? nullptr : s->tri_cold.p, s->sph_hot.p, s->sph_cold.p,
                          s->quad_hot.p, s->quad_cold.p};
     HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
-    HIP_TRY(s->blas_builder->build(s->blas_pairs.p, s->blas_roots.p, s->gpu_counts.p, s->stream));
+    HIP_TRY(s->blas_builder->build(s->blas_pairs.p, s->blas_roots.p, s->gpu_counts.p, s->stream, &raw, &out));   // + gather
     HIP_TRY(s->blas_builder->collapse_wide(s->blas_pairs.p, s->blas_roots.p, s->blas_quads.p, nullptr, s->stream));
-    HIP_TRY(s->blas_builder->gather_blas(raw, out, s->stream));
     s->blas_dirty = false;
     s->blas_builds++;
     return RT_OK;

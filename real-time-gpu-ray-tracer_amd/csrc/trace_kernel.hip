@@ -141,7 +141,7 @@ __device__ __forceinline__ f3 unit(f3 a) {                   // Vec3.cuh:129-137
     return mk(a.x * f, a.y * f, a.z * f);
 }
 __device__ __forceinline__ float comp(f3 a, int i) { return i == 0 ? a.x : (i == 1 ? a.y : a.z); }
-// unit(e1 x e2) with the arithmetic the BLAS builders store a triangle's normals with (lbvh.hip gather_blas_kernel,
+// unit(e1 x e2) with the arithmetic the BLAS builders store a triangle's normals with (lbvh.hip gather_item,
 // host_math.hpp; Triangle.cuh:26-46): correctly rounded 1 / sqrt, no contraction, in every FAST variant
 __device__ __forceinline__ f3 tri_face_normal(f3 a, f3 b) {
 #pragma clang fp contract(off)
