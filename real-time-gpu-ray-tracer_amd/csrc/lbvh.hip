@@ -101,6 +101,17 @@ __device__ __forceinline__ void quad_box_centroid(const rt_parallelogram &p, Box
     c = of(p.q) + of(p.u) * 0.5f + of(p.v) * 0.5f;
 }
 
+// a triangle's hot record as gather_item writes it without cold records (caller index and member in the pads)
+__device__ __forceinline__ TriHot tri_hot_record(const float *tv, uint32_t prim, uint32_t member) {
+    const V3 v0 = v3(tv[0], tv[1], tv[2]);
+    const V3 e1 = v3(tv[3], tv[4], tv[5]) - v0, e2 = v3(tv[6], tv[7], tv[8]) - v0;
+    TriHot H;
+    H.v0[0] = v0.x; H.v0[1] = v0.y; H.v0[2] = v0.z; H.pad0 = __uint_as_float(prim);
+    H.e1[0] = e1.x; H.e1[1] = e1.y; H.e1[2] = e1.z; H.pad1 = __uint_as_float(member);
+    H.e2[0] = e2.x; H.e2[1] = e2.y; H.e2[2] = e2.z; H.pad2 = 0.0f;
+    return H;
+}
+
 // ---- Morton / ordered-float helpers --------------------------------------------------------
 __device__ __forceinline__ uint32_t f2o(float f) {          // order-preserving float -> uint
     const uint32_t u = __float_as_uint(f);
@@ -132,16 +143,21 @@ __global__ void init_bounds_kernel(uint32_t *bounds, uint32_t n_segs) {
     bounds[i] = (i & 1) ? 0u : 0xFFFFFFFFu;               // even: min slots, odd: max slots
 }
 
+// stage (optional, BLAS builds without cold records): each triangle item's TriHot record in item order, so the
+// gather after the sort reads one 48-B record per leaf slot instead of the vertices plus the member table
 __global__ void prep_blas_kernel(const LbvhSeg *segs, const uint32_t *seg_of, uint32_t n, RawPrimsGPU raw,
-                                 float *box, float4 *cent) {
+                                 float *box, float4 *cent, TriHot *stage, const uint32_t *item_member) {
     const uint32_t it = blockIdx.x * BLOCK + threadIdx.x;
     if (it >= n) return;
     const LbvhSeg S = segs[seg_of[it]];
     const uint32_t prim = S.prim_base + (it - S.item_base);
     Box bx;
     V3 c;
-    if (S.ptype == RT_PRIM_TRIANGLE) tri_box_centroid(raw.tri_verts + 9 * (size_t)prim, bx, c);
-    else if (S.ptype == RT_PRIM_SPHERE) sphere_box_centroid(raw.spheres[prim], bx, c);
+    if (S.ptype == RT_PRIM_TRIANGLE) {
+        const float *tv = raw.tri_verts + 9 * (size_t)prim;
+        tri_box_centroid(tv, bx, c);
+        if (stage) stage[it] = tri_hot_record(tv, prim, S.member_count ? item_member[it] : 0u);
+    } else if (S.ptype == RT_PRIM_SPHERE) sphere_box_centroid(raw.spheres[prim], bx, c);
     else quad_box_centroid(raw.quads[prim], bx, c);
 #pragma unroll
     for (int k = 0; k < 6; k++) box[6 * (size_t)it + k] = bx.b[k];
@@ -293,8 +309,12 @@ __device__ __forceinline__ uint32_t material_slot(uint32_t type, uint32_t index,
 }
 
 __device__ __forceinline__ void gather_item(const LbvhSeg &S, uint32_t p, const uint32_t *vals, const RawPrimsGPU &raw,
-                                            const PrimOutGPU &out, const uint32_t *item_member) {
+                                            const PrimOutGPU &out, const uint32_t *item_member, const TriHot *stage) {
     const uint32_t slot = S.slot_base + (p - S.item_base);
+    if (stage && S.ptype == RT_PRIM_TRIANGLE && !out.tri_cold) {     // prep staged the record in item order
+        out.tri_hot[slot] = stage[vals[p]];
+        return;
+    }
     const uint32_t prim = S.prim_base + (vals[p] - S.item_base);
     if (S.ptype == RT_PRIM_TRIANGLE) {
         const float *tv = raw.tri_verts + 9 * (size_t)prim;
@@ -360,7 +380,8 @@ constexpr int KWIN = 256;
 __global__ __launch_bounds__(BLOCK) void karras_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *keys,
                                                        uint32_t n, uint32_t *child, uint32_t *parent, uint32_t *parent_leaf,
                                                        uint32_t *range, uint32_t *flag, const uint32_t *vals, RawPrimsGPU raw,
-                                                       PrimOutGPU out, const uint32_t *item_member, uint32_t gather) {
+                                                       PrimOutGPU out, const uint32_t *item_member, const TriHot *stage,
+                                                       uint32_t gather) {
     __shared__ uint32_t skey[BLOCK + 2 * KWIN];
     const int64_t w0 = (int64_t)blockIdx.x * BLOCK - KWIN;       // position of skey[0]
     for (int k = threadIdx.x; k < BLOCK + 2 * KWIN; k += BLOCK) {
@@ -372,7 +393,7 @@ __global__ __launch_bounds__(BLOCK) void karras_kernel(const LbvhSeg *segs, cons
     if (p >= n) return;
     const LbvhSeg S = segs[seg_of[p]];
     // fused BLAS gather (build() with raw / out): item p's leaf-ordered record; its loads overlap the searches below
-    if (gather) gather_item(S, p, vals, raw, out, item_member);
+    if (gather) gather_item(S, p, vals, raw, out, item_member, stage);
     const int m = (int)S.count;
     const int i = (int)(p - S.item_base);
     if (m == 1) { parent_leaf[p] = NONE; return; }
@@ -1061,7 +1082,7 @@ static void dfree(T *&p) {
 }
 
 void LbvhBuilder::release() {
-    dfree(segs_); dfree(seg_of_); dfree(members_); dfree(item_member_); dfree(own_box_); dfree(own_cent_); dfree(bounds_);
+    dfree(segs_); dfree(seg_of_); dfree(members_); dfree(item_member_); dfree(own_box_); dfree(own_cent_); dfree(stage_); dfree(bounds_);
     dfree(k0_); dfree(k1_); dfree(v0_); dfree(v1_); dfree(child_); dfree(parent_); dfree(parent_leaf_);
     dfree(range_); dfree(flag_); dfree(height_); dfree(nbox_); dfree(kept_); dfree(pidx_); dfree(front_); dfree(count_); dfree(frontier_);
     last_count_ = nullptr;
@@ -1112,15 +1133,17 @@ hipError_t LbvhBuilder::init(const std::vector<LbvhSeg> &segs, hipStream_t strea
     return hipStreamSynchronize(stream);
 }
 
-hipError_t LbvhBuilder::prep_blas_items(const RawPrimsGPU &raw, hipStream_t stream) {
+hipError_t LbvhBuilder::prep_blas_items(const RawPrimsGPU &raw, hipStream_t stream, bool stage_hot) {
     if (!own_box_) {
         LB_TRY(dalloc(own_box_, 6 * (size_t)n_items_));
         LB_TRY(dalloc(own_cent_, n_items_));
     }
+    if (stage_hot && !stage_) LB_TRY(dalloc(stage_, n_items_));
     box_ = own_box_;
     cent_ = own_cent_;
+    stage_ready_ = stage_hot;
     hipLaunchKernelGGL(prep_blas_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, seg_of_, n_items_, raw,
-                       box_, cent_);
+                       box_, cent_, stage_hot ? stage_ : nullptr, item_member_);
     return hipGetLastError();
 }
 
@@ -1188,7 +1211,8 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
     }
     hipLaunchKernelGGL(karras_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, seg_of_, k1_, N, child_, parent_,
                        parent_leaf_, range_, flag_, v1_, raw ? *raw : RawPrimsGPU{}, out ? *out : PrimOutGPU{}, item_member_,
-                       (uint32_t)(raw && out));
+                       stage_ready_ ? stage_ : nullptr, (uint32_t)(raw && out));
+    stage_ready_ = false;
     hipLaunchKernelGGL(bottom_up_local_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, v1_, box_, child_, parent_,
                        parent_leaf_, range_, nbox_, height_, kept_);
     if (max_count_ > LOCAL_MAX) {

@@ -91,7 +91,8 @@ public:
     uint32_t max_pairs() const { return n_items_ > n_segs_ ? n_items_ - n_segs_ : 1u; }
 
     // BLAS items: boxes / centroids of the segments' primitives (reference box semantics).
-    hipError_t prep_blas_items(const RawPrimsGPU &raw, hipStream_t stream);
+    // stage_hot (BLAS builds without cold records): triangle records staged in item order for the next build()
+    hipError_t prep_blas_items(const RawPrimsGPU &raw, hipStream_t stream, bool stage_hot = false);
     // TLAS items: caller-provided boxes (6 floats per item) and centroids (4 floats per item).  An item whose
     // centroid has w != 0 is inactive (an instance group's member while the group is one item, or a broken
     // group): it is kept out of the centroid bounds and sorted behind every active item (its box must be all
@@ -128,6 +129,8 @@ private:
     float4 *cent_ = nullptr;
     float *own_box_ = nullptr;
     float4 *own_cent_ = nullptr;
+    TriHot *stage_ = nullptr;             // prep_blas_items(stage_hot): TriHot per item, item order
+    bool stage_ready_ = false;
     uint32_t *bounds_ = nullptr;          // 6 ordered-uint per segment (centroid bounds)
     uint32_t *k0_ = nullptr, *k1_ = nullptr;           // Morton codes (per item, then sorted within each segment)
     uint32_t *v0_ = nullptr, *v1_ = nullptr;

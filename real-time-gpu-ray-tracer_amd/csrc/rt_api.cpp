@@ -1034,7 +1034,7 @@ rt_status gpu_build_blas(rt_scene *s) {
         const RawPrimsGPU raw{s->raw_tris.p, s->raw_verts.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
         const PrimOutGPU out{sp.tri_hot.p, s->raw_shading() ? nullptr : sp.tri_cold.p, sp.sph_hot.p, sp.sph_cold.p,
                              sp.quad_hot.p, sp.quad_cold.p};
-        HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
+        HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream, !out.tri_cold));
         HIP_TRY(s->blas_builder->build(sp.pairs.p, sp.roots.p, s->gpu_counts.p, s->stream, &raw, &out));   // + gather
         HIP_TRY(s->blas_builder->collapse_wide(sp.pairs.p, sp.roots.p, sp.quads.p, nullptr, s->stream));
         std::swap(s->blas_pairs, sp.pairs); std::swap(s->blas_quads, sp.quads); std::swap(s->blas_roots, sp.roots);
@@ -1053,7 +1053,7 @@ rt_status gpu_build_blas(rt_scene *s) {
     const RawPrimsGPU raw{s->raw_tris.p, s->raw_verts.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
     const PrimOutGPU out{s->tri_hot.p, s->raw_shading() ? nullptr : s->tri_cold.p, s->sph_hot.p, s->sph_cold.p,
                          s->quad_hot.p, s->quad_cold.p};
-    HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream));
+    HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream, !out.tri_cold));
     HIP_TRY(s->blas_builder->build(s->blas_pairs.p, s->blas_roots.p, s->gpu_counts.p, s->stream, &raw, &out));   // + gather
     HIP_TRY(s->blas_builder->collapse_wide(s->blas_pairs.p, s->blas_roots.p, s->blas_quads.p, nullptr, s->stream));
     s->blas_dirty = false;
