@@ -28,5 +28,8 @@ def test_presorted_sah_equals_nodewise(checker, n, kind, leaf):
 
 
 def test_presorted_sah_is_faster_on_a_c3_tlas(checker):
-    r = json.loads(subprocess.run([checker, "258", "0", "1"], check=True, capture_output=True, text=True).stdout)
-    assert r["same"] == 1 and r["presort_ms"] < r["nodewise_ms"], r
+    # a wall-clock comparison on a shared CPU: the best of three runs of each builder (one run flaked once under load)
+    runs = [json.loads(subprocess.run([checker, "258", "0", "1"], check=True, capture_output=True, text=True).stdout)
+            for _ in range(3)]
+    assert all(r["same"] == 1 for r in runs), runs
+    assert min(r["presort_ms"] for r in runs) < min(r["nodewise_ms"] for r in runs), runs
