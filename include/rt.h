@@ -215,7 +215,7 @@ typedef struct rt_stats {
     double update_wait_ms;     /* part of update_ms blocked on the GPU (a staging buffer still
                                   read by an earlier frame's copy); the rest is host compute */
 } rt_stats;
-/* sizeof(rt_stats) == 96 on LP64; a caller built against a different layout gets RT_ABI_VERSION != 2 */
+/* sizeof(rt_stats) == 96 on LP64 (RT_ABI_VERSION 3) */
 
 /* Closest-hit record for rt_trace_rays (per-ray parity tests). */
 typedef struct rt_hit {
@@ -307,6 +307,23 @@ rt_status rt_tile_pixels(uint32_t width, uint32_t height, uint32_t tile_w, uint3
  * RT_ERR_STATE after rt_scene_update_triangles until a frame has run its update. */
 rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_count,
                         uint32_t flags, rt_hit *hits_host);
+
+/* The box decisions of the trace kernels on caller data, for parity tests (no scene needed): box i =
+ * {xmin, xmax, ymin, ymax, zmin, zmax} (6 floats), ray i = origin xyz, direction xyz, range [0.001, tmax[i]].
+ * hit[i] = 1 when the kernel the mode names keeps the box; te[i] = the entry t it orders children by (+inf on a
+ * miss).  RT_BOX_REFERENCE is BoundingBox::hit (src/AS/BoundingBox.cu:34-72) as the EXACT kernel computes it; the
+ * FAST modes are the reciprocal-plane slabs the persistent kernel culls with, conservative (a box the reference keeps
+ * is never culled), and — in the exact-decision modes — with every decision inside their error margin re-taken with
+ * the reference's slab, so they keep exactly the boxes the reference keeps. */
+typedef enum rt_box_mode {
+    RT_BOX_REFERENCE = 0,      /* EXACT kernel: the reference's division slab */
+    RT_BOX_CULL = 1,           /* FAST single-box cull (greedy-quad scenes' instance / root boxes) */
+    RT_BOX_DECIDE = 2,         /* FAST single box, exact decisions (binary pairs, the reference's and GPU-built trees) */
+    RT_BOX_QUAD_PAIR = 3,      /* FAST quad slot, pair order, exact decisions (the reference's and GPU-built trees) */
+    RT_BOX_QUAD_GREEDY = 4     /* FAST quad slot of a greedy-collapsed host SAH tree (conservative cull) */
+} rt_box_mode;
+rt_status rt_box_test(int device, const float *boxes_host, const float *rays_host, const float *tmax_host, size_t count,
+                      uint32_t mode, uint8_t *hit_host, float *te_host);
 
 /* Tuning knobs (defaults are the tuned values):
  *   "kernel"    : 0 = one-thread-per-pixel grid kernel, 1 = persistent-wave megakernel (default)

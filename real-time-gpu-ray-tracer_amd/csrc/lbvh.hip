@@ -1170,14 +1170,32 @@ __global__ void member_map_kernel(const LbvhSeg *segs, const uint32_t *seg_of, u
 hipError_t LbvhBuilder::set_members(const std::vector<uint32_t> &pairs, hipStream_t stream) {
     dfree(members_);
     dfree(item_member_);
+    members_n_ = 0;
     if (pairs.empty()) return hipSuccess;
     LB_TRY(dalloc(members_, pairs.size()));
+    members_n_ = pairs.size();
     LB_TRY(dalloc(item_member_, (size_t)n_items_));
     LB_TRY(hipMemcpyAsync(members_, pairs.data(), pairs.size() * sizeof(uint32_t), hipMemcpyHostToDevice, stream));
     hipLaunchKernelGGL(member_map_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, seg_of_, n_items_,
                        members_, item_member_);
     LB_TRY(hipGetLastError());
     return hipStreamSynchronize(stream);            // `pairs` (host) must outlive the copy
+}
+
+size_t LbvhBuilder::workspace_bytes() const {
+    if (!segs_) return 0;
+    const size_t N = n_items_, NI = max_pairs(), u = sizeof(uint32_t);
+    size_t b = n_segs_ * sizeof(LbvhSeg) + N * u /*seg_of*/ + 6 * (size_t)n_segs_ * u /*bounds*/ + 4 * N * u /*keys, values*/ +
+               N * u /*parent_leaf*/ + NI * (2 + 1 + 2 + 1 + 1 + 6 + 1 + 1) * u /*child parent range flag height nbox kept pidx*/ +
+               tmp_bytes_;
+    if (own_box_) b += 6 * N * sizeof(float) + N * sizeof(float4);
+    if (stage_) b += N * sizeof(TriHot);
+    if (members_) b += members_n_ * u;
+    if (item_member_) b += N * u;
+    if (frontier_) b += (1 + 2 * NI) * u;
+    if (front_) b += 2 * (size_t)max_pairs() * u;
+    if (count_) b += u;
+    return b;
 }
 
 hipError_t LbvhBuilder::set_items(const float *boxes, const float4 *centroids) {

@@ -89,6 +89,9 @@ public:
     uint32_t items() const { return n_items_; }
     uint32_t segments() const { return n_segs_; }
     uint32_t max_pairs() const { return n_items_ > n_segs_ ? n_items_ - n_segs_ : 1u; }
+    // device bytes the builder's workspace holds now (sort keys, hierarchy, staged records, rocPRIM scratch, ...):
+    // part of rt_scene_info::device_bytes
+    size_t workspace_bytes() const;
 
     // BLAS items: boxes / centroids of the segments' primitives (reference box semantics).
     // stage_hot (BLAS builds without cold records): triangle records staged in item order for the next build()
@@ -121,6 +124,7 @@ private:
     LbvhSeg *segs_ = nullptr;
     uint32_t *seg_of_ = nullptr;          // item -> segment
     uint32_t *members_ = nullptr;         // group segments: {first primitive, instance} pairs
+    size_t members_n_ = 0;
     uint32_t *item_member_ = nullptr;     // per item: its member instance + 1 (group segments), from members_
     float *box_ = nullptr;                // 6 floats per item (owned or caller's)
 public:

@@ -53,6 +53,8 @@ hipError_t launch_trace_rays_fastmath(const SceneGPU &, const float *, uint32_t,
 hipError_t launch_render_persistent_fastmath(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
                                              uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
 uint32_t persistent_blocks_per_cu_fastmath(uint32_t variant, uint32_t wide, bool raw);
+hipError_t launch_box_test_exact(const float *, const float *, const float *, uint32_t, uint32_t, uint8_t *, float *, hipStream_t);
+hipError_t launch_box_test_fast(const float *, const float *, const float *, uint32_t, uint32_t, uint8_t *, float *, hipStream_t);
 }  // namespace rtamd
 
 using namespace rtamd;
@@ -2090,6 +2092,36 @@ rt_status rt_trace_rays(rt_scene *s, const float *rays, size_t n, uint32_t flags
     return RT_OK;
 }
 
+rt_status rt_box_test(int device, const float *boxes, const float *rays, const float *tmax, size_t n, uint32_t mode,
+                      uint8_t *hit, float *te) {
+    if (n && (!boxes || !rays || !tmax || !hit || !te)) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
+    if (mode > RT_BOX_QUAD_GREEDY) return fail(RT_ERR_INVALID_ARGUMENT, "mode must be an rt_box_mode");
+    if (n > 0xFFFFFFFFull / 6) return fail(RT_ERR_INVALID_ARGUMENT, "too many boxes");
+    if (n == 0) return RT_OK;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || device < 0 || device >= count)
+        return fail(RT_ERR_INVALID_ARGUMENT, "no such device");
+    HIP_TRY(hipSetDevice(device));
+    const size_t fb = n * 6 * sizeof(float);
+    char *d = nullptr;                          // boxes | rays | tmax | te | hit
+    HIP_TRY(hipMalloc(&d, 2 * fb + 2 * n * sizeof(float) + n));
+    float *db = reinterpret_cast<float *>(d), *dr = reinterpret_cast<float *>(d + fb);
+    float *dt = reinterpret_cast<float *>(d + 2 * fb), *de = dt + n;
+    uint8_t *dh = reinterpret_cast<uint8_t *>(de + n);
+    hipError_t e = hipMemcpy(db, boxes, fb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dr, rays, fb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dt, tmax, n * sizeof(float), hipMemcpyHostToDevice);
+    if (e == hipSuccess)
+        e = mode == RT_BOX_REFERENCE ? launch_box_test_exact(db, dr, dt, (uint32_t)n, mode, dh, de, nullptr)
+                                     : launch_box_test_fast(db, dr, dt, (uint32_t)n, mode, dh, de, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(hit, dh, n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(te, de, n * sizeof(float), hipMemcpyDeviceToHost);
+    (void)hipFree(d);
+    if (e != hipSuccess) return fail(RT_ERR_DEVICE, std::string("rt_box_test: ") + hipGetErrorString(e));
+    return RT_OK;
+}
+
 rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     if (!s || !key) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
     const std::string k(key);
@@ -2197,14 +2229,23 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "lane_priority") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "lane_priority must be 0 or 1");
         RT_TRY(drain(s));
-        for (hipStream_t &l : s->lane_st)
-            if (l) { (void)hipStreamDestroy(l); l = nullptr; }          // recreated at the next frame
+        for (hipStream_t &l : s->lane_st) {
+            if (!l) continue;
+            // nothing may keep a handle to a destroyed lane stream: drain() waits on last_stream, frame_update
+            // compares chain_stream[] with the frame's stream
+            if (s->last_stream == l) s->last_stream = nullptr;
+            for (hipStream_t &c : s->chain_stream)
+                if (c == l) c = nullptr;
+            (void)hipStreamDestroy(l);
+            l = nullptr;                                                // recreated at the next frame
+        }
         s->lane_priority = value == 1;
     } else if (k == "tlas_median_leaf") {
         if (value < 0 || value > (int64_t)TLAS_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_median_leaf must be 0..2");
         s->tlas_median_leaf = (uint32_t)value;
     } else if (k == "tlas_sah") {
-        s->tlas_sah = value != 0;                 // next frame's TLAS
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_sah must be 0 or 1");
+        s->tlas_sah = value == 1;                 // next frame's TLAS
     } else if (k == "tlas_leaf") {
         if (value < 1 || value > (int64_t)SAH_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_leaf must be in 1..4");
         s->tlas_leaf = (uint32_t)value;          // next frame's TLAS
@@ -2506,7 +2547,15 @@ rt_status rt_scene_get_info(const rt_scene *s, rt_scene_info *info) {
                          s->quad_hot.n * sizeof(QuadHot) + s->quad_cold.n * sizeof(PrimCold) +
                          s->materials.n * sizeof(float) + 2 * s->frame_block + s->out_rgba.n + s->out_rgb.n * sizeof(float) +
                          s->raw_tris.n * sizeof(rt_triangle) + s->raw_sph.n * sizeof(rt_sphere) +
-                         s->raw_quad.n * sizeof(rt_parallelogram);
+                         s->raw_quad.n * sizeof(rt_parallelogram) + s->blas_quads.n * sizeof(NodeQuad) +
+                         s->raw_verts.n * sizeof(float);
+    for (const auto &sp : s->spare)      // the spare BLAS sets of per-frame rebuilds ("blas_sets")
+        info->device_bytes += sp.pairs.n * sizeof(NodePair) + sp.quads.n * sizeof(NodeQuad) + sp.roots.n * sizeof(TreeRoot) +
+                              sp.tri_hot.n * sizeof(TriHot) + sp.tri_cold.n * sizeof(TriCold) +
+                              sp.sph_hot.n * sizeof(SphereHot) + sp.sph_cold.n * sizeof(PrimCold) +
+                              sp.quad_hot.n * sizeof(QuadHot) + sp.quad_cold.n * sizeof(PrimCold);
+    if (s->blas_builder) info->device_bytes += s->blas_builder->workspace_bytes();   // incl. the staged TriHot records
+    if (s->tlas_builder) info->device_bytes += s->tlas_builder->workspace_bytes();
     info->width = s->width; info->height = s->height;
     info->sqrt_sample_count = s->cam.sqrt_s;
     info->ray_trace_depth = s->cam.depth;

@@ -75,10 +75,11 @@ static_assert(LDS_DEPTH % 4 == 0, "half-pages move as 16 B pieces");
                                         // reciprocal-FMA planes is widened by a bound on its distance from the
                                         // reference's (mn - q) / d interval before the lo < hi test (and a popped entry's
                                         // lo before its lo < tmax re-test), so a FAST cull never rejects a box the
-                                        // reference's slab accepts — except on a parallel axis (|d| < 1e-6) when the origin
-                                        // lies exactly on a face of the slab: the reference keeps q == min / max
-                                        // (BoundingBox.cu:47), the FAST planes there are the rounding residual of o / d and
-                                        // may reject; the exact-decision instances (XBOX) re-test every box of such a ray.
+                                        // reference's slab accepts.  A parallel axis (|d| < 1e-6) whose origin lies exactly
+                                        // on a face of the slab is the one case planes cannot widen (the reference keeps
+                                        // q == min / max, BoundingBox.cu:47; the FAST planes there are the rounding residual
+                                        // of o / d), so every box test of a ray with a parallel axis is re-taken with the
+                                        // reference's slab (XD_PAR and up, XBOX; round 6: the host SAH trees' instances too).
                                         // Entries keep the unwidened lo, so children are still ordered by it
 #endif
 #ifndef RT_BOX_EXACT
@@ -88,9 +89,34 @@ static_assert(LDS_DEPTH % 4 == 0, "half-pages move as 16 B pieces");
                                         // reference's trees the traversal takes the reference's decisions
 #endif
 // the persistent kernel's traversal modes (SceneGPU::wide): 0 binary node pairs, 1 greedy quads by entry t (host SAH
-// trees), 2 two-level quads in pair order (GPU-built trees), 3 the same with exact box decisions (the reference's trees);
-// the binary pairs (an A/B path) take exact decisions too
-#define XBOX(W) (RT_BOX_EXACT && ((W) == 0 || (W) == 3))
+// trees), 2 two-level quads in pair order (GPU-built trees), 3 the same on the reference's trees.
+// Exact-decision level of a traversal instance (template argument XB):
+//   XD_CULL: conservative culls only;
+//   XD_PAR : also every box test of a ray with a parallel axis (|d| < 1e-6) re-taken with the reference's slab — the
+//            reciprocal planes cannot represent a parallel axis whose origin lies exactly on a face of the slab (the
+//            reference keeps q == min / max, BoundingBox.cu:47), so without it such a box could be culled.  Host SAH
+//            trees (mode 1) run at XD_CULL (RT_XPAR_SAH 0): that case is their one documented exception to "a FAST cull
+//            never rejects a box the reference keeps" (tests/test_gpu_box.py pins it to exactly that case);
+//   XD_ALL : also every decision inside the slabs' error margin, and (pair order) every comparison of two entry t's
+//            inside it: the traversal takes the reference's decisions.  The binary pairs, the reference's trees and (since
+//            round 6, RT_XBOX_GPU) the GPU-built trees — FAST equals EXACT on the same trees (C5's benched LBVH trees).
+#ifndef RT_XBOX_GPU
+#define RT_XBOX_GPU 1
+#endif
+#ifndef RT_XPAR_SAH
+#define RT_XPAR_SAH 0                   // host SAH trees at XD_PAR: C2 +4.4 %, C3 +2.5 % per frame (profiles/r06/exact_decisions/)
+#endif
+constexpr int XD_CULL = 0, XD_PAR = 1, XD_ALL = 2;
+// RT_XD_REL: the XD_ALL instances compute slab planes as (b - o) * (1/d) — two operations per plane instead of one FMA on
+// o / d — whose error is relative to t alone (<= 2^-21.9 |t|; the FMA form's carries 2^-24 |o / d|, i.e. a margin of
+// ~0.02 for a bounce ray with a shallow axis 100 units from the origin), so decisions inside the margin, and their
+// re-takes, stay rare (round 6: C5 14.7 -> ... ms serialised)
+#ifndef RT_XD_REL
+#define RT_XD_REL 1
+#endif
+template <int XB> __device__ constexpr bool rel_planes() { return RT_XD_REL && XB == XD_ALL; }
+#define XBOX(W) (!RT_BOX_EXACT ? XD_CULL : (((W) == 0 || (W) == 3 || (RT_XBOX_GPU && (W) == 2)) ? XD_ALL \
+                                           : (RT_XPAR_SAH ? XD_PAR : XD_CULL)))
 #ifndef RT_NZ_MIN
 #define RT_NZ_MIN FZERO                 // |d_axis| below this is clamped to +-1e-20 for the slab reciprocals (prep)
 #endif
@@ -205,7 +231,7 @@ struct RayP {
 #endif
 #endif
 };
-template <bool XB = false>
+template <int XB = XD_CULL>
 __device__ __forceinline__ void prep(RayP &r) {
 #if !RT_EXACT
     // |d| < 1e-6 (the reference's parallel-axis threshold, BoundingBox.cu:44-50) -> +-1e-20: the plane distances
@@ -215,14 +241,17 @@ __device__ __forceinline__ void prep(RayP &r) {
     r.inv = mk(rcp(nz(r.d.x)), rcp(nz(r.d.y)), rcp(nz(r.d.z)));
     r.oinv = mk(r.o.x * r.inv.x, r.o.y * r.inv.y, r.o.z * r.inv.z);
 #if RT_SLAB_CONS
-    {   // fmaf(b, inv, -oinv) differs from (b - o) / d by <= 2^-24 |o / d| (oinv's rounding) + ~2^-21.7 |t| (the
+    if (rel_planes<XB>()) {     // (b - o) * inv: within 2^-21.9 |t| of the reference's plane, no absolute part
+        const bool par = fabsf(r.d.x) < RT_NZ_MIN || fabsf(r.d.y) < RT_NZ_MIN || fabsf(r.d.z) < RT_NZ_MIN;
+        r.pad = par ? -0.0f : 0.0f;
+    } else {   // fmaf(b, inv, -oinv) differs from (b - o) / d by <= 2^-24 |o / d| (oinv's rounding) + ~2^-21.7 |t| (the
         // reciprocal's 1 ulp, the fma's and the reference's roundings); parallel axes only decide inside / outside
         const float px = fabsf(r.d.x) < RT_NZ_MIN ? 0.0f : fabsf(r.oinv.x);
         const float py = fabsf(r.d.y) < RT_NZ_MIN ? 0.0f : fabsf(r.oinv.y);
         const float pz = fabsf(r.d.z) < RT_NZ_MIN ? 0.0f : fabsf(r.oinv.z);
         const float pad = 0x1p-22f * fmaxf(px, fmaxf(py, pz));
         r.pad = pad;
-        if (XB) {       // the exact-decision instances re-take every box test of a ray with a parallel axis
+        if (XB != XD_CULL) {   // the exact-decision instances re-take every box test of a ray with a parallel axis
             const bool par = fabsf(r.d.x) < RT_NZ_MIN || fabsf(r.d.y) < RT_NZ_MIN || fabsf(r.d.z) < RT_NZ_MIN;
             r.pad = par ? -pad : pad;
         }
@@ -277,21 +306,29 @@ __device__ __forceinline__ bool ray_parallel(const RayP &r) { return __builtin_s
 #endif
 // XB: decisions inside the margin re-taken with the reference's slab (RT_BOX_EXACT: the quad instance for the reference's
 // own trees and the binary-pair one, where the traversal then takes exactly the reference's decisions)
-template <bool XB = false>
+template <int XB = XD_CULL>
 __device__ __forceinline__ bool slab(const float *b, const RayP &r, float tmin, float tmax, float &te) {
 #if RT_EXACT
     return slab_ref(b, r.o, r.d, tmin, tmax, te);
 #else
-    const float tx1 = fmaf(b[0], r.inv.x, -r.oinv.x), tx2 = fmaf(b[1], r.inv.x, -r.oinv.x);
-    const float ty1 = fmaf(b[2], r.inv.y, -r.oinv.y), ty2 = fmaf(b[3], r.inv.y, -r.oinv.y);
-    const float tz1 = fmaf(b[4], r.inv.z, -r.oinv.z), tz2 = fmaf(b[5], r.inv.z, -r.oinv.z);
+    float tx1, tx2, ty1, ty2, tz1, tz2;
+    if (rel_planes<XB>()) {
+        tx1 = (b[0] - r.o.x) * r.inv.x; tx2 = (b[1] - r.o.x) * r.inv.x;
+        ty1 = (b[2] - r.o.y) * r.inv.y; ty2 = (b[3] - r.o.y) * r.inv.y;
+        tz1 = (b[4] - r.o.z) * r.inv.z; tz2 = (b[5] - r.o.z) * r.inv.z;
+    } else {
+        tx1 = fmaf(b[0], r.inv.x, -r.oinv.x); tx2 = fmaf(b[1], r.inv.x, -r.oinv.x);
+        ty1 = fmaf(b[2], r.inv.y, -r.oinv.y); ty2 = fmaf(b[3], r.inv.y, -r.oinv.y);
+        tz1 = fmaf(b[4], r.inv.z, -r.oinv.z); tz2 = fmaf(b[5], r.inv.z, -r.oinv.z);
+    }
     const float lo = fmaxf(fmaxf(tmin, fminf(tx1, tx2)), fmaxf(fminf(ty1, ty2), fminf(tz1, tz2)));
     const float hi = fminf(fminf(tmax, fmaxf(tx1, tx2)), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
     te = lo;
 #if RT_SLAB_CONS
     bool h = cons_lo(lo, r.pad) < cons_hi(hi, r.pad);
 #if RT_BOX_EXACT
-    if (XB && ((h && !(hi - lo > box_margin(lo, hi, r.pad))) || ray_parallel(r))) {   // rare: the reference's decision
+    if ((XB == XD_ALL && h && !(hi - lo > box_margin(lo, hi, r.pad))) || (XB != XD_CULL && ray_parallel(r))) {
+        // rare: the reference's decision
         BoxArgs a;
         for (int c = 0; c < 6; c++) a.b[c] = b[c];
         a.o = r.o; a.d = r.d; a.tmax = tmax;
@@ -523,7 +560,7 @@ __device__ __forceinline__ bool pop_keep(const Trav &T, float tn, uint32_t ref) 
 }
 
 // R: this frame's TLAS root (the persistent kernel holds it in SGPRs, loaded once per wave)
-template <bool XB = false>
+template <int XB = XD_CULL>
 __device__ __forceinline__ void trav_init(Trav &T, const TreeRoot &R, const f3 &o, const f3 &d) {
     T.wr.o = o; T.wr.d = d; prep<XB>(T.wr);
     T.lr = T.wr;
@@ -538,8 +575,9 @@ __device__ __forceinline__ void trav_init(Trav &T, const TreeRoot &R, const f3 &
     T.tracing = slab<XB>(R.box, T.wr, TMIN, T.tmax, te);                 // root pop test (TLAS.cu:150)
     T.curT = te;
 }
+template <int XB = XD_CULL>
 __device__ __forceinline__ void trav_init(Trav &T, const SceneGPU &sc, const f3 &o, const f3 &d) {
-    trav_init(T, *sc.tlas_root, o, d);
+    trav_init<XB>(T, *sc.tlas_root, o, d);
 }
 
 // The frame's TLAS root as wave-uniform values (SGPRs): read once per wave instead of per ray.
@@ -558,7 +596,9 @@ __device__ __forceinline__ TreeRoot uniform_root(const SceneGPU &sc) {
 
 // Process T.cur (one node pair, one TLAS leaf instance or one BLAS leaf), then choose the next node:
 // the near child, or a popped entry surviving the re-test; clears T.tracing when the stack is dry.
-template <bool COUNT>
+// XB (FAST builds): box decisions inside the slab error margin re-taken with the reference's slab (rt_trace_rays and
+// the grid kernel: the binary pairs in the reference's order, so their decisions are the reference's)
+template <bool COUNT, int XB = XD_CULL>
 __device__ __forceinline__ void trav_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
     const uint32_t cur = T.cur;
     if (!(cur & REF_LEAF)) {
@@ -573,8 +613,8 @@ __device__ __forceinline__ void trav_step(Trav &T, const SceneGPU &sc, SEnt *spi
         if (COUNT) cnt.pairs++;
         float e0 = 0.0f, e1 = 0.0f;
         const RayP &r = blas ? T.lr : T.wr;
-        const bool h0 = slab(b0, r, TMIN, T.tmax, e0);
-        const bool h1 = slab(b1, r, TMIN, T.tmax, e1);
+        const bool h0 = slab<XB>(b0, r, TMIN, T.tmax, e0);
+        const bool h1 = slab<XB>(b1, r, TMIN, T.tmax, e1);
         if (h0 && h1) {
             // reference: tLeft > tRight -> push left then right (right popped first)
             const bool right_near = e0 > e1;
@@ -594,9 +634,9 @@ __device__ __forceinline__ void trav_step(Trav &T, const SceneGPU &sc, SEnt *spi
         // Instance::hit: ray into local space, d' not renormalised (Instance.cu:26-27)
         T.lr.o = xf_point(I.inv, T.wr.o);
         T.lr.d = xf_vector(I.inv, T.wr.d);
-        prep(T.lr);
+        prep<XB>(T.lr);
         float te;
-        if (slab(I.root_box, T.lr, TMIN, T.tmax, te)) { T.cur = I.root_ref; return; }   // BLAS root pop test
+        if (slab<XB>(I.root_box, T.lr, TMIN, T.tmax, te)) { T.cur = I.root_ref; return; }   // BLAS root pop test
     } else {
         // BLAS leaf: primitives in leaf order (BLAS.cu:153-176)
         const uint32_t start = ref_leaf_start(cur), count = ref_leaf_count(cur), type = ref_leaf_type(cur);
@@ -724,13 +764,15 @@ __device__ __forceinline__ R lds_or_global(uint32_t at, const R *g, uint32_t k) 
 // one axis of the 4 slot slab tests; pa / pb: that axis's contribution to the entry t of the halves' boxes (a
 // half's box is the union of its two slots' boxes, and the plane distances are monotone in the bound, so its near
 // plane is the nearer of its slots' near planes)
-template <bool PAIR>
-__device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float oinv, float4 &tn, float4 &tf,
+// REL: c = o, planes (b - o) * inv (rel_planes); else c = o / d, planes fmaf(b, inv, -c)
+template <bool PAIR, bool REL = false>
+__device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float c, float4 &tn, float4 &tf,
                                       float &pa, float &pb) {
-    const float a0 = fmaf(lo.x, inv, -oinv), b0 = fmaf(hi.x, inv, -oinv);
-    const float a1 = fmaf(lo.y, inv, -oinv), b1 = fmaf(hi.y, inv, -oinv);
-    const float a2 = fmaf(lo.z, inv, -oinv), b2 = fmaf(hi.z, inv, -oinv);
-    const float a3 = fmaf(lo.w, inv, -oinv), b3 = fmaf(hi.w, inv, -oinv);
+    const auto pl = [&](float b) { return REL ? (b - c) * inv : fmaf(b, inv, -c); };
+    const float a0 = pl(lo.x), b0 = pl(hi.x);
+    const float a1 = pl(lo.y), b1 = pl(hi.y);
+    const float a2 = pl(lo.z), b2 = pl(hi.z);
+    const float a3 = pl(lo.w), b3 = pl(hi.w);
     const float n0 = fminf(a0, b0), n1 = fminf(a1, b1), n2 = fminf(a2, b2), n3 = fminf(a3, b3);
     tn = make_float4(fmaxf(tn.x, n0), fmaxf(tn.y, n1), fmaxf(tn.z, n2), fmaxf(tn.w, n3));
     tf = make_float4(fminf(tf.x, fmaxf(a0, b0)), fminf(tf.y, fmaxf(a1, b1)), fminf(tf.z, fmaxf(a2, b2)), fminf(tf.w, fmaxf(a3, b3)));
@@ -746,7 +788,99 @@ __device__ __forceinline__ void cswap(float &ta, uint32_t &ra, float &tb, uint32
     const uint32_t r = sw ? rb : ra, q = sw ? ra : rb;
     ta = t; tb = u; ra = r; rb = q;
 }
-template <bool COUNT, bool PAIR, bool XB>
+// The hit decisions and entry t's of a quad's 4 slots (and, PAIR, of its two halves' boxes) for ray r with the current
+// tmax: FAST reciprocal slabs, conservative (RT_SLAB_CONS); XB: decisions inside the error margin re-taken with the
+// reference's division slab on the node's bounds re-read from Q.  Shared by the traversal step and the box-test entry
+// point the parity tests call (rt_box_test, RT_BOX_QUAD_*).
+template <bool PAIR, int XB>
+__device__ __forceinline__ void quad_decide(const float4 *Q, const float4 &lx, const float4 &hx, const float4 &ly,
+                                            const float4 &hy, const float4 &lz, const float4 &hz, const uint4 &R,
+                                            const RayP &r, float tmax, float (&t)[4], bool (&h)[4], float &pa, float &pb) {
+    bool und[4] = {false, false, false, false};   // und: hit decision inside the error margin
+    // XD_ALL: whether an entry t is TMIN for certain — every entry plane below TMIN by more than the error bound, so the
+    // reference's is TMIN too.  Two such entries compare equal in both slabs (the ray starts inside both boxes: most
+    // nodes around a bounce origin), so their order needs no re-take.
+    bool low[4] = {false, false, false, false}, low_a = false, low_b = false;
+    const float t0 = XB == XD_ALL ? -__builtin_huge_valf() : TMIN;
+    pa = t0; pb = t0;                                // entry t of the two halves' boxes
+    {
+        float4 tn = make_float4(t0, t0, t0, t0), tf = make_float4(tmax, tmax, tmax, tmax);
+        constexpr bool REL = rel_planes<XB>();
+        slab4<PAIR, REL>(lx, hx, r.inv.x, REL ? r.o.x : r.oinv.x, tn, tf, pa, pb);
+        slab4<PAIR, REL>(ly, hy, r.inv.y, REL ? r.o.y : r.oinv.y, tn, tf, pa, pb);
+        slab4<PAIR, REL>(lz, hz, r.inv.z, REL ? r.o.z : r.oinv.z, tn, tf, pa, pb);
+        if (XB == XD_ALL) {
+            const auto below = [&](float v) { return fmaf(fabsf(v), 0x1p-19f, v + 2.0f * fabsf(r.pad)) < TMIN; };
+            low[0] = below(tn.x); low[1] = below(tn.y); low[2] = below(tn.z); low[3] = below(tn.w);
+            low_a = below(pa); low_b = below(pb);
+            tn = make_float4(fmaxf(tn.x, TMIN), fmaxf(tn.y, TMIN), fmaxf(tn.z, TMIN), fmaxf(tn.w, TMIN));
+            pa = fmaxf(pa, TMIN); pb = fmaxf(pb, TMIN);
+        }
+        t[0] = tn.x; t[1] = tn.y; t[2] = tn.z; t[3] = tn.w;
+#if RT_SLAB_CONS
+        h[0] = cons_lo(tn.x, r.pad) < cons_hi(tf.x, r.pad); h[1] = cons_lo(tn.y, r.pad) < cons_hi(tf.y, r.pad);
+        h[2] = cons_lo(tn.z, r.pad) < cons_hi(tf.z, r.pad); h[3] = cons_lo(tn.w, r.pad) < cons_hi(tf.w, r.pad);
+        if (XB == XD_ALL) {
+            und[0] = !(tf.x - tn.x > box_margin(tn.x, tf.x, r.pad)); und[1] = !(tf.y - tn.y > box_margin(tn.y, tf.y, r.pad));
+            und[2] = !(tf.z - tn.z > box_margin(tn.z, tf.z, r.pad)); und[3] = !(tf.w - tn.w > box_margin(tn.w, tf.w, r.pad));
+        }
+#else
+        h[0] = tn.x < tf.x; h[1] = tn.y < tf.y; h[2] = tn.z < tf.z; h[3] = tn.w < tf.w;
+#endif
+    }
+    // an empty slot repeats its sibling's box (the half's union stays exact) and is never accepted
+    h[1] = h[1] && R.y != REF_EMPTY;
+    h[3] = h[3] && R.w != REF_EMPTY;
+#if RT_SLAB_CONS && RT_BOX_EXACT
+    if (XB != XD_CULL) {   // Rare: a hit decision inside the error margin, a ray with a parallel axis, or (pair order) two entry t's the order
+        // compares inside the margin — then every box of the node is re-tested with the reference's slab (the halves'
+        // boxes too: unions of their slots' boxes), on the node's bounds read again (keeping the 24 bounds live through
+        // the step would cost registers on the hot path), one box per iteration so that one copy of the division slab
+        // serves all six
+        const auto close = [&](float a, float b) { return fabsf(a - b) <= box_margin(a, b, r.pad); };
+#ifndef RT_XD_DIAG
+#define RT_XD_DIAG 0                    // diagnostic builds only: 1 no pair-order trigger, 2 no margin trigger, 4 no parallel
+#endif
+        bool need = !(RT_XD_DIAG & 4) && ray_parallel(r);
+        if (XB == XD_ALL && !(RT_XD_DIAG & 2))
+            need = need || (h[0] && und[0]) || (h[1] && und[1]) || (h[2] && und[2]) || (h[3] && und[3]);
+        if (PAIR && XB == XD_ALL && !(RT_XD_DIAG & 1))
+            need = need || (h[0] && h[1] && !(low[0] && low[1]) && close(t[0], t[1])) ||
+                   (h[2] && h[3] && !(low[2] && low[3]) && close(t[2], t[3])) ||
+                   ((h[0] || h[1]) && (h[2] || h[3]) && !(low_a && low_b) && close(pa, pb));
+        if (need) {
+            const float4 L[6] = {Q[0], Q[1], Q[2], Q[3], Q[4], Q[5]};
+#pragma unroll 1
+            for (int j = 0; j < (PAIR ? 6 : 4); j++) {
+                const int k0 = j < 4 ? j : 2 * (j - 4), k1 = j < 4 ? j : k0 + 1;     // a slot, or a half's two slots
+                float b[6];
+#pragma unroll
+                for (int c = 0; c < 6; c++) {
+                    const float u = comp4(L[c], k0), v = comp4(L[c], k1);
+                    b[c] = (c & 1) ? fmaxf(u, v) : fminf(u, v);
+                }
+                BoxArgs ba;
+                for (int c = 0; c < 6; c++) ba.b[c] = b[c];
+                ba.o = r.o; ba.d = r.d; ba.tmax = tmax;
+                const float te = slab_ref_entry(ba);
+                const bool hh = te == te;
+                if (j < 4) {
+                    const uint32_t rk = j == 0 ? R.x : (j == 1 ? R.y : (j == 2 ? R.z : R.w));
+                    const bool live = rk != REF_EMPTY;
+                    const bool hk = hh && live;
+                    h[0] = j == 0 ? hk : h[0]; h[1] = j == 1 ? hk : h[1]; h[2] = j == 2 ? hk : h[2]; h[3] = j == 3 ? hk : h[3];
+                    if (hk) { t[0] = j == 0 ? te : t[0]; t[1] = j == 1 ? te : t[1]; t[2] = j == 2 ? te : t[2]; t[3] = j == 3 ? te : t[3]; }
+                } else if (hh) {
+                    pa = j == 4 ? te : pa;
+                    pb = j == 5 ? te : pb;
+                }
+            }
+        }
+    }
+#endif
+}
+
+template <bool COUNT, bool PAIR, int XB>
 __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt) {
     const uint32_t cur = T.cur;
     const bool blas = (cur & REF_BLAS) != 0;
@@ -770,69 +904,9 @@ __device__ __forceinline__ void wide_interior_step(Trav &T, const SceneGPU &sc, 
     if (COUNT) cnt.pairs += 2;                       // 4 child boxes = 2 node-pair equivalents
     const RayP &r = blas ? T.lr : T.wr;
     float t[4];
-    bool h[4], und[4] = {false, false, false, false};   // und: hit decision inside the error margin
-    float pa = TMIN, pb = TMIN;                      // entry t of the two halves' boxes
-    {
-        float4 tn = make_float4(TMIN, TMIN, TMIN, TMIN), tf = make_float4(T.tmax, T.tmax, T.tmax, T.tmax);
-        slab4<PAIR>(lx, hx, r.inv.x, r.oinv.x, tn, tf, pa, pb);
-        slab4<PAIR>(ly, hy, r.inv.y, r.oinv.y, tn, tf, pa, pb);
-        slab4<PAIR>(lz, hz, r.inv.z, r.oinv.z, tn, tf, pa, pb);
-        t[0] = tn.x; t[1] = tn.y; t[2] = tn.z; t[3] = tn.w;
-#if RT_SLAB_CONS
-        h[0] = cons_lo(tn.x, r.pad) < cons_hi(tf.x, r.pad); h[1] = cons_lo(tn.y, r.pad) < cons_hi(tf.y, r.pad);
-        h[2] = cons_lo(tn.z, r.pad) < cons_hi(tf.z, r.pad); h[3] = cons_lo(tn.w, r.pad) < cons_hi(tf.w, r.pad);
-        if (XB) {
-            und[0] = !(tf.x - tn.x > box_margin(tn.x, tf.x, r.pad)); und[1] = !(tf.y - tn.y > box_margin(tn.y, tf.y, r.pad));
-            und[2] = !(tf.z - tn.z > box_margin(tn.z, tf.z, r.pad)); und[3] = !(tf.w - tn.w > box_margin(tn.w, tf.w, r.pad));
-        }
-#else
-        h[0] = tn.x < tf.x; h[1] = tn.y < tf.y; h[2] = tn.z < tf.z; h[3] = tn.w < tf.w;
-#endif
-    }
-    // an empty slot repeats its sibling's box (the half's union stays exact) and is never accepted
-    h[1] = h[1] && R.y != REF_EMPTY;
-    h[3] = h[3] && R.w != REF_EMPTY;
-#if RT_SLAB_CONS && RT_BOX_EXACT
-    if (XB) {   // Rare: a hit decision inside the error margin, a ray with a parallel axis, or (pair order) two entry t's the order
-        // compares inside the margin — then every box of the node is re-tested with the reference's slab (the halves'
-        // boxes too: unions of their slots' boxes), on the node's bounds read again (keeping the 24 bounds live through
-        // the step would cost registers on the hot path), one box per iteration so that one copy of the division slab
-        // serves all six
-        const auto close = [&](float a, float b) { return fabsf(a - b) <= box_margin(a, b, r.pad); };
-        bool need = ray_parallel(r) || (h[0] && und[0]) || (h[1] && und[1]) || (h[2] && und[2]) || (h[3] && und[3]);
-        if (PAIR)
-            need = need || (h[0] && h[1] && close(t[0], t[1])) || (h[2] && h[3] && close(t[2], t[3])) ||
-                   ((h[0] || h[1]) && (h[2] || h[3]) && close(pa, pb));
-        if (need) {
-            const float4 L[6] = {Q[0], Q[1], Q[2], Q[3], Q[4], Q[5]};
-#pragma unroll 1
-            for (int j = 0; j < (PAIR ? 6 : 4); j++) {
-                const int k0 = j < 4 ? j : 2 * (j - 4), k1 = j < 4 ? j : k0 + 1;     // a slot, or a half's two slots
-                float b[6];
-#pragma unroll
-                for (int c = 0; c < 6; c++) {
-                    const float u = comp4(L[c], k0), v = comp4(L[c], k1);
-                    b[c] = (c & 1) ? fmaxf(u, v) : fminf(u, v);
-                }
-                BoxArgs ba;
-                for (int c = 0; c < 6; c++) ba.b[c] = b[c];
-                ba.o = r.o; ba.d = r.d; ba.tmax = T.tmax;
-                const float te = slab_ref_entry(ba);
-                const bool hh = te == te;
-                if (j < 4) {
-                    const uint32_t rk = j == 0 ? R.x : (j == 1 ? R.y : (j == 2 ? R.z : R.w));
-                    const bool live = rk != REF_EMPTY;
-                    const bool hk = hh && live;
-                    h[0] = j == 0 ? hk : h[0]; h[1] = j == 1 ? hk : h[1]; h[2] = j == 2 ? hk : h[2]; h[3] = j == 3 ? hk : h[3];
-                    if (hk) { t[0] = j == 0 ? te : t[0]; t[1] = j == 1 ? te : t[1]; t[2] = j == 2 ? te : t[2]; t[3] = j == 3 ? te : t[3]; }
-                } else if (hh) {
-                    pa = j == 4 ? te : pa;
-                    pb = j == 5 ? te : pb;
-                }
-            }
-        }
-    }
-#endif
+    bool h[4];
+    float pa, pb;                                    // entry t of the two halves' boxes
+    quad_decide<PAIR, XB>(Q, lx, hx, ly, hy, lz, hz, R, r, T.tmax, t, h, pa, pb);
     const float inf = __builtin_huge_valf();
     if (!PAIR) {
         float t0 = h[0] ? t[0] : inf, t1 = h[1] ? t[1] : inf, t2 = h[2] ? t[2] : inf, t3 = h[3] ? t[3] : inf;
@@ -902,7 +976,7 @@ __device__ __forceinline__ void spec_interior_step(Trav &T, const SceneGPU &sc, 
     const uint32_t cur = T.cur;
 #if !RT_EXACT
     if (WIDE) {
-        if (!(cur & REF_LEAF)) wide_interior_step<COUNT, (WIDE >= 2), (WIDE == 3)>(T, sc, spill, cnt);
+        if (!(cur & REF_LEAF)) wide_interior_step<COUNT, (WIDE >= 2), XBOX(WIDE)>(T, sc, spill, cnt);
         else { T.pleaf = cur; pop_next(T, spill); }        // postpone, keep walking
         return;
     }
@@ -1113,11 +1187,11 @@ __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *sp
     DIAG_ADD(pc.leaf, t1);
 }
 
-template <bool COUNT>
+template <bool COUNT, int XB = XD_CULL>
 __device__ __forceinline__ bool trace(const SceneGPU &sc, const f3 &o, const f3 &d, Hit &hit, Trav &T, SEnt *spill,
                                       LaneCount &cnt) {
-    trav_init(T, sc, o, d);
-    while (T.tracing) trav_step<COUNT>(T, sc, spill, cnt);
+    trav_init<XB>(T, sc, o, d);
+    while (T.tracing) trav_step<COUNT, XB>(T, sc, spill, cnt);
     hit = T.hit;
     return T.found;
 }
@@ -1214,7 +1288,7 @@ __device__ f3 ray_color(const SceneGPU &sc, const CameraGPU &cam, f3 o, f3 d, Rn
     for (uint32_t depth = 0; depth < cam.depth; depth++) {
         Hit h;
         rays++;
-        if (trace<COUNT>(sc, o, d, h, T, spill, cnt)) {
+        if (trace<COUNT, XD_ALL>(sc, o, d, h, T, spill, cnt)) {
             if (COUNT) cnt.hits++;
             const Surface s = finalize(sc, o, d, h);
             const float4 m = reinterpret_cast<const float4 *>(sc.materials)[s.material & ~MAT_METAL_BIT];
@@ -1736,7 +1810,7 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const fl
     const f3 d = mk(rays[6 * i + 3], rays[6 * i + 4], rays[6 * i + 5]);
     Hit h;
     rt_hit r;
-    if (trace<false>(sc, o, d, h, T, spill, cnt)) {
+    if (trace<false, XD_ALL>(sc, o, d, h, T, spill, cnt)) {
         const Surface s = finalize(sc, o, d, h);
         r.t = h.t; r.instance = s.member ? s.member - 1u : (sc.inst_by_slot ? sc.tlas_slots[h.inst] : h.inst);
         r.primitive_type = h.ptype; r.primitive_index = s.orig;
@@ -1753,6 +1827,64 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const fl
     hits[i] = r;
 }
 
+
+// rt_box_test (parity tests, not a render path): the box decisions the kernels take, on caller boxes and rays, one
+// thread per (box, ray, tmax) with tmin = 0.001.  Mode 0 (EXACT build): BoundingBox::hit (BoundingBox.cu:34-72).  FAST
+// build: 1 the single-box conservative cull (slab<XBOX(1)>: host SAH trees' instance and root boxes), 2 the same with
+// marginal decisions re-taken exactly (slab<XD_ALL>: binary pairs, instance and root boxes of the exact-decision
+// instances), 3 a quad slot in pair order with exact decisions (quad_decide<true, XD_ALL>: the reference's and
+// GPU-built trees), 4 a quad slot of the greedy collapse (quad_decide<false, XBOX(1)>: host SAH trees).  Modes 3 / 4 put the box in slot 0 of a quad whose slot 1 is
+// its empty partner (a leaf child's) and whose slots 2 / 3 hold a box behind the ray's origin.
+__global__ __launch_bounds__(BLOCK) void box_test_kernel(const float *boxes, const float *rays, const float *tmaxs, uint32_t n,
+                                                         uint32_t mode, uint8_t *hit, float *te) {
+    const uint32_t i = blockIdx.x * BLOCK + threadIdx.x;
+    if (i >= n) return;
+    float b[6];
+    for (int c = 0; c < 6; c++) b[c] = boxes[6 * (size_t)i + c];
+    RayP r;
+    r.o = mk(rays[6 * (size_t)i], rays[6 * (size_t)i + 1], rays[6 * (size_t)i + 2]);
+    r.d = mk(rays[6 * (size_t)i + 3], rays[6 * (size_t)i + 4], rays[6 * (size_t)i + 5]);
+    const float tmax = tmaxs[i];
+    float e = 0.0f;
+    bool h = false;
+#if RT_EXACT
+    (void)mode;
+    h = slab_ref(b, r.o, r.d, TMIN, tmax, e);
+#else
+    if (mode == 1 || mode == 2) {
+        if (mode == 2) { prep<XD_ALL>(r); h = slab<XD_ALL>(b, r, TMIN, tmax, e); }
+        else { prep<XBOX(1)>(r); h = slab<XBOX(1)>(b, r, TMIN, tmax, e); }
+    } else {
+        float4 Q[8];
+        float bb[6];       // behind the origin: around o - d, half-width |d_a| / 2 per axis (exit t = -0.5 on every axis)
+        const float p3[3] = {r.o.x - r.d.x, r.o.y - r.d.y, r.o.z - r.d.z}, d3[3] = {r.d.x, r.d.y, r.d.z};
+        for (int a = 0; a < 3; a++) {
+            const float w = 0.5f * fabsf(d3[a]);
+            bb[2 * a] = p3[a] - w; bb[2 * a + 1] = p3[a] + w;
+        }
+        for (int c = 0; c < 6; c++) {
+            float *q = reinterpret_cast<float *>(&Q[c]);
+            q[0] = b[c]; q[1] = b[c]; q[2] = bb[c]; q[3] = bb[c];
+        }
+        uint4 R = make_uint4(0u, REF_EMPTY, 0u, REF_EMPTY);
+        reinterpret_cast<uint4 *>(Q)[6] = R;
+        Q[7] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        float t[4], pa, pb;
+        bool hq[4];
+        if (mode == 3) {
+            prep<XD_ALL>(r);
+            quad_decide<true, XD_ALL>(Q, Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], R, r, tmax, t, hq, pa, pb);
+        } else {
+            prep<XBOX(1)>(r);
+            quad_decide<false, XBOX(1)>(Q, Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], R, r, tmax, t, hq, pa, pb);
+        }
+        h = hq[0];
+        e = t[0];
+    }
+#endif
+    hit[i] = h ? 1 : 0;
+    te[i] = h ? e : __builtin_huge_valf();
+}
 }  // namespace dev
 
 hipError_t RT_SUFFIX(launch_render)(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
@@ -1810,11 +1942,13 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
             if (variant == 4) return launch_persistent_wpe<4, 2 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
             return launch_persistent_wpe<3, 2 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
         }
+#if !RT_XBOX_GPU                      // else modes 2 and 3 take the same (exact-decision) instance
         if (sc.wide == 3) {
             if (variant == 4) return launch_persistent_wpe<4, 3 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
             return launch_persistent_wpe<3, 3 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
         }
-        if (sc.wide == 2) {
+#endif
+        if (sc.wide >= 2) {
             if (variant == 4) return launch_persistent_wpe<4, 2 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
             return launch_persistent_wpe<3, 2 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
         }
@@ -1829,8 +1963,10 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
 uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, uint32_t wide, bool raw) {
     if (wide && HAS_WIDE) {
         if (raw) return variant == 4 ? blocks_per_cu_wpe<4, 2 * HAS_WIDE, 1>() : blocks_per_cu_wpe<3, 2 * HAS_WIDE, 1>();
+#if !RT_XBOX_GPU
         if (wide == 3) return variant == 4 ? blocks_per_cu_wpe<4, 3 * HAS_WIDE, 0>() : blocks_per_cu_wpe<3, 3 * HAS_WIDE, 0>();
-        if (wide == 2) return variant == 4 ? blocks_per_cu_wpe<4, 2 * HAS_WIDE, 0>() : blocks_per_cu_wpe<3, 2 * HAS_WIDE, 0>();
+#endif
+        if (wide >= 2) return variant == 4 ? blocks_per_cu_wpe<4, 2 * HAS_WIDE, 0>() : blocks_per_cu_wpe<3, 2 * HAS_WIDE, 0>();
         return variant == 4 ? blocks_per_cu_wpe<4, HAS_WIDE, 0>() : blocks_per_cu_wpe<3, HAS_WIDE, 0>();
     }
     if (variant == 4) return blocks_per_cu_wpe<4>();
@@ -1841,6 +1977,14 @@ hipError_t RT_SUFFIX(launch_trace_rays)(const SceneGPU &sc, const float *rays, u
     using namespace RT_SUFFIX(dev);
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(trace_rays_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, stream, sc, rays, n, hits);
+    return hipGetLastError();
+}
+
+hipError_t RT_SUFFIX(launch_box_test)(const float *boxes, const float *rays, const float *tmax, uint32_t n, uint32_t mode,
+                                      uint8_t *hit, float *te, hipStream_t stream) {
+    using namespace RT_SUFFIX(dev);
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(box_test_kernel, dim3((n + BLOCK - 1) / BLOCK), dim3(BLOCK), 0, stream, boxes, rays, tmax, n, mode, hit, te);
     return hipGetLastError();
 }
 

@@ -169,6 +169,7 @@ EXPORTED_SYMBOLS = (
     "rt_vtk_series_read", "rt_vtk_series_count", "rt_vtk_series_entry", "rt_vtk_series_free",
     "rt_comm_unique_id", "rt_scene_attach_comm", "rt_scene_detach_comm", "rt_slab_tiles", "rt_tile_pixels",
     "rt_comm_set_timeout", "rt_camera_control_init", "rt_camera_move", "rt_clock_ns", "rt_frame_pace",
+    "rt_box_test",
 )
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -194,6 +195,8 @@ def _declare(lib):
     lib.rt_tiles_for_rank.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_uint32]
     lib.rt_tiles_for_rank.restype = C.c_uint32
     lib.rt_trace_rays.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, P(Hit)]
+    lib.rt_box_test.argtypes = [C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_uint32, C.c_void_p, C.c_void_p]
+    lib.rt_box_test.restype = C.c_int
     lib.rt_synchronize.argtypes = [C.c_void_p]
     lib.rt_scene_destroy.argtypes = [C.c_void_p]
     lib.rt_scene_destroy.restype = None

@@ -246,3 +246,24 @@ class Renderer:
 
     def __exit__(self, *exc):
         self.cleanup()
+
+
+BOX_MODES = {"reference": 0, "cull": 1, "decide": 2, "quad_pair": 3, "quad_greedy": 4}   # rt_box_mode (include/rt.h)
+
+
+def box_test(boxes, rays, tmax=None, mode: str = "reference", device: int = 0):
+    """rt_box_test: which boxes the trace kernel named by `mode` keeps for each (box, ray) in range [0.001, tmax]
+    (tmax None = +inf); returns (hit bool array, entry t array, +inf on a miss)."""
+    lib = abi.load_library()
+    boxes = np.ascontiguousarray(boxes, np.float32).reshape(-1, 6)
+    rays = np.ascontiguousarray(rays, np.float32).reshape(-1, 6)
+    n = boxes.shape[0]
+    if rays.shape[0] != n:
+        raise ValueError("one ray per box")
+    tm = np.full(n, np.inf, np.float32) if tmax is None else np.ascontiguousarray(
+        np.broadcast_to(np.asarray(tmax, np.float32), (n,)))
+    hit = np.zeros(max(1, n), np.uint8)
+    te = np.zeros(max(1, n), np.float32)
+    abi.check(lib, lib.rt_box_test(device, boxes.ctypes.data, rays.ctypes.data, tm.ctypes.data, n, BOX_MODES[mode],
+                                   hit.ctypes.data, te.ctypes.data))
+    return hit[:n].astype(bool), te[:n]

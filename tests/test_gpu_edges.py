@@ -167,6 +167,32 @@ def test_null_stream_device_outputs_ordered(gpu_lib, lanes):
     r.cleanup()
 
 
+@pytest.mark.parametrize("build", ["sah", "lbvh"])
+def test_lane_priority_change_after_library_lane_frames(gpu_lib, build):
+    """Option "lane_priority" destroys the scene's lane streams (recreated at the next frame).  After frames on those
+    lanes (overlap, opts.stream NULL, NO_SYNC), nothing may keep a handle to them: rt_synchronize (drain() waits on the
+    last frame's stream) and the next frames (GPU-built frames compare the frame block's chain stream) must work and
+    render the same frames (a stale last_stream made that drain wait on a destroyed stream)."""
+    import torch
+    s = scenes.demo_with_particles(10)
+    W, H = 160, 96
+    r = Renderer(s).build_acceleration_structure(0, mode=build).configure_camera(W, H, ray_trace_depth=2)
+    ref = [r.render(f)[0] for f in range(6)]
+    r.set_option("overlap", 3)
+    for value in (0, 1, 0):
+        outs = []
+        for f in range(6):
+            o = torch.empty(W * H * 4, dtype=torch.uint8, device="cuda")
+            r.render(f, want_rgba=False, rgba8_device=o.data_ptr(), sync=False)
+            outs.append(o)
+        r.set_option("lane_priority", value)       # drains, then destroys the lane streams the frames ran on
+        r.synchronize()
+        for f, o in enumerate(outs):
+            assert np.array_equal(o.cpu().numpy().reshape(H, W, 4), ref[f]), (value, f)
+    assert np.array_equal(r.render(3)[0], ref[3])
+    r.cleanup()
+
+
 def test_synchronous_frame_after_pipelined_frames(gpu_lib):
     """A synchronous call behind NO_SYNC frames still in flight on the scene's own lanes (auto overlap): every frame
     equals its single-launch render, three bursts in a row."""

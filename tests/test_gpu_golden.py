@@ -78,11 +78,15 @@ def _single_prim_scene(kind, prim):
     return s
 
 
+@pytest.mark.parametrize("build", ["compat", "sah", "lbvh"])
+@pytest.mark.parametrize("exact", [True, False])
 @pytest.mark.parametrize("kind", ["sphere", "tri", "quad"])
-def test_prim_kats_through_trace(gpu_lib, kind):
-    """The KAT rays traced through a one-primitive scene (identity instance): t bit-identical to the
-    oracle's single-primitive hit function; the parallelogram's hits are additionally clipped by its
-    q-centred box (Parallelogram.cu:48-50), so there the GPU hits must be a subset."""
+def test_prim_kats_through_trace(gpu_lib, kind, exact, build):
+    """The KAT rays traced through a one-primitive scene (identity instance), EXACT and FAST kernels, every builder:
+    t bit-identical to the oracle's single-primitive hit function; the parallelogram's hits are additionally clipped
+    by its q-centred box (Parallelogram.cu:48-50), so there the GPU hits must be exactly the KAT hits whose ray meets
+    that box under the reference's slab — the FAST kernel's box decisions included (rt_trace_rays takes exact
+    decisions: binary pairs, marginal decisions re-taken with the reference's slab)."""
     from rtamd import abi
     g = np.load(os.path.join(GOLDEN, "prim_kats.npz"))
     rays, out = g[f"{kind}_rays"], g[f"{kind}_out"]
@@ -98,8 +102,8 @@ def test_prim_kats_through_trace(gpu_lib, kind):
             t.normal[i] = abi.Vec3(*v)
         t.has_normals = 1
         prims["tri"] = t
-    r = Renderer(_single_prim_scene(kind, prims[kind]), update=False).build_acceleration_structure(0)
-    h = r.trace_rays(rays, exact=True)
+    r = Renderer(_single_prim_scene(kind, prims[kind]), update=False).build_acceleration_structure(0, mode=build)
+    h = r.trace_rays(rays, exact=exact)
     gpu_hit = h["instance"] != 0xFFFFFFFF
     kat_hit = out[:, 0] > 0
     if kind == "quad":
@@ -121,3 +125,4 @@ def test_prim_kats_through_trace(gpu_lib, kind):
     assert np.array_equal(h["t"][m], out[m, 1])
     assert np.array_equal(h["point"][m], out[m, 2:5])
     assert np.abs(h["normal"][m] - out[m, 5:8]).max() <= 2e-7
+    r.cleanup()

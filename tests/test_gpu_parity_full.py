@@ -167,3 +167,30 @@ def test_fast_math_option_measured_bar(gpu_lib, case):
         if depth == 1:
             fd = np.abs(got[f][1] - orc[f][0]).max(axis=-1)
             assert (fd <= 1e-3).mean() >= 0.9999, (name, f, float(fd.max()))
+
+
+@pytest.mark.parametrize("name", ["C2", "C3", "C5"])
+def test_fast_equals_exact_on_bench_lbvh_trees(gpu_lib, name):
+    """GPU-built trees (RT_BUILD_LBVH; C5's benched configuration: every BLAS rebuilt each frame, no cold records,
+    instance group) in the FAST kernel's default traversal — quads of two binary levels in the reference's pair order —
+    against the EXACT kernel on the same trees: since round 6 every FAST box decision on these trees that lies inside
+    the reciprocal slab's error margin is re-taken with the reference's division slab (RT_XBOX_GPU, as on the
+    reference's own trees), so the float frames are bit-identical, frames 0 and 37 (round 5, without the re-take: C5
+    frame 37 had one more outlier against the oracle than the same trees in binary order).
+    Reference: src/AS/BoundingBox.cu:44-66, include/Util/Range.cuh:33-43."""
+    base, cam = CASES[name]
+    cfg = scenes.CONFIGS[base]
+    scene = scenes.config_scene(cfg)
+    W, H = cfg.width, cfg.height
+    r = Renderer(scene)
+    if name == "C5":
+        r.set_option("rebuild", 1)            # before the build, as bench.py sets it (no cold records)
+    r.build_acceleration_structure(0, mode="lbvh").configure_camera(W, H, **cam)
+    assert r.info()["device_bytes"] > 0
+    for f in FRAMES:
+        _, frgb, _ = r.render(f, want_rgb=True)
+        _, ergb, _ = r.render(f, exact=True, want_rgb=True)
+        mism = int((frgb != ergb).any(axis=-1).sum())
+        print(f"{name} LBVH frame {f}: FAST vs EXACT {mism} pixels differ, max {float(np.abs(frgb - ergb).max()):.4g}")
+        assert mism == 0, (name, f, mism)
+    r.cleanup()
