@@ -317,10 +317,10 @@ rt_status rt_trace_rays(rt_scene *scene, const float *rays_host, size_t ray_coun
  * the reference's slab, so they keep exactly the boxes the reference keeps. */
 typedef enum rt_box_mode {
     RT_BOX_REFERENCE = 0,      /* EXACT kernel: the reference's division slab */
-    RT_BOX_CULL = 1,           /* FAST single-box cull (greedy-quad scenes' instance / root boxes) */
-    RT_BOX_DECIDE = 2,         /* FAST single box, exact decisions (binary pairs, the reference's and GPU-built trees) */
-    RT_BOX_QUAD_PAIR = 3,      /* FAST quad slot, pair order, exact decisions (the reference's and GPU-built trees) */
-    RT_BOX_QUAD_GREEDY = 4     /* FAST quad slot of a greedy-collapsed host SAH tree (conservative cull) */
+    RT_BOX_CULL = 1,           /* FAST single-box cull (SAH / GPU-built scenes' instance and root boxes) */
+    RT_BOX_DECIDE = 2,         /* FAST single box, exact decisions (binary pairs; the reference's trees; "exact_decisions") */
+    RT_BOX_QUAD_PAIR = 3,      /* FAST quad slot, pair order, exact decisions (the reference's trees; "exact_decisions") */
+    RT_BOX_QUAD_GREEDY = 4     /* FAST quad slot, conservative cull (host SAH trees; GPU-built trees by default) */
 } rt_box_mode;
 rt_status rt_box_test(int device, const float *boxes_host, const float *rays_host, const float *tmax_host, size_t count,
                       uint32_t mode, uint8_t *hit_host, float *te_host);
@@ -364,6 +364,10 @@ rt_status rt_box_test(int device, const float *boxes_host, const float *rays_hos
  *   "wide"      : FAST persistent kernel: 1 (default) = quad trees (the reference's trees and GPU-built ones: two
  *                 binary levels per quad visited in the binary tree's order; RT_BUILD_SAH: the greedy collapse
  *                 visited by entry t), 0 = binary node pairs
+ *   "exact_decisions": RT_BUILD_LBVH: 1 = the FAST kernel re-takes every box decision and pair-order comparison inside
+ *                 its slabs' error margin with the reference's slab, as it always does on the reference's own trees, so
+ *                 its frames equal the EXACT kernel's on the same trees bit for bit (C5: ~35 % slower per launch:
+ *                 sibling boxes' entry t's often tie); 0 (default) = conservative culls (frames within SURVEY's bars)
  *   "cold_records": RT_BUILD_LBVH: 1 = the GPU builder writes TriCold records (normals, material, caller index) beside
  *                 TriHot; 0 = a hit reads the caller's triangle instead; -1 (default) = 1 unless "rebuild" is 1 at
  *                 rt_scene_build (same pixels either way; set before rt_scene_build, as is "rebuild" to take effect)

@@ -183,6 +183,7 @@ struct rt_scene {
     DevBuf<NodePair> blas_pairs;
     DevBuf<NodeQuad> blas_quads;    // option "wide"
     bool wide = true;               // FAST persistent kernel traverses the quad trees (host-built modes)
+    bool exact_decisions = false;   // option "exact_decisions": GPU-built trees take the exact-decision traversal (mode 3)
     uint32_t lds_scene = 2;         // quad-tree kernel: 1 = TLAS quads (+ instance hot records) in LDS when they
                                     // fit, 2 = also sphere / parallelogram records and instance cold records
     // option "grid_pct": the persistent grid as a percentage of the resident capacity; 0 = auto: 50 when
@@ -852,10 +853,12 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.tlas_quads = reinterpret_cast<const NodeQuad *>(s->frame_dev[b] + s->off_quads);
     g.blas_quads = s->blas_quads.p;
     // quad trees (GPU-built: from collapse_wide): 1 = host SAH BLASes collapsed greedily, visited by entry t; 2 = two
-    // binary levels per quad visited in the reference's order (GPU-built trees); 3 = the same on the reference's own
-    // trees, with every box decision inside the FAST slab's error margin re-taken with the reference's slab
+    // binary levels per quad visited in the reference's order (GPU-built trees); 3 = the same with every box decision
+    // inside the FAST slab's error margin re-taken with the reference's slab (the reference's own trees; GPU-built
+    // trees with option "exact_decisions")
     g.wide = s->wide && s->blas_quads.p != nullptr
-                 ? (s->quad_halves() ? (s->build_mode == RT_BUILD_COMPAT_MEDIAN ? 3u : 2u) : 1u) : 0u;
+                 ? (s->quad_halves() ? ((s->build_mode == RT_BUILD_COMPAT_MEDIAN || s->exact_decisions) ? 3u : 2u) : 1u)
+                 : 0u;
     g.tlas_slots = reinterpret_cast<const uint32_t *>(s->frame_dev[b] + s->off_slots);
     const bool gpu_slots = s->gpu_tlas() && s->block_by_slot[b];   // the slot-ordered copies of GPU-built frames
     g.inst_hot = reinterpret_cast<const InstHot *>(s->frame_dev[b] + (gpu_slots ? s->off_hot_s : s->off_hot));
@@ -2193,6 +2196,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     } else if (k == "wide") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "wide must be 0 or 1");
         s->wide = value == 1;
+    } else if (k == "exact_decisions") {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "exact_decisions must be 0 or 1");
+        s->exact_decisions = value == 1;
     } else if (k == "tlas_classes") {
         if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_classes must be 0 or 1");
         s->tlas_size_classes = value == 1;

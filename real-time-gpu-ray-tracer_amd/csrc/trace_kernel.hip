@@ -89,7 +89,8 @@ static_assert(LDS_DEPTH % 4 == 0, "half-pages move as 16 B pieces");
                                         // reference's trees the traversal takes the reference's decisions
 #endif
 // the persistent kernel's traversal modes (SceneGPU::wide): 0 binary node pairs, 1 greedy quads by entry t (host SAH
-// trees), 2 two-level quads in pair order (GPU-built trees), 3 the same on the reference's trees.
+// trees), 2 two-level quads in pair order (GPU-built trees), 3 the same with exact decisions (the reference's trees, and
+// GPU-built trees with option "exact_decisions").
 // Exact-decision level of a traversal instance (template argument XB):
 //   XD_CULL: conservative culls only;
 //   XD_PAR : also every box test of a ray with a parallel axis (|d| < 1e-6) re-taken with the reference's slab — the
@@ -98,23 +99,17 @@ static_assert(LDS_DEPTH % 4 == 0, "half-pages move as 16 B pieces");
 //            trees (mode 1) run at XD_CULL (RT_XPAR_SAH 0): that case is their one documented exception to "a FAST cull
 //            never rejects a box the reference keeps" (tests/test_gpu_box.py pins it to exactly that case);
 //   XD_ALL : also every decision inside the slabs' error margin, and (pair order) every comparison of two entry t's
-//            inside it: the traversal takes the reference's decisions.  The binary pairs, the reference's trees and (since
-//            round 6, RT_XBOX_GPU) the GPU-built trees — FAST equals EXACT on the same trees (C5's benched LBVH trees).
+//            inside it: the traversal takes the reference's decisions.  The binary pairs and mode 3 — FAST then equals EXACT
+//            on the same trees (tests/test_gpu_parity_full.py: the reference's trees, and C5's benched LBVH trees).
 #ifndef RT_XBOX_GPU
-#define RT_XBOX_GPU 1
+#define RT_XBOX_GPU 0                   // mode 2 at XD_ALL: C5 8.8 -> 11.9 ms, C2-LBVH 0.38 -> 0.49 ms serialised (ties
+                                        // between sibling boxes' entries are common, profiles/r06/exact_decisions/): GPU-built
+                                        // trees take exact decisions as mode 3, with option "exact_decisions"
 #endif
 #ifndef RT_XPAR_SAH
 #define RT_XPAR_SAH 0                   // host SAH trees at XD_PAR: C2 +4.4 %, C3 +2.5 % per frame (profiles/r06/exact_decisions/)
 #endif
 constexpr int XD_CULL = 0, XD_PAR = 1, XD_ALL = 2;
-// RT_XD_REL: the XD_ALL instances compute slab planes as (b - o) * (1/d) — two operations per plane instead of one FMA on
-// o / d — whose error is relative to t alone (<= 2^-21.9 |t|; the FMA form's carries 2^-24 |o / d|, i.e. a margin of
-// ~0.02 for a bounce ray with a shallow axis 100 units from the origin), so decisions inside the margin, and their
-// re-takes, stay rare (round 6: C5 14.7 -> ... ms serialised)
-#ifndef RT_XD_REL
-#define RT_XD_REL 1
-#endif
-template <int XB> __device__ constexpr bool rel_planes() { return RT_XD_REL && XB == XD_ALL; }
 #define XBOX(W) (!RT_BOX_EXACT ? XD_CULL : (((W) == 0 || (W) == 3 || (RT_XBOX_GPU && (W) == 2)) ? XD_ALL \
                                            : (RT_XPAR_SAH ? XD_PAR : XD_CULL)))
 #ifndef RT_NZ_MIN
@@ -241,10 +236,7 @@ __device__ __forceinline__ void prep(RayP &r) {
     r.inv = mk(rcp(nz(r.d.x)), rcp(nz(r.d.y)), rcp(nz(r.d.z)));
     r.oinv = mk(r.o.x * r.inv.x, r.o.y * r.inv.y, r.o.z * r.inv.z);
 #if RT_SLAB_CONS
-    if (rel_planes<XB>()) {     // (b - o) * inv: within 2^-21.9 |t| of the reference's plane, no absolute part
-        const bool par = fabsf(r.d.x) < RT_NZ_MIN || fabsf(r.d.y) < RT_NZ_MIN || fabsf(r.d.z) < RT_NZ_MIN;
-        r.pad = par ? -0.0f : 0.0f;
-    } else {   // fmaf(b, inv, -oinv) differs from (b - o) / d by <= 2^-24 |o / d| (oinv's rounding) + ~2^-21.7 |t| (the
+    {   // fmaf(b, inv, -oinv) differs from (b - o) / d by <= 2^-24 |o / d| (oinv's rounding) + ~2^-21.7 |t| (the
         // reciprocal's 1 ulp, the fma's and the reference's roundings); parallel axes only decide inside / outside
         const float px = fabsf(r.d.x) < RT_NZ_MIN ? 0.0f : fabsf(r.oinv.x);
         const float py = fabsf(r.d.y) < RT_NZ_MIN ? 0.0f : fabsf(r.oinv.y);
@@ -311,16 +303,9 @@ __device__ __forceinline__ bool slab(const float *b, const RayP &r, float tmin, 
 #if RT_EXACT
     return slab_ref(b, r.o, r.d, tmin, tmax, te);
 #else
-    float tx1, tx2, ty1, ty2, tz1, tz2;
-    if (rel_planes<XB>()) {
-        tx1 = (b[0] - r.o.x) * r.inv.x; tx2 = (b[1] - r.o.x) * r.inv.x;
-        ty1 = (b[2] - r.o.y) * r.inv.y; ty2 = (b[3] - r.o.y) * r.inv.y;
-        tz1 = (b[4] - r.o.z) * r.inv.z; tz2 = (b[5] - r.o.z) * r.inv.z;
-    } else {
-        tx1 = fmaf(b[0], r.inv.x, -r.oinv.x); tx2 = fmaf(b[1], r.inv.x, -r.oinv.x);
-        ty1 = fmaf(b[2], r.inv.y, -r.oinv.y); ty2 = fmaf(b[3], r.inv.y, -r.oinv.y);
-        tz1 = fmaf(b[4], r.inv.z, -r.oinv.z); tz2 = fmaf(b[5], r.inv.z, -r.oinv.z);
-    }
+    const float tx1 = fmaf(b[0], r.inv.x, -r.oinv.x), tx2 = fmaf(b[1], r.inv.x, -r.oinv.x);
+    const float ty1 = fmaf(b[2], r.inv.y, -r.oinv.y), ty2 = fmaf(b[3], r.inv.y, -r.oinv.y);
+    const float tz1 = fmaf(b[4], r.inv.z, -r.oinv.z), tz2 = fmaf(b[5], r.inv.z, -r.oinv.z);
     const float lo = fmaxf(fmaxf(tmin, fminf(tx1, tx2)), fmaxf(fminf(ty1, ty2), fminf(tz1, tz2)));
     const float hi = fminf(fminf(tmax, fmaxf(tx1, tx2)), fminf(fmaxf(ty1, ty2), fmaxf(tz1, tz2)));
     te = lo;
@@ -764,15 +749,13 @@ __device__ __forceinline__ R lds_or_global(uint32_t at, const R *g, uint32_t k) 
 // one axis of the 4 slot slab tests; pa / pb: that axis's contribution to the entry t of the halves' boxes (a
 // half's box is the union of its two slots' boxes, and the plane distances are monotone in the bound, so its near
 // plane is the nearer of its slots' near planes)
-// REL: c = o, planes (b - o) * inv (rel_planes); else c = o / d, planes fmaf(b, inv, -c)
-template <bool PAIR, bool REL = false>
-__device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float c, float4 &tn, float4 &tf,
+template <bool PAIR>
+__device__ __forceinline__ void slab4(const float4 &lo, const float4 &hi, float inv, float oinv, float4 &tn, float4 &tf,
                                       float &pa, float &pb) {
-    const auto pl = [&](float b) { return REL ? (b - c) * inv : fmaf(b, inv, -c); };
-    const float a0 = pl(lo.x), b0 = pl(hi.x);
-    const float a1 = pl(lo.y), b1 = pl(hi.y);
-    const float a2 = pl(lo.z), b2 = pl(hi.z);
-    const float a3 = pl(lo.w), b3 = pl(hi.w);
+    const float a0 = fmaf(lo.x, inv, -oinv), b0 = fmaf(hi.x, inv, -oinv);
+    const float a1 = fmaf(lo.y, inv, -oinv), b1 = fmaf(hi.y, inv, -oinv);
+    const float a2 = fmaf(lo.z, inv, -oinv), b2 = fmaf(hi.z, inv, -oinv);
+    const float a3 = fmaf(lo.w, inv, -oinv), b3 = fmaf(hi.w, inv, -oinv);
     const float n0 = fminf(a0, b0), n1 = fminf(a1, b1), n2 = fminf(a2, b2), n3 = fminf(a3, b3);
     tn = make_float4(fmaxf(tn.x, n0), fmaxf(tn.y, n1), fmaxf(tn.z, n2), fmaxf(tn.w, n3));
     tf = make_float4(fminf(tf.x, fmaxf(a0, b0)), fminf(tf.y, fmaxf(a1, b1)), fminf(tf.z, fmaxf(a2, b2)), fminf(tf.w, fmaxf(a3, b3)));
@@ -805,10 +788,9 @@ __device__ __forceinline__ void quad_decide(const float4 *Q, const float4 &lx, c
     pa = t0; pb = t0;                                // entry t of the two halves' boxes
     {
         float4 tn = make_float4(t0, t0, t0, t0), tf = make_float4(tmax, tmax, tmax, tmax);
-        constexpr bool REL = rel_planes<XB>();
-        slab4<PAIR, REL>(lx, hx, r.inv.x, REL ? r.o.x : r.oinv.x, tn, tf, pa, pb);
-        slab4<PAIR, REL>(ly, hy, r.inv.y, REL ? r.o.y : r.oinv.y, tn, tf, pa, pb);
-        slab4<PAIR, REL>(lz, hz, r.inv.z, REL ? r.o.z : r.oinv.z, tn, tf, pa, pb);
+        slab4<PAIR>(lx, hx, r.inv.x, r.oinv.x, tn, tf, pa, pb);
+        slab4<PAIR>(ly, hy, r.inv.y, r.oinv.y, tn, tf, pa, pb);
+        slab4<PAIR>(lz, hz, r.inv.z, r.oinv.z, tn, tf, pa, pb);
         if (XB == XD_ALL) {
             const auto below = [&](float v) { return fmaf(fabsf(v), 0x1p-19f, v + 2.0f * fabsf(r.pad)) < TMIN; };
             low[0] = below(tn.x); low[1] = below(tn.y); low[2] = below(tn.z); low[3] = below(tn.w);
@@ -833,25 +815,33 @@ __device__ __forceinline__ void quad_decide(const float4 *Q, const float4 &lx, c
     h[3] = h[3] && R.w != REF_EMPTY;
 #if RT_SLAB_CONS && RT_BOX_EXACT
     if (XB != XD_CULL) {   // Rare: a hit decision inside the error margin, a ray with a parallel axis, or (pair order) two entry t's the order
-        // compares inside the margin — then every box of the node is re-tested with the reference's slab (the halves'
-        // boxes too: unions of their slots' boxes), on the node's bounds read again (keeping the 24 bounds live through
-        // the step would cost registers on the hot path), one box per iteration so that one copy of the division slab
-        // serves all six
-        const auto close = [&](float a, float b) { return fabsf(a - b) <= box_margin(a, b, r.pad); };
+        // compares inside the margin — then the boxes involved (a ray with a parallel axis: every box of the node) are
+        // re-tested with the reference's slab (a half's box: the union of its slots' boxes), on the node's bounds read
+        // again (keeping the 24 bounds live through the step would cost registers on the hot path), one box per
+        // iteration so that one copy of the division slab serves all six.  Boxes of the mask m: bit k = slot k, bits 4 / 5
+        // = the halves.  Re-taking only the two entries a close comparison involves (round 6) instead of all six boxes
+        // took C5 from ... ms per serialised launch.
+#ifndef RT_XD_DIAG
+#define RT_XD_DIAG 0
+#endif
+        const auto close = [&](float a, float b) {
+            return fabsf(a - b) <= box_margin(a, b, r.pad) && !((RT_XD_DIAG & 8) && a == b);
+        };
 #ifndef RT_XD_DIAG
 #define RT_XD_DIAG 0                    // diagnostic builds only: 1 no pair-order trigger, 2 no margin trigger, 4 no parallel
 #endif
-        bool need = !(RT_XD_DIAG & 4) && ray_parallel(r);
+        uint32_t m = (!(RT_XD_DIAG & 4) && ray_parallel(r)) ? (PAIR ? 0x3Fu : 0xFu) : 0u;
         if (XB == XD_ALL && !(RT_XD_DIAG & 2))
-            need = need || (h[0] && und[0]) || (h[1] && und[1]) || (h[2] && und[2]) || (h[3] && und[3]);
+            m |= (h[0] && und[0] ? 1u : 0u) | (h[1] && und[1] ? 2u : 0u) | (h[2] && und[2] ? 4u : 0u) | (h[3] && und[3] ? 8u : 0u);
         if (PAIR && XB == XD_ALL && !(RT_XD_DIAG & 1))
-            need = need || (h[0] && h[1] && !(low[0] && low[1]) && close(t[0], t[1])) ||
-                   (h[2] && h[3] && !(low[2] && low[3]) && close(t[2], t[3])) ||
-                   ((h[0] || h[1]) && (h[2] || h[3]) && !(low_a && low_b) && close(pa, pb));
-        if (need) {
+            m |= (h[0] && h[1] && !(low[0] && low[1]) && close(t[0], t[1]) ? 0x3u : 0u) |
+                 (h[2] && h[3] && !(low[2] && low[3]) && close(t[2], t[3]) ? 0xCu : 0u) |
+                 ((h[0] || h[1]) && (h[2] || h[3]) && !(low_a && low_b) && close(pa, pb) ? 0x30u : 0u);
+        if (m) {
             const float4 L[6] = {Q[0], Q[1], Q[2], Q[3], Q[4], Q[5]};
 #pragma unroll 1
-            for (int j = 0; j < (PAIR ? 6 : 4); j++) {
+            for (; m; m &= m - 1u) {
+                const int j = __builtin_ctz(m);
                 const int k0 = j < 4 ? j : 2 * (j - 4), k1 = j < 4 ? j : k0 + 1;     // a slot, or a half's two slots
                 float b[6];
 #pragma unroll
@@ -1939,6 +1929,10 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
     // data lives (finalize's RAW; GPU-built trees are always in pair order)
     if (sc.wide && HAS_WIDE) {
         if (sc.raw_tris) {
+            if (sc.wide == 3) {
+                if (variant == 4) return launch_persistent_wpe<4, 3 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+                return launch_persistent_wpe<3, 3 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+            }
             if (variant == 4) return launch_persistent_wpe<4, 2 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
             return launch_persistent_wpe<3, 2 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
         }
@@ -1962,6 +1956,7 @@ hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraG
 // the occupancy of the instance launch_render_persistent runs for (wide, raw): the persistent grid is sized from it
 uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, uint32_t wide, bool raw) {
     if (wide && HAS_WIDE) {
+        if (raw && wide == 3) return variant == 4 ? blocks_per_cu_wpe<4, 3 * HAS_WIDE, 1>() : blocks_per_cu_wpe<3, 3 * HAS_WIDE, 1>();
         if (raw) return variant == 4 ? blocks_per_cu_wpe<4, 2 * HAS_WIDE, 1>() : blocks_per_cu_wpe<3, 2 * HAS_WIDE, 1>();
 #if !RT_XBOX_GPU
         if (wide == 3) return variant == 4 ? blocks_per_cu_wpe<4, 3 * HAS_WIDE, 0>() : blocks_per_cu_wpe<3, 3 * HAS_WIDE, 0>();

@@ -102,6 +102,51 @@ def world_c4(n=8, lanes=8, frames=(0, 37)):
     return bad, time.time() - t0
 
 
+def world_c5(n=8, frames=(0, 5)):
+    """bench.py's N > 1 configuration of C5 (verdict r5 item 1): 10 M triangles at 3840x2160, 8 -> 4 traced spp, depth 2,
+    the GPU LBVH with every BLAS and the TLAS rebuilt each frame ("rebuild" set before the build, as bench.py does:
+    no cold records), the scene's own lanes ("overlap" -1 before the attach: 8 communicators; with the rebuild the
+    library runs 2 lanes), 32x32 tiles over n ranks, frames 0..max(frames) pipelined with RT_RENDER_NO_SYNC and no
+    caller stream — the scene stream's rebuilds, the lane streams' traces and the communicators' sends / receives all
+    in flight together; rank 0's kept frames against single-launch frames of a scene built and rebuilt the same way."""
+    cfg = scenes.CONFIGS["C5"]
+    scene = scenes.config_scene(cfg)
+    cam = dict(sample_count=cfg.spp, ray_trace_depth=cfg.depth)
+    Wc, Hc = cfg.width, cfg.height
+
+    def c5_scene():
+        r = Renderer(scene)
+        r.set_option("rebuild", 1)
+        return r.build_acceleration_structure(0, mode="lbvh").configure_camera(Wc, Hc, **cam)
+
+    ref_r = c5_scene()
+    ref = {f: ref_r.render(f)[0] for f in frames}
+    ref_r.cleanup()
+    rs = [c5_scene() for _ in range(n)]
+    cid = Renderer.comm_unique_id()
+    for k, r in enumerate(rs):
+        r.set_option("overlap", -1)
+        r.attach_comm(cid, k, n, TILE, TILE)
+        r.set_comm_timeout(120000)
+    keep = {f: torch.zeros(Wc * Hc * 4, dtype=torch.uint8, device="cuda") for f in frames}
+    scratch = [torch.zeros(Wc * Hc * 4, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for f in range(max(frames) + 1):
+        buf = keep[f] if f in keep else scratch[f % 2]
+        for k in reversed(range(n)):
+            rs[k].render(f, want_rgba=False, rgba8_device=buf.data_ptr() if k == 0 else None, sync=False)
+    for r in rs:
+        r.synchronize()
+    torch.cuda.synchronize()
+    dt = time.time() - t0
+    lanes = int(rs[0].info()["overlap_lanes"])
+    bad = [f for f in frames if not np.array_equal(keep[f].cpu().numpy().reshape(Hc, Wc, 4), ref[f])]
+    for r in rs:
+        r.cleanup()
+    return bad, dt, lanes
+
+
 def main():
     assert os.environ.get("RTAMD_RCCL_LIB"), "run through tests/test_gpu_fake_rccl.py"
     if len(sys.argv) > 1 and sys.argv[1] == "c4":
@@ -109,6 +154,14 @@ def main():
         bad, dt = world_c4()
         print(json.dumps({"world": 8, "config": "C4", "lanes": 8, "communicators": 8, "stage_depth": 64, "tile": TILE,
                           "frames": [0, 37], "frames_differing": bad, "s": round(dt, 2)}), flush=True)
+        assert not bad, bad
+        print(json.dumps({"ok": True}), flush=True)
+        return
+    if len(sys.argv) > 1 and sys.argv[1] == "c5":
+        torch.cuda.set_device(0)
+        bad, dt, lanes = world_c5()
+        print(json.dumps({"world": 8, "config": "C5", "build": "lbvh", "rebuild": True, "lanes": lanes, "communicators": 8,
+                          "tile": TILE, "frames": [0, 5], "frames_differing": bad, "s": round(dt, 2)}), flush=True)
         assert not bad, bad
         print(json.dumps({"ok": True}), flush=True)
         return

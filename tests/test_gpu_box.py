@@ -2,14 +2,14 @@
 
 The FAST kernels cull with reciprocal-direction planes (one FMA per plane) and widen the interval by a bound on its
 distance from the reference's, so a FAST cull never rejects a box the reference keeps; the exact-decision kernels
-(binary pairs, quads of the reference's trees and, since round 6, of GPU-built trees) re-take every decision inside
-that margin with the reference's division slab.  Checked here per mode of include/rt.h `rt_box_mode`:
+(binary pairs, quads of the reference's trees and, with option "exact_decisions", of GPU-built trees) re-take every
+decision inside that margin with the reference's division slab.  Checked here per mode of include/rt.h `rt_box_mode`:
 
   * RT_BOX_REFERENCE (the EXACT kernel): hit flag and entry t bit-identical to the golden AABB KATs (oracle);
   * RT_BOX_DECIDE / RT_BOX_QUAD_PAIR: the same hit flags as the KATs, for every ray (the decisions of the W = 0 / 2 / 3
     instances), entry t within the margin (bit-identical wherever the decision was re-taken);
-  * RT_BOX_CULL / RT_BOX_QUAD_GREEDY (host SAH trees): a superset of the KAT hits — never a missed hit the reference
-    keeps; an extra one only inside the margin.
+  * RT_BOX_CULL / RT_BOX_QUAD_GREEDY (host SAH and, by default, GPU-built trees): a superset of the KAT hits — never a
+    missed hit the reference keeps but for the documented parallel-axis-on-a-face case; extras only inside the margin.
 
 Beyond the 4 096 golden rays (10 % with a zero direction component): crafted rays with a parallel axis whose origin
 lies exactly on a face, on an edge or a corner of the box (the reference keeps q == min / max, BoundingBox.cu:47),

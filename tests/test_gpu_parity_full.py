@@ -172,11 +172,12 @@ def test_fast_math_option_measured_bar(gpu_lib, case):
 @pytest.mark.parametrize("name", ["C2", "C3", "C5"])
 def test_fast_equals_exact_on_bench_lbvh_trees(gpu_lib, name):
     """GPU-built trees (RT_BUILD_LBVH; C5's benched configuration: every BLAS rebuilt each frame, no cold records,
-    instance group) in the FAST kernel's default traversal — quads of two binary levels in the reference's pair order —
-    against the EXACT kernel on the same trees: since round 6 every FAST box decision on these trees that lies inside
-    the reciprocal slab's error margin is re-taken with the reference's division slab (RT_XBOX_GPU, as on the
-    reference's own trees), so the float frames are bit-identical, frames 0 and 37 (round 5, without the re-take: C5
-    frame 37 had one more outlier against the oracle than the same trees in binary order).
+    instance group) in the FAST kernel's quad traversal — two binary levels per quad in the reference's pair order —
+    with option "exact_decisions" (round 6): every FAST box decision and pair-order comparison on these trees that
+    lies inside the reciprocal slab's error margin is re-taken with the reference's division slab, as on the
+    reference's own trees, so the float frames equal the EXACT kernel's on the same trees bit for bit, frames 0 and 37.
+    (The default keeps conservative culls: the re-takes cost C5 ~35 % per launch; round 5's C5 frame 37
+    had one more outlier against the oracle than the same trees in binary order.)
     Reference: src/AS/BoundingBox.cu:44-66, include/Util/Range.cuh:33-43."""
     base, cam = CASES[name]
     cfg = scenes.CONFIGS[base]
@@ -185,6 +186,7 @@ def test_fast_equals_exact_on_bench_lbvh_trees(gpu_lib, name):
     r = Renderer(scene)
     if name == "C5":
         r.set_option("rebuild", 1)            # before the build, as bench.py sets it (no cold records)
+    r.set_option("exact_decisions", 1)
     r.build_acceleration_structure(0, mode="lbvh").configure_camera(W, H, **cam)
     assert r.info()["device_bytes"] > 0
     for f in FRAMES:
