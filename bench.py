@@ -57,7 +57,6 @@ def parse():
                    help="BVH builder: SAH (default), the reference's random-axis median split, or the GPU LBVH builder")
     p.add_argument("--rebuild", action="store_true", help="--build lbvh: rebuild every BLAS on the GPU each frame (C5)")
     p.add_argument("--kernel", type=int, default=1, help="1 = persistent megakernel, 0 = grid kernel")
-    p.add_argument("--threshold", type=int, default=None, help="refill threshold (default: the library's tuned value)")
     p.add_argument("--overlap", type=int, default=None,
                    help="L >= 2: consecutive frames cycle L streams / library lanes so frame k+1 fills the CUs "
                         "frame k's tail leaves idle; 0 or 1: frames are serialised (default 3)")
@@ -272,8 +271,6 @@ def main():
         r.set_option("rebuild", 1)
     r.build_acceleration_structure(0, mode=args.build).configure_camera(cfg.width, cfg.height)
     r.set_option("kernel", args.kernel)
-    if args.threshold is not None:
-        r.set_option("threshold", args.threshold)
     for kv in args.opt:
         k, v = kv.split("=")
         r.set_option(k, int(v, 0))
@@ -495,7 +492,7 @@ def main():
                                    ("current stream + new streams" if prio is None else f"new streams, priority {prio}")))),
                 "hw_queues": int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4),
                 "tile": TILE,
-                "threshold": args.threshold if args.threshold is not None else "auto (64 at depth x spp <= 2, else 40)",
+                "threshold": "auto (64 at depth x spp <= 2, else 40)",
                 "options": args.pre_opt + args.opt,
                 "kernel": ("EXACT" if args.exact else "FAST") + (" persistent" if args.kernel else " grid"),
                 "bvh": args.build,

@@ -325,95 +325,66 @@ typedef enum rt_box_mode {
 rt_status rt_box_test(int device, const float *boxes_host, const float *rays_host, const float *tmax_host, size_t count,
                       uint32_t mode, uint8_t *hit_host, float *te_host);
 
-/* Tuning knobs (defaults are the tuned values):
- *   "kernel"    : 0 = one-thread-per-pixel grid kernel, 1 = persistent-wave megakernel (default)
- *   "threshold" : persistent kernel — lanes that must be waiting before a wave leaves the
- *                 traversal loop to shade / regenerate (1..64; default 0 = auto: 64 when depth x samples <= 2,
- *                 else 40)
- *   "variant"   : persistent kernel register budget: 0 = compiler's choice, 4 = at least 4 waves per SIMD
- *   "fast_math" : FAST frames only: 1 = hardware reciprocal / rsq and FMA contraction in the primitive tests, transforms
- *                 and shading (about 8 % faster; 0.01-0.09 % of pixels then differ from the reference's arithmetic);
- *                 0 (default) = the reference's correctly rounded arithmetic wherever a value reaches a hit or a pixel
- *   "queue_parts": persistent kernel work-queue bands (1..8, default 8; a wave starts on band XCC_ID % parts)
- *   "reorder"   : 1 (default) = each launch claims its band's 8x8 units heaviest-first, ordered by the
- *                 traversal work the previous launch of the same layout and lane recorded per unit (schedule.hip);
- *                 0 = screen order.  Images are identical either way (the RNG is keyed by pixel).
- *   "reorder_period": with "reorder", K = a lane records unit costs on one launch in K and rebuilds its
- *                 claim order on the next; the other launches reuse the order (default 8; 1 = every launch)
- *   "split"     : with "reorder", heavy units are claimed in pieces shared by several waves: halves from
- *                 cost level k_half, quarters from k_quarter (value k_half | k_quarter << 8, levels 0..15 =
- *                 half-octaves of a unit's mean traversal steps per pixel; 0xFF = never; default 12 | 12 << 8)
- *   "nt_store"  : 1 = non-temporal RGBA8 stores
- *   "grab"      : pixels claimed per work-queue atomic (multiple of 8, default 64)
- *   "supertile" : walk each band in supertile x supertile units of 8x8 pixels (default 16; 0 = rows)
- *   "rebuild"   : RT_BUILD_LBVH only: 1 = rebuild every BLAS on the GPU every frame (default 0)
- *   "timeline"  : 1 = record a per-wave timeline of each persistent launch (debug)
- *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal steps (debug)
- *   "leaf_early": persistent kernel: a round's interior loop also ends once no more than this many lanes are still
- *                 looking for a leaf (0..64; 0 = when every traversing lane holds one); -1 (default) = auto: 0 for
- *                 paths of <= 2 segments (depth x samples), else 12.  Results are identical for every value
+/* Scene options (19 keys; every default is the measured best, so a drop-in caller sets none of them but
+ * "overlap").  Unknown keys return RT_ERR_INVALID_ARGUMENT.
+ * Frames and lanes:
+ *   "overlap"   : L = consecutive rt_render calls cycle through L (2..8) internal lanes (work-queue heads, unit costs,
+ *                 schedule); a launch waits only for the previous launch of its own lane and for its frame block, so
+ *                 frame k+1's launch runs in the CUs frame k's tail leaves idle.  Frames with opts.stream NULL run on
+ *                 lane streams the scene creates; a caller that passes streams cycles its own.  -1 = auto: the scene
+ *                 also picks L and the staging depth per frame kind (2 lanes with a per-frame rebuild, else 8 lanes /
+ *                 64 buffers for a rank's tile share, else 4).  With lanes the caller orders its own output buffers:
+ *                 device outputs of NO_SYNC frames without a stream are complete once rt_synchronize returns
+ *                 (default 0 = 1 lane: every launch of the scene is serialised)
+ *   "stage_depth": pinned host staging buffers the per-frame upload cycles through (2..64, default 16, allocated on
+ *                 first use): the host stages frame k once frame k - depth's trace is done (drains the scene)
  *   "lane_priority": the lane streams the scene creates for "overlap" frames without a caller stream: 1 (default) =
  *                 the device's highest stream priority (hardware queues of their own: full overlap at the default
  *                 GPU_MAX_HW_QUEUES of 4), 0 = normal priority
- *   "scene_priority": 1 = create the scene stream (uploads, GPU tree builds) at the device's highest priority;
- *                 0 (default).  Set before rt_scene_build (RT_ERR_STATE after)
- *   "tlas_sah"  : RT_BUILD_SAH: 1 (default) = build the per-frame host TLAS with SAH; 0 = the reference's median split
- *                 (TLAS.cu:4-129; "tlas_median_leaf" 1..2 = its leaf size, 0 = the reference's 2)
- *   "tlas_leaf" : instances per leaf of an SAH or GPU-built TLAS (1..4, default 1; GPU-built TLASes: set before
- *                 rt_scene_build)
+ *   "grid_pct"  : persistent grid as a percentage of the resident workgroup capacity (1..100; default 0 = auto:
+ *                 100 when no other lane's launch is in flight, else 50 with up to 3 lanes and 100 / lanes + 12
+ *                 with more, so several lanes' launches run side by side; a launch of >= 16 M camera paths: 100)
+ * GPU-built scenes (RT_BUILD_LBVH; the builder's options are set before rt_scene_build):
+ *   "rebuild"   : 1 = rebuild every BLAS on the GPU every frame (default 0)
+ *   "cold_records": 1 = the GPU builder writes TriCold records (normals, material, caller index) beside TriHot;
+ *                 0 = a hit reads the caller's triangle instead; -1 (default) = 1 unless "rebuild" is 1 at
+ *                 rt_scene_build (same pixels either way)
+ *   "blas_double": per-frame rebuilds: 1 = write a spare BLAS set and swap it in, so a frame's rebuild overlaps the
+ *                 previous frames' traces (default 1; 0 = one set, a rebuild waits for every lane's trace)
+ *   "blas_sets" : with "blas_double": BLAS sets cycled (2..3, default 3): frame k+1's rebuild waits only for the trace
+ *                 of frame k + 1 - sets
+ *   "tlas_small": 1 (default) = a GPU TLAS of at most 512 records is built by one workgroup in one launch; 0 = the
+ *                 multi-kernel builder (results identical up to the tree's shape)
+ *   "exact_decisions": 1 = the FAST kernel re-takes every box decision and pair-order comparison inside its slabs'
+ *                 error margin with the reference's slab, as it always does on the reference's own trees, so its
+ *                 frames equal the EXACT kernel's on the same trees bit for bit (C5: ~34 % slower per frame: sibling
+ *                 boxes' entry t's often tie); 0 (default) = conservative culls (frames within SURVEY's bars)
+ * Host-built scenes:
+ *   "group"     : triangle instances with bit-identical transforms (each with a BLAS of its own) share one BLAS over
+ *                 all their triangles, entered as one TLAS item while every member keeps that transform (default 1;
+ *                 set before rt_scene_build; hits report the member instance; 0 = one TLAS item per instance)
+ *   "gpu_tlas"  : RT_BUILD_SAH: 1 = keep the host-built SAH BLASes but compute the instance records and build the
+ *                 TLAS on the GPU every frame, as RT_BUILD_LBVH does.  Set before rt_scene_build (default 0)
+ *   "tlas_sah"  : RT_BUILD_SAH: 1 (default) = build the per-frame host TLAS with SAH; 0 = the reference's median
+ *                 split (TLAS.cu:4-129)
+ * Kernel:
+ *   "kernel"    : 0 = one-thread-per-pixel grid kernel, 1 = persistent-wave megakernel (default)
  *   "wide"      : FAST persistent kernel: 1 (default) = quad trees (the reference's trees and GPU-built ones: two
  *                 binary levels per quad visited in the binary tree's order; RT_BUILD_SAH: the greedy collapse
  *                 visited by entry t), 0 = binary node pairs
- *   "exact_decisions": RT_BUILD_LBVH: 1 = the FAST kernel re-takes every box decision and pair-order comparison inside
- *                 its slabs' error margin with the reference's slab, as it always does on the reference's own trees, so
- *                 its frames equal the EXACT kernel's on the same trees bit for bit (C5: ~35 % slower per launch:
- *                 sibling boxes' entry t's often tie); 0 (default) = conservative culls (frames within SURVEY's bars)
- *   "cold_records": RT_BUILD_LBVH: 1 = the GPU builder writes TriCold records (normals, material, caller index) beside
- *                 TriHot; 0 = a hit reads the caller's triangle instead; -1 (default) = 1 unless "rebuild" is 1 at
- *                 rt_scene_build (same pixels either way; set before rt_scene_build, as is "rebuild" to take effect)
- *   "blas_sets" : RT_BUILD_LBVH rebuilds with "blas_double": BLAS sets cycled (2..3, default 3): frame k+1's rebuild
- *                 waits only for the trace of frame k + 1 - sets (set before rt_scene_build)
- *   "blas_leaf" : RT_BUILD_SAH: primitives per BLAS leaf (1..4, default 4; set before rt_scene_build)
- *   "gpu_tlas"  : RT_BUILD_SAH: 1 = keep the host-built SAH BLASes but compute the instance records and
- *                 build the TLAS on the GPU every frame, as RT_BUILD_LBVH does (only changed instances
- *                 cross PCIe; no host TLAS build per frame).  Set before rt_scene_build (default 0)
- *   "inst_by_slot": 1 = host-built TLAS: stage the per-frame instance records in TLAS leaf-slot order
- *                 (default 1; 0 = instance order, for A/B — results are identical)
- *   "reserve"   : with "overlap", the persistent grid leaves this many workgroup slots free (default 16, two
- *                 per XCD) so the next lanes' schedule / upload / GPU TLAS kernels start beside the running launch
- *   "stage_depth": pinned host staging buffers the per-frame upload cycles through (2..64, default 16, allocated on
- *                 first use): the host stages frame k once frame k - depth's trace is done, so a larger depth lets
- *                 the host run further ahead of many overlapped lanes (drains the scene when changed)
- *   "blas_double": RT_BUILD_LBVH rebuilds (option "rebuild", rt_scene_update_triangles): 1 = write a spare BLAS
- *                 set and swap it in, so a frame's rebuild overlaps the previous frame's trace (default 1;
- *                 0 = one set, a rebuild waits for every lane's trace)
- *   "merge"     : "reorder": two adjacent 8x8 units whose recorded cost is below this level (0..16; levels are
- *                 half-octaves of steps per pixel) become one 128-pixel claim item (default 6; 0 = off)
- *   "group"     : RT_BUILD_SAH with a host-built TLAS: triangle instances with bit-identical transforms (each
- *                 with a BLAS of its own) share one SAH BLAS over all their triangles, entered as one TLAS item
- *                 while every member keeps that transform (default 1; set before rt_scene_build; hits report
- *                 the member instance; 0 = one TLAS item per instance)
- *   "lds_blas"  : with "lds_scene" 2 and "group": the top levels of the first group's BLAS (quads numbered level
- *                 by level) fill the rest of the LDS scene region (default 1; 0 = from HBM; results identical)
- *   "grid_pct"  : persistent grid as a percentage of the resident workgroup capacity (1..100; default 0 = auto:
- *                 100 when no other lane's launch is in flight, else 50 with up to 3 lanes and 100 / lanes + 12
- *                 with more (37 at 4 lanes, 24 at 8), so several lanes' launches run side by side)
- *   "lds_scene" : FAST quad-tree kernel: 1 = every workgroup copies the frame's TLAS quads and, when they fit
- *                 as well, the instance hot records into 19 KB of LDS and reads them there; 2 = also the
- *                 sphere / parallelogram records and the instance cold records, while they fit (default 2;
- *                 0 = all from HBM; results identical)
- *   "tlas_small": GPU-built frames (RT_BUILD_LBVH, "gpu_tlas"): 1 (default) = a TLAS of at most 512 records is built
- *                 by one workgroup in one launch; 0 = the multi-kernel builder (results identical up to the tree's
- *                 shape: inactive records are left out instead of sorted into a subtree no ray enters)
- *   "overlap"   : L = consecutive rt_render calls cycle through L (2..8) internal lanes (work-queue
- *                 heads, unit costs, schedule); a launch waits only for the previous launch of its own
- *                 lane and for its frame block, so frame k+1's launch runs in the CUs frame k's tail
- *                 leaves idle.  Frames with opts.stream NULL run on lane streams the scene creates; a
- *                 caller that passes streams cycles its own.  -1 = auto: the scene also picks L and the
- *                 staging depth per frame kind (2 lanes with a per-frame rebuild, else 8 lanes / 64
- *                 buffers for a rank's tile share, else 4).  With lanes the caller orders
- *                 its own output buffers: device outputs of NO_SYNC frames without a stream are complete
- *                 once rt_synchronize returns (default 0 = 1 lane: every launch of the scene is serialised) */
+ *   "fast_math" : FAST frames only: 1 = hardware reciprocal / rsq and FMA contraction in the primitive tests, transforms
+ *                 and shading (about 8 % faster; 0.01-0.09 % of pixels then differ from the reference's arithmetic);
+ *                 0 (default) = the reference's correctly rounded arithmetic wherever a value reaches a hit or a pixel
+ *   "reorder"   : 1 (default) = each launch claims its band's 8x8 units heaviest-first, ordered by the traversal work
+ *                 the lane's last recording launch measured per unit (schedule.hip); 0 = screen order.  Images are
+ *                 identical either way (the RNG is keyed by pixel)
+ * Debug:
+ *   "timeline"  : 1 = record a per-wave timeline of each persistent launch
+ *   "costmap"   : 1 = with RT_RENDER_COUNT_WORK, record per-pixel traversal steps
+ * (Removed in round 6, measured defaults kept: threshold, leaf_early, queue_parts, grab, supertile, merge, split,
+ * reorder_period, reserve, lds_scene, lds_blas, inst_by_slot, blas_leaf, tlas_leaf, tlas_median_leaf; removed with
+ * their code as measured negative or neutral: variant, nt_store, cost_max, tlas_classes, wide_merge, scene_priority.
+ * DESIGN.md §4 keeps the measurements.) */
 rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
 
 /* Debug buffers of the last launch that recorded them (synchronises the scene's stream):

@@ -392,16 +392,13 @@ struct FlatWide {
     uint32_t height = 0;           // quad levels on the longest root-to-leaf path
 };
 
-// merge_cap > 0: a binary subtree holding <= merge_cap items (<= 4, the leaf ref's count field) becomes
-// one leaf — its leaves are contiguous slots (the builders emit leaves depth-first, left first).  Fewer,
-// fuller leaves mean fewer leaf rounds per ray for the same primitive tests.
 // level_order: quads numbered level by level (breadth first), so the first k quads are the tree's top
 // levels (the LDS-resident part of a group's BLAS); otherwise depth first
 // halves = false (host SAH trees): the greedy BVH2 -> BVH4 collapse instead — a quad starts from a binary node's two
 // children and repeatedly replaces its largest-area interior child by that child's two children until it holds 4
 // (fewer quads per ray; the kernel visits such quads by entry t); empty slots have every bound = +inf.
 inline FlatWide flatten_tree_wide(const Tree &t, uint32_t quad_base, uint32_t slot_base, uint32_t ptype, bool blas,
-                                  bool halves = true, uint32_t merge_cap = 0, bool level_order = false) {
+                                  bool halves = true, bool level_order = false) {
     FlatWide f;
     const uint32_t n = (uint32_t)t.nodes.size();
     if (n == 0) return f;
@@ -412,7 +409,7 @@ inline FlatWide flatten_tree_wide(const Tree &t, uint32_t quad_base, uint32_t sl
         if (nd.count > 0) { items[j] = nd.count; first[j] = nd.index; }
         else { items[j] = items[nd.index] + items[nd.index + 1]; first[j] = first[nd.index]; }
     }
-    auto is_leaf = [&](uint32_t j) { return t.nodes[j].count > 0 || (merge_cap && items[j] <= merge_cap); };
+    auto is_leaf = [&](uint32_t j) { return t.nodes[j].count > 0; };
     auto leaf_ref = [&](uint32_t j) { return make_leaf_ref(slot_base + first[j], items[j], ptype, blas); };
     if (is_leaf(0)) { f.root_ref = leaf_ref(0); return f; }
     struct Todo { uint32_t node, quad, depth; };

@@ -187,7 +187,7 @@ struct SceneGPU {
     uint32_t instance_count;
     uint32_t rough_count;           // material slot of metal m = rough_count + m
     uint32_t material_count;        // slots in `materials` (roughs + metals)
-    // option "lds_scene" (FAST persistent kernel, quad trees): the frame's TLAS quads (7 dwordx4 each, the
+    // setting "lds_scene" (FAST persistent kernel, quad trees): the frame's TLAS quads (7 dwordx4 each, the
     // pad dropped) and then, if they fit as well, the instance hot records (5 dwordx4 each) are copied into
     // LDS_SCENE_F4 dwordx4 of LDS at the start of every workgroup; 0 = read from HBM
     uint32_t lds_quads;             // TLAS quads in LDS (every TLAS interior ref indexes below it)
@@ -249,7 +249,6 @@ struct OutputGPU {
     // persistent kernel: work queue split into `queue_parts` bands of units (one per XCD), each with
     // its own head counter QUEUE_STRIDE words apart; optional per-wave timeline (debug)
     uint32_t queue_parts;
-    uint32_t nt_store;              // 1: RGBA8 stores are non-temporal (keep the scene in L2)
     uint32_t grab;                  // pixels claimed per queue atomic
     uint32_t supertile;             // frame mode, grab 64: walk bands in supertile x supertile units (0 = rows)
     unsigned long long *timeline;   // TIMELINE_WORDS per wave (rt.h, rt_scene_debug_read)
@@ -259,8 +258,7 @@ struct OutputGPU {
     // largest cost (traversal rounds + 1) of unit u's pixels for the next launch's order
     const uint32_t *order;
     uint32_t *unit_cost;
-    uint32_t cost_max;              // 1: a unit's cost is 64 x its longest path (atomicMax), not the sum of its paths
-    uint32_t leaf_early;            // option "leaf_early": interior loop ends with <= this many lanes still descending
+    uint32_t leaf_early;            // setting "leaf_early": interior loop ends with <= this many lanes still descending
 };
 constexpr uint32_t QUEUE_STRIDE = 32;         // u32 words between partition heads (128 B lines)
 constexpr uint32_t QUEUE_MAX_PARTS = 8;

@@ -237,13 +237,10 @@ __global__ __launch_bounds__(BLOCK) void bounds_kernel(const uint32_t *seg_of, c
     }
 }
 
-// size_box (optional, the TLAS builder): a 2-bit size class above the 30-bit Morton code, so the tree's
-// first splits separate items as large as the whole centroid spread (C2's ground sphere) from mid-size
-// and small ones.  Plain Morton order drops such an item among its small neighbours and every ancestor
-// box up to the root inherits its extent, so rays descend into those subtrees for nothing (measured: a
-// GPU TLAS over C2's instances made the launch 28 % slower than the host SAH TLAS).
+// 30-bit Morton codes over each segment's centroid bounds.  (Round 3's 2-bit size class above the code for the TLAS,
+// option "tlas_classes", measured neutral and was removed in round 6.)
 __global__ void morton_kernel(const uint32_t *seg_of, const float4 *cent, uint32_t n, const uint32_t *bounds,
-                              const float *size_box, uint32_t *keys, uint32_t *vals) {
+                              uint32_t *keys, uint32_t *vals) {
     const uint32_t it = blockIdx.x * BLOCK + threadIdx.x;
     if (it >= n) return;
     const uint32_t seg = seg_of[it];
@@ -257,15 +254,7 @@ __global__ void morton_kernel(const uint32_t *seg_of, const float4 *cent, uint32
     const uint32_t x = quant10(c.x, o2f(B[0]), o2f(B[1]));
     const uint32_t y = quant10(c.y, o2f(B[2]), o2f(B[3]));
     const uint32_t z = quant10(c.z, o2f(B[4]), o2f(B[5]));
-    uint32_t m = (expand10(x) << 2) | (expand10(y) << 1) | expand10(z);
-    if (size_box) {
-        const float *b = size_box + 6 * (size_t)it;
-        const float ext = fmaxf(fmaxf(b[1] - b[0], b[3] - b[2]), b[5] - b[4]);
-        const float spread = fmaxf(fmaxf(o2f(B[1]) - o2f(B[0]), o2f(B[3]) - o2f(B[2])), o2f(B[5]) - o2f(B[4]));
-        const uint32_t cls = ext >= 0.5f * spread ? 0u : (ext >= 0.0625f * spread ? 1u : 2u);
-        m |= cls << 30;
-    }
-    keys[it] = m;
+    keys[it] = (expand10(x) << 2) | (expand10(y) << 1) | expand10(z);
     vals[it] = it;
 }
 
@@ -1214,14 +1203,13 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
         const uint32_t nb = (uint32_t)((N + (uint64_t)BLOCK * ipt - 1) / ((uint64_t)BLOCK * ipt));
         hipLaunchKernelGGL(bounds_kernel, dim3(nb), dim3(BLOCK), 0, stream, seg_of_, cent_, N, ipt, bounds_);
     }
-    hipLaunchKernelGGL(morton_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, seg_of_, cent_, N, bounds_,
-                       size_classes_ ? box_ : nullptr, k0_, v0_);
+    hipLaunchKernelGGL(morton_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, seg_of_, cent_, N, bounds_, k0_, v0_);
     LB_TRY(hipGetLastError());
     size_t bytes = tmp_bytes_;
     if (big_segs_.size() < n_segs_)
         hipLaunchKernelGGL(local_sort_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, k0_, k1_, v1_);
-    // BLAS codes are 30-bit Morton codes; TLAS items may carry size classes and inactive items (0xFFFFFFFF)
-    const int end_bit = (box_ == own_box_ && !size_classes_) ? 30 : 32;
+    // BLAS codes are 30-bit Morton codes; TLAS items may be inactive (0xFFFFFFFF)
+    const int end_bit = box_ == own_box_ ? 30 : 32;
     for (const auto &b : big_segs_) {
         bytes = tmp_bytes_;
         LB_TRY(rocprim::radix_sort_pairs(tmp_, bytes, k0_ + b.first, k1_ + b.first, v0_ + b.first, v1_ + b.first, b.second, 0,

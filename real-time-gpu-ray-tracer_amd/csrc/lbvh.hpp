@@ -127,9 +127,6 @@ private:
     size_t members_n_ = 0;
     uint32_t *item_member_ = nullptr;     // per item: its member instance + 1 (group segments), from members_
     float *box_ = nullptr;                // 6 floats per item (owned or caller's)
-public:
-    bool size_classes_ = false;           // TLAS: size class above the Morton code (morton_kernel)
-private:
     float4 *cent_ = nullptr;
     float *own_box_ = nullptr;
     float4 *own_cent_ = nullptr;

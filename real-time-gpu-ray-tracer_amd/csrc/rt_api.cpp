@@ -35,24 +35,24 @@ hipError_t launch_trace_rays_exact(const SceneGPU &, const float *, uint32_t, rt
 hipError_t launch_trace_rays_fast(const SceneGPU &, const float *, uint32_t, rt_hit *, hipStream_t);
 hipError_t launch_assemble(const void *, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, uint32_t, void *, hipStream_t);
 hipError_t launch_render_persistent_exact(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
-                                          uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
+                                          uint32_t *, uint32_t, uint32_t, bool, hipStream_t);
 hipError_t launch_render_persistent_fast(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
-                                         uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
+                                         uint32_t *, uint32_t, uint32_t, bool, hipStream_t);
 hipError_t launch_frame_copy(void *, const void *, size_t, unsigned long long *, uint32_t *, hipStream_t);
 hipError_t launch_schedule(uint32_t *, uint32_t *, uint32_t *, uint32_t *, uint32_t, uint32_t, uint32_t, bool, uint32_t,
                            uint32_t, uint32_t, void *, const void *, size_t, unsigned long long *, hipStream_t);
-uint32_t persistent_blocks_per_cu_exact(uint32_t variant, uint32_t wide, bool raw);
+uint32_t persistent_blocks_per_cu_exact(uint32_t wide, bool raw);
 hipError_t launch_instance_slot_order(const uint32_t *, const InstHot *, const InstCold *, uint32_t, InstHot *, InstCold *,
                                       hipStream_t);
 hipError_t launch_instance_update(const InstDelta *, uint32_t, InstParams *, uint32_t, InstHot *, InstCold *, float *, float4 *,
                                   const uint32_t *, const TreeRoot *, const uint32_t *, bool, hipStream_t);
-uint32_t persistent_blocks_per_cu_fast(uint32_t variant, uint32_t wide, bool raw);
+uint32_t persistent_blocks_per_cu_fast(uint32_t wide, bool raw);
 // option "fast_math": the FAST kernels compiled with hardware reciprocals and FMA contraction (trace_fastmath.o)
 hipError_t launch_render_fastmath(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *, hipStream_t);
 hipError_t launch_trace_rays_fastmath(const SceneGPU &, const float *, uint32_t, rt_hit *, hipStream_t);
 hipError_t launch_render_persistent_fastmath(const SceneGPU &, const CameraGPU &, const OutputGPU &, bool, unsigned long long *,
-                                             uint32_t *, uint32_t, uint32_t, uint32_t, bool, hipStream_t);
-uint32_t persistent_blocks_per_cu_fastmath(uint32_t variant, uint32_t wide, bool raw);
+                                             uint32_t *, uint32_t, uint32_t, bool, hipStream_t);
+uint32_t persistent_blocks_per_cu_fastmath(uint32_t wide, bool raw);
 hipError_t launch_box_test_exact(const float *, const float *, const float *, uint32_t, uint32_t, uint8_t *, float *, hipStream_t);
 hipError_t launch_box_test_fast(const float *, const float *, const float *, uint32_t, uint32_t, uint8_t *, float *, hipStream_t);
 }  // namespace rtamd
@@ -90,7 +90,7 @@ constexpr uint32_t BLAS_LEAF_CAP = 4;   // BLAS.cuh:17
 constexpr uint32_t TLAS_LEAF_CAP = 2;   // TLAS.cuh:22
 constexpr uint32_t SAH_LEAF_CAP = 4;    // RT_BUILD_SAH: <= 4 items per leaf (2-bit count in a leaf ref)
 constexpr uint32_t LBVH_BLAS_LEAF_CAP = 4;
-// GPU TLAS leaves hold up to option "tlas_leaf" instances (default 1, as the SAH TLAS: a leaf's
+// GPU TLAS leaves hold up to fixed setting "tlas_leaf" (an option until round 5) instances (default 1, as the SAH TLAS: a leaf's
 // instances are entered without their own box test; 2 = the reference's TLAS leaf size, TLAS.cuh:22)
 
 struct InstState {
@@ -169,7 +169,7 @@ struct rt_scene {
     std::vector<InstGroup> groups;  // option "group": TLAS item n + g is group g
     std::vector<uint32_t> group_of; // per instance: its group + 1 (0: none)
     bool group_inst = true;         // option "group" (set before the build)
-    bool lds_blas = true;           // option "lds_blas": with "lds_scene" 2, a group BLAS's top levels in LDS
+    bool lds_blas = true;           // fixed setting "lds_blas" (an option until round 5): with "lds_scene" 2, a group BLAS's top levels in LDS
     uint32_t frame_items[8] = {};   // per frame block: TLAS items (= instance records when staged by slot)
     Tree tlas;
     FlatTree tlas_flat;
@@ -204,7 +204,6 @@ struct rt_scene {
     int cold_records = -1;
     bool cold_eff = false;          // the build's choice (rt_scene_build)
     bool raw_shading() const { return build_mode == RT_BUILD_LBVH && !cold_eff; }
-    uint32_t wide_merge = 0;        // quad trees: binary subtrees of <= wide_merge items become one leaf (set before build)
     DevBuf<TriHot> tri_hot;
     DevBuf<TriCold> tri_cold;
     DevBuf<SphereHot> sph_hot;
@@ -271,14 +270,14 @@ struct rt_scene {
     // cycles L streams; with L <= 1 every frame uses lane 0 and launches of one scene are serialised.
     uint32_t *queue[NLANE] = {};
     bool overlap = false;
-    uint32_t blas_leaf = SAH_LEAF_CAP;   // option "blas_leaf": RT_BUILD_SAH BLAS leaf size (1..4), next rt_scene_build
-    uint32_t tlas_leaf = 1;   // option "tlas_leaf": RT_BUILD_SAH per-frame SAH TLAS leaf size (1..4; 1 measured best)
-    uint32_t tlas_median_leaf = 0;   // option "tlas_median_leaf": RT_BUILD_SAH median TLAS leaf size (0 = the reference's 2)
+    uint32_t blas_leaf = SAH_LEAF_CAP;   // fixed setting "blas_leaf" (an option until round 5): RT_BUILD_SAH BLAS leaf size (1..4), next rt_scene_build
+    uint32_t tlas_leaf = 1;   // fixed setting "tlas_leaf" (an option until round 5): RT_BUILD_SAH per-frame SAH TLAS leaf size (1..4; 1 measured best)
+    uint32_t tlas_median_leaf = 0;   // fixed setting "tlas_median_leaf" (an option until round 5): RT_BUILD_SAH median TLAS leaf size (0 = the reference's 2)
     bool tlas_sah = true;     // option "tlas_sah": RT_BUILD_SAH builds its per-frame TLAS with SAH (0: the median split)
-    bool inst_by_slot = true;       // option "inst_by_slot": host-built TLAS stages instance records in slot order
+    bool inst_by_slot = true;       // fixed setting "inst_by_slot" (an option until round 5): host-built TLAS stages instance records in slot order
     bool block_by_slot[NLANE] = {};  // per frame block: staged in slot order
     uint32_t lanes = 1;
-    // option "reserve": with overlapped lanes the persistent grid leaves this many workgroup slots free (two
+    // fixed setting "reserve" (an option until round 5): with overlapped lanes the persistent grid leaves this many workgroup slots free (two
     // per XCD at 16), so the next lanes' schedule / upload kernels and GPU TLAS builds run beside a launch
     // that holds the rest of the GPU instead of waiting for its drain (C2, 3 lanes: 16 -> 0.260-0.261,
     // 8 -> 0.261-0.265, 0 -> 0.268-0.272 ms/frame; profiles/r02_sweep_lanes.jsonl)
@@ -290,7 +289,7 @@ struct rt_scene {
     // (auto_lanes: the settings bench.py measured best), so a drop-in caller passes no streams at all
     hipStream_t lane_st[NLANE] = {};
     bool overlap_auto = false;
-    // option "leaf_early" (OutputGPU::leaf_early): -1 = auto, 0 for paths of <= 2 segments (depth x samples; C2, C4),
+    // fixed setting "leaf_early" (an option until round 5) (OutputGPU::leaf_early): -1 = auto, 0 for paths of <= 2 segments (depth x samples; C2, C4),
     // else LEAF_EARLY_AUTO (C3 1.54 -> 1.25, C5 5.79 -> 4.97 ms/frame; C2 0.181 -> 0.185 with it,
     // profiles/r05/leaf_early/)
     int leaf_early = -1;
@@ -299,16 +298,14 @@ struct rt_scene {
     // hardware queues of their own, so 4 lanes run side by side at the default GPU_MAX_HW_QUEUES (4) — C2 0.256 ->
     // 0.180 ms/frame, C3 2.15 -> 1.54, a 1/8 share 0.064 -> 0.046 — as at 12 queues (profiles/r05/lanes/)
     bool lane_priority = true;
-    bool scene_priority = false;    // option "scene_priority" (set before rt_scene_build): the scene stream at the highest
     bool stage_depth_set = false;   // option "stage_depth" given explicitly (auto lanes leave it alone)
     hipEvent_t ev_lane_done[NLANE] = {};   // last trace launch of each lane finished
     uint32_t cus = 0;
-    // option "threshold" (lanes waiting before a wave leaves traversal to shade and refill); 0 = auto: 64 when
+    // fixed setting "threshold" (an option until round 5) (lanes waiting before a wave leaves traversal to shade and refill); 0 = auto: 64 when
     // a pixel's path has at most two segments (depth x samples <= 2: the wave then shades and refills all its
     // lanes at once), else 40 (C2 0.194 -> 0.184 ms/frame, serialised 0.35 -> 0.33 ms; C3 at 64 would lose
     // 23 %, 40 ties 32; profiles/r02_sweep_thr2.jsonl)
     uint32_t threshold = 0;
-    uint32_t variant = 0;           // register-budget variant of the persistent kernel (0, 4)
     // option "fast_math": FAST frames with hardware reciprocal / rsq and FMA contraction instead of the reference's
     // correctly rounded arithmetic (C2 -7 %, C3 -9 % per pipelined frame; 0.008-0.09 % of pixels then differ from the
     // oracle even on its own trees); default 0: bit-identical to the oracle on the reference's trees
@@ -316,10 +313,8 @@ struct rt_scene {
     double update_wait_ms = 0.0;    // last frame_update: time blocked on ev_copied (GPU progress)
     bool use_persistent = true;
     uint32_t queue_parts = 8;       // one band per XCD (measured with "reorder": 8 beat 4, 2 and 1 on C2)
-    uint32_t nt_store = 0;
     uint32_t grab = 64;             // pixels per queue claim
-    uint32_t cost_max = 0;
-    // option "merge": two adjacent units below this cost level share one claim item (128 pixels): 6 (sky, about
+    // fixed setting "merge" (an option until round 5): two adjacent units below this cost level share one claim item (128 pixels): 6 (sky, about
     // 4 steps per pixel) measured C2 0.203 -> 0.199 ms/frame; 8 or 10 (also the ground) put 128-pixel items at
     // the end of the order and lengthen the tail (profiles/r02_sweep_merge.jsonl)
     uint32_t merge = 6;
@@ -334,7 +329,7 @@ struct rt_scene {
     uint32_t split = 12u | 12u << 8;
     DevBuf<uint32_t> unit_cost[NLANE], unit_order[NLANE];
     uint32_t sched_sig[NLANE][7] = {};  // launch layout the recorded costs belong to
-    // option "reorder_period" K: a lane records unit costs on one launch in K and rebuilds its order on
+    // fixed setting "reorder_period" (an option until round 5) K: a lane records unit costs on one launch in K and rebuilds its order on
     // the next; the launches between reuse the order (the heaviest regions move little between frames)
     uint32_t reorder_period = 8;        // measured: 8 (C2 0.242 ms/step) beats 1 (0.265) with 3 lanes
     uint32_t sched_phase[NLANE] = {};
@@ -407,7 +402,6 @@ struct rt_scene {
     bool blas_double = true;
     uint64_t blas_builds = 0;
     hipEvent_t ev_render_done = nullptr;   // last trace launch finished (BLAS rebuilds wait on it)
-    bool tlas_size_classes = false;     // option "tlas_classes": GPU TLAS keys start with an item size class (measured neutral)
     bool gpu_tlas_sah = false;          // option "gpu_tlas" (set before the build): RT_BUILD_SAH BLASes, per-frame TLAS on the GPU
     // option "tlas_small": GPU-built frames with at most SMALL_TLAS_MAX records in the TLAS build it in one workgroup
     // (lbvh.hip tlas_small_kernel) instead of the ~17-launch chain
@@ -798,7 +792,7 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
                                       s->build_mode == RT_BUILD_SAH && s->tlas_median_leaf ? s->tlas_median_leaf : TLAS_LEAF_CAP,
                                       hm::tlas_axis_state(s->build_seed, frame));
     s->tlas_flat = flatten_tree(s->tlas, 0, 0, 0, false);
-    s->tlas_wide = flatten_tree_wide(s->tlas, 0, 0, 0, false, s->quad_halves(), s->wide_merge);
+    s->tlas_wide = flatten_tree_wide(s->tlas, 0, 0, 0, false, s->quad_halves());
 
     TreeRoot root{};
     std::memcpy(root.box, s->tlas_flat.root_box, sizeof root.box);
@@ -872,7 +866,7 @@ SceneGPU scene_gpu(const rt_scene *s) {
     g.instance_count = s->frame_items[b];   // records the frame's TLAS holds (GPU-built, small path: the live ones)
     g.rough_count = (uint32_t)s->roughs.size();
     g.material_count = (uint32_t)(s->materials.n / 4);
-    // option "lds_scene": the quads the frame's TLAS refs can index (host-built: this frame's quad count;
+    // fixed setting "lds_scene" (an option until round 5): the quads the frame's TLAS refs can index (host-built: this frame's quad count;
     // GPU-built: quad q is rooted at pair q, < n - 1) and, if they fit too, the instance hot records
     // then, in this order while they fit: sphere and parallelogram records (hot + cold), instance cold records
     g.lds_icold = g.lds_sph_hot = g.lds_sph_cold = g.lds_q_hot = g.lds_q_cold = LDS_NONE;
@@ -1262,7 +1256,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             if ((uint64_t)slot_base[in.ptype] + in.pcount >= MAX_LEAF_SLOTS)
                 return fail(RT_ERR_UNSUPPORTED, "too many primitives of one type (2^26 leaf slots)");
             bh.flat = flatten_tree(bh.tree, pair_base, bh.slot_base, in.ptype, true);
-            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, in.ptype, true, s->quad_halves(), s->wide_merge);
+            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, in.ptype, true, s->quad_halves());
             quad_base += (uint32_t)bh.wide.quads.size();
             s->max_blas_height = std::max(s->max_blas_height, bh.flat.height);
             pair_base += (uint32_t)bh.flat.pairs.size();
@@ -1346,7 +1340,7 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
             bh.pair_base = pair_base;
             bh.slot_base = slot_base[RT_PRIM_TRIANGLE];
             bh.flat = flatten_tree(bh.tree, pair_base, bh.slot_base, RT_PRIM_TRIANGLE, true);
-            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, RT_PRIM_TRIANGLE, true, s->quad_halves(), s->wide_merge,
+            bh.wide = flatten_tree_wide(bh.tree, quad_base, bh.slot_base, RT_PRIM_TRIANGLE, true, s->quad_halves(),
                                         /*level_order=*/true);
             quad_base += (uint32_t)bh.wide.quads.size();
             s->max_blas_height = std::max(s->max_blas_height, bh.flat.height);
@@ -1364,9 +1358,8 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
     for (const auto &m : s->metals) { mats.push_back(m.albedo.x); mats.push_back(m.albedo.y); mats.push_back(m.albedo.z); mats.push_back(m.fuzz); }
     rt_status st;
     if (!s->stream) {
-        int lo = 0, hi = 0;                        // option "scene_priority": the scene stream (uploads, GPU BLAS builds)
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIP_TRY(hipStreamCreateWithPriority(&s->stream, hipStreamNonBlocking, s->scene_priority ? hi : 0));
+        // the scene stream (uploads, GPU BLAS builds) at normal priority: the highest measured neutral (round 3)
+        HIP_TRY(hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking));
     }
     if (!s->ev_render_done) HIP_TRY(hipEventCreateWithFlags(&s->ev_render_done, hipEventDisableTiming));
     if (!s->r_done) s->r_done = s->ev_render_done;
@@ -1479,7 +1472,6 @@ rt_status rt_scene_build(rt_scene *s, rt_build_mode mode, uint64_t seed) {
         s->tlas_builder = new LbvhBuilder();
         const std::vector<LbvhSeg> tseg{LbvhSeg{0u, (uint32_t)n, 0u, 0u, 0u, 0u, s->tlas_leaf, 0u}};
         HIP_TRY(s->tlas_builder->init(tseg, s->stream));
-        s->tlas_builder->size_classes_ = s->tlas_size_classes;
     }
     for (int i = 0; i < rt_scene::NSTAGE; i++) {
         if (s->staging[i]) { (void)hipHostFree(s->staging[i]); s->staging[i] = nullptr; }   // frame_update allocates
@@ -1727,7 +1719,6 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     // consecutive frames concurrently on two streams.
     const int q = s->overlap ? (int)s->lane : 0;
     OutputGPU out{};
-    out.nt_store = s->nt_store;
     out.leaf_early = s->leaf_early >= 0 ? (uint32_t)s->leaf_early
                                         : (s->cam.depth * s->cam.sqrt_s * s->cam.sqrt_s <= 2u ? 0u : rt_scene::LEAF_EARLY_AUTO);
     const uint32_t W = s->width, H = s->height;
@@ -1814,9 +1805,9 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         out.grab = s->grab;
         out.supertile = s->supertile;
         if (s->timeline_on) {
-            const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, 0u, false)
-                                                    : (s->fast_math ? persistent_blocks_per_cu_fastmath(s->variant, g.wide, g.raw_tris != nullptr)
-                                                                   : persistent_blocks_per_cu_fast(s->variant, g.wide, g.raw_tris != nullptr)));
+            const uint32_t blocks = s->cus * (exact ? persistent_blocks_per_cu_exact(0u, false)
+                                                    : (s->fast_math ? persistent_blocks_per_cu_fastmath(g.wide, g.raw_tris != nullptr)
+                                                                   : persistent_blocks_per_cu_fast(g.wide, g.raw_tris != nullptr)));
             const size_t words = (size_t)blocks * 4 * TIMELINE_WORDS;
             if (s->timeline.n < words) {
                 s->timeline.release();
@@ -1915,7 +1906,6 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         s->sched_valid[q] = true;
         out.order = s->order_ok[q] ? unit_order.p : nullptr;
         out.unit_cost = track ? unit_cost.p : nullptr;
-        out.cost_max = s->cost_max;
     }
     if (s->pending_copy >= 0) {                // the frame block's upload (and the lane's counter / queue reset)
         HIP_TRY(launch_frame_copy(s->frame_dev[s->pending_copy], s->staging_dev[s->pending_stage], s->frame_block,
@@ -1943,9 +1933,9 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
     s->last_stream = stream;
     HIP_TRY(hipEventRecord(s->ring_start[slot], stream));
     if (s->use_persistent) {
-        const uint32_t cap = s->cus * (exact ? persistent_blocks_per_cu_exact(s->variant, 0u, false)
-                                             : (s->fast_math ? persistent_blocks_per_cu_fastmath(s->variant, g.wide, g.raw_tris != nullptr)
-                                                            : persistent_blocks_per_cu_fast(s->variant, g.wide, g.raw_tris != nullptr)));
+        const uint32_t cap = s->cus * (exact ? persistent_blocks_per_cu_exact(0u, false)
+                                             : (s->fast_math ? persistent_blocks_per_cu_fastmath(g.wide, g.raw_tris != nullptr)
+                                                            : persistent_blocks_per_cu_fast(g.wide, g.raw_tris != nullptr)));
         uint32_t blocks = s->overlap && cap > 2 * s->reserve ? cap - s->reserve : cap;
         uint32_t pct = s->grid_pct;
         if (pct == 0) {
@@ -1965,11 +1955,11 @@ rt_status rt_render(rt_scene *s, uint64_t frame, const rt_render_opts *opts, uin
         if (pct < 100) blocks = std::max<uint32_t>(8u, blocks * pct / 100u);
         const uint32_t thr = s->threshold ? s->threshold : (cam.depth * cam.sqrt_s * cam.sqrt_s <= 2u ? 64u : 40u);
         HIP_TRY(exact ? launch_render_persistent_exact(g, cam, out, count, lane_counters, s->queue[q], blocks, thr,
-                                                       s->variant, reset_queue, stream)
+                                                       reset_queue, stream)
                       : (s->fast_math ? launch_render_persistent_fastmath(g, cam, out, count, lane_counters, s->queue[q], blocks,
-                                                                          thr, s->variant, reset_queue, stream)
+                                                                          thr, reset_queue, stream)
                                       : launch_render_persistent_fast(g, cam, out, count, lane_counters, s->queue[q], blocks, thr,
-                                                                      s->variant, reset_queue, stream)));
+                                                                      reset_queue, stream)));
     }
     else
         HIP_TRY(exact ? launch_render_exact(g, cam, out, count, lane_counters, stream)
@@ -2125,24 +2115,24 @@ rt_status rt_box_test(int device, const float *boxes, const float *rays, const f
     return RT_OK;
 }
 
+// The caller-facing options (include/rt.h, 19 keys).  Round 6 removed the tuning switches whose only use was an A/B
+// study (their measured defaults are fixed now: refill threshold, leaf_early, queue bands, claim size, supertile walk,
+// merge / split claim items, reorder period, reserved slots, LDS scene levels, instance-record order, leaf sizes) and
+// the measured-negative or neutral ones with their code (variant, nt_store, cost_max, tlas_classes, wide_merge,
+// scene_priority): DESIGN.md §4 keeps their measurements.
 rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
     if (!s || !key) return fail(RT_ERR_INVALID_ARGUMENT, "null argument");
     const std::string k(key);
+    const auto boolean = [&](const char *name) -> rt_status {
+        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, std::string(name) + " must be 0 or 1");
+        return RT_OK;
+    };
     if (k == "kernel") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "kernel must be 0 or 1");
+        RT_TRY(boolean("kernel"));
         s->use_persistent = value == 1;
-    } else if (k == "threshold") {
-        if (value < 0 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "threshold must be in 0..64 (0 = auto)");
-        s->threshold = (uint32_t)value;
-    } else if (k == "variant") {
-        if (value != 0 && value != 4) return fail(RT_ERR_INVALID_ARGUMENT, "variant must be 0 or 4");
-        s->variant = (uint32_t)value;
     } else if (k == "fast_math") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "fast_math must be 0 or 1");
+        RT_TRY(boolean("fast_math"));
         s->fast_math = value == 1;
-    } else if (k == "queue_parts") {
-        if (value < 1 || value > (int64_t)QUEUE_MAX_PARTS) return fail(RT_ERR_INVALID_ARGUMENT, "queue_parts must be in 1..8");
-        s->queue_parts = (uint32_t)value;
     } else if (k == "stage_depth") {
         // pinned staging buffers the host cycles through: it stages frame k once frame k - depth's trace is done
         if (value < 2 || value > rt_scene::NSTAGE) return fail(RT_ERR_INVALID_ARGUMENT, "stage_depth must be in 2..64");
@@ -2150,25 +2140,16 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         s->stage_depth = (int)value;
         s->stage_next = 0;
         s->stage_depth_set = true;
-    } else if (k == "nt_store") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "nt_store must be 0 or 1");
-        s->nt_store = (uint32_t)value;
-    } else if (k == "grab") {
-        if (value < 8 || value > 4096 || (value % 8)) return fail(RT_ERR_INVALID_ARGUMENT, "grab must be a multiple of 8 in 8..4096");
-        s->grab = (uint32_t)value;
-    } else if (k == "supertile") {
-        if (value < 0 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "supertile must be in 0..64");
-        s->supertile = (uint32_t)value;
     } else if (k == "rebuild") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "rebuild must be 0 or 1");
+        RT_TRY(boolean("rebuild"));
         if (value == 1 && s->built && s->build_mode != RT_BUILD_LBVH)
             return fail(RT_ERR_UNSUPPORTED, "per-frame BLAS rebuild needs RT_BUILD_LBVH");
         s->rebuild_blas = value == 1;
     } else if (k == "timeline") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "timeline must be 0 or 1");
+        RT_TRY(boolean("timeline"));
         s->timeline_on = value == 1;
     } else if (k == "costmap") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "costmap must be 0 or 1");
+        RT_TRY(boolean("costmap"));
         s->costmap_on = value == 1;
     } else if (k == "cold_records") {
         if (value < -1 || value > 1) return fail(RT_ERR_INVALID_ARGUMENT, "cold_records must be -1, 0 or 1");
@@ -2179,61 +2160,29 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         RT_TRY(drain(s));
         s->blas_sets = (uint32_t)value;
     } else if (k == "blas_double") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "blas_double must be 0 or 1");
+        RT_TRY(boolean("blas_double"));
         s->blas_double = value == 1;
-    } else if (k == "merge") {
-        if (value < 0 || value > 16) return fail(RT_ERR_INVALID_ARGUMENT, "merge must be in 0..16");
-        s->merge = (uint32_t)value;
-    } else if (k == "cost_max") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "cost_max must be 0 or 1");
-        s->cost_max = (uint32_t)value;
     } else if (k == "grid_pct") {
         if (value < 0 || value > 100) return fail(RT_ERR_INVALID_ARGUMENT, "grid_pct must be in 0..100 (0 = auto)");
         s->grid_pct = (uint32_t)value;
-    } else if (k == "lds_scene") {
-        if (value < 0 || value > 2) return fail(RT_ERR_INVALID_ARGUMENT, "lds_scene must be 0, 1 or 2");
-        s->lds_scene = (uint32_t)value;
     } else if (k == "wide") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "wide must be 0 or 1");
+        RT_TRY(boolean("wide"));
         s->wide = value == 1;
     } else if (k == "exact_decisions") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "exact_decisions must be 0 or 1");
+        RT_TRY(boolean("exact_decisions"));
         s->exact_decisions = value == 1;
-    } else if (k == "tlas_classes") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_classes must be 0 or 1");
-        s->tlas_size_classes = value == 1;
-        if (s->tlas_builder) s->tlas_builder->size_classes_ = s->tlas_size_classes;
     } else if (k == "tlas_small") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_small must be 0 or 1");
+        RT_TRY(boolean("tlas_small"));
         s->tlas_small = value == 1;
     } else if (k == "gpu_tlas") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "gpu_tlas must be 0 or 1");
+        RT_TRY(boolean("gpu_tlas"));
         if (s->built) return fail(RT_ERR_UNSUPPORTED, "gpu_tlas is set before rt_scene_build");
         s->gpu_tlas_sah = value == 1;
-    } else if (k == "wide_merge") {
-        if (value != 0 && (value < 2 || value > 4)) return fail(RT_ERR_INVALID_ARGUMENT, "wide_merge must be 0 or 2..4");
-        s->wide_merge = (uint32_t)value;          // BLAS quads: next rt_scene_build; TLAS: next frame
-    } else if (k == "split") {
-        if (value < 0 || value > 0xFFFF) return fail(RT_ERR_INVALID_ARGUMENT, "split must be k_half | k_quarter << 8");
-        s->split = (uint32_t)value;
-    } else if (k == "lds_blas") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "lds_blas must be 0 or 1");
-        s->lds_blas = value == 1;
     } else if (k == "group") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "group must be 0 or 1");
+        RT_TRY(boolean("group"));
         s->group_inst = value == 1;                   // next rt_scene_build
-    } else if (k == "blas_leaf") {
-        if (value < 1 || value > (int64_t)SAH_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "blas_leaf must be in 1..4");
-        s->blas_leaf = (uint32_t)value;
-    } else if (k == "leaf_early") {
-        if (value < -1 || value > 64) return fail(RT_ERR_INVALID_ARGUMENT, "leaf_early must be -1 (auto) or 0..64");
-        s->leaf_early = (int)value;
-    } else if (k == "scene_priority") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "scene_priority must be 0 or 1");
-        if (s->stream) return fail(RT_ERR_STATE, "scene_priority is set before rt_scene_build");
-        s->scene_priority = value == 1;
     } else if (k == "lane_priority") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "lane_priority must be 0 or 1");
+        RT_TRY(boolean("lane_priority"));
         RT_TRY(drain(s));
         for (hipStream_t &l : s->lane_st) {
             if (!l) continue;
@@ -2246,19 +2195,9 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
             l = nullptr;                                                // recreated at the next frame
         }
         s->lane_priority = value == 1;
-    } else if (k == "tlas_median_leaf") {
-        if (value < 0 || value > (int64_t)TLAS_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_median_leaf must be 0..2");
-        s->tlas_median_leaf = (uint32_t)value;
     } else if (k == "tlas_sah") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_sah must be 0 or 1");
+        RT_TRY(boolean("tlas_sah"));
         s->tlas_sah = value == 1;                 // next frame's TLAS
-    } else if (k == "tlas_leaf") {
-        if (value < 1 || value > (int64_t)SAH_LEAF_CAP) return fail(RT_ERR_INVALID_ARGUMENT, "tlas_leaf must be in 1..4");
-        s->tlas_leaf = (uint32_t)value;          // next frame's TLAS
-    } else if (k == "inst_by_slot") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "inst_by_slot must be 0 or 1");
-        RT_TRY(drain(s));
-        s->inst_by_slot = value == 1;            // takes effect with the next frame's staging
     } else if (k == "overlap") {
         if (value < -1 || value > rt_scene::NLANE) return fail(RT_ERR_INVALID_ARGUMENT, "overlap must be -1 (auto) or 0..8 lanes");
         RT_TRY(drain(s));
@@ -2266,15 +2205,8 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         s->lanes = value < 1 ? (value == -1 ? 4u : 1u) : (uint32_t)value;      // auto: resolved per frame (auto_lanes)
         s->overlap = s->lanes > 1;
         s->lane = 0;
-    } else if (k == "reserve") {
-        if (value < 0 || value > 256) return fail(RT_ERR_INVALID_ARGUMENT, "reserve must be in 0..256");
-        s->reserve = (uint32_t)value;
-    } else if (k == "reorder_period") {
-        if (value < 1 || value > 1024) return fail(RT_ERR_INVALID_ARGUMENT, "reorder_period must be in 1..1024");
-        s->reorder_period = (uint32_t)value;
-        for (uint32_t &p : s->sched_phase) p = 0;
     } else if (k == "reorder") {
-        if (value != 0 && value != 1) return fail(RT_ERR_INVALID_ARGUMENT, "reorder must be 0 or 1");
+        RT_TRY(boolean("reorder"));
         if (s->reorder != (value == 1)) for (bool &v : s->sched_valid) v = false;
         s->reorder = value == 1;
     } else {

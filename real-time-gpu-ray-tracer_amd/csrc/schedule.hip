@@ -21,7 +21,7 @@
 // frame's TLAS / instance block from pinned staging and clears the lane's work counters.
 //
 // Footprint (measured, profiles/r02_*): with overlapped lanes this kernel runs while the other lane's
-// persistent grid holds the GPU, in the workgroup slots the grid leaves free (option "reserve": one per
+// persistent grid holds the GPU, in the workgroup slots the grid leaves free (setting "reserve": one per
 // XCD).  Round 1's version (one 1024-thread workgroup, 64 KB of LDS per band) could only start once the
 // other launch drained and averaged 172 us per frame; a 256-thread version with 49 KB of LDS still
 // waited (84 us: a drained render workgroup leaves 32 KB holes of LDS); building the order in the render
@@ -125,12 +125,12 @@ __global__ __launch_bounds__(SCHED_THREADS) void schedule_kernel(uint32_t *__res
         if (t == 0) queue[(QUEUE_MAX_PARTS + part) * QUEUE_STRIDE] = n;
         return;
     }
-    // even per-thread ranges: a merged pair of light units (option "merge") never spans two threads
+    // even per-thread ranges: a merged pair of light units (setting "merge") never spans two threads
     const uint32_t per = ((n + SCHED_THREADS - 1) / SCHED_THREADS + 1) & ~1u;
     const uint32_t lo = b0 + min(n, t * per), hi = b0 + min(n, (t + 1) * per);
     const auto cls = [&](uint32_t u) { return (uint32_t)(nib[(u - gbase) >> 1] >> (4 * ((u - gbase) & 1u))) & 15u; };
     for (uint32_t c = 0; c < SCHED_CLASSES; c++) cnt[c * SCHED_THREADS + t] = 0;
-    // option "merge": two adjacent light units (levels below km, pair offset even) become one 128-pixel item
+    // setting "merge": two adjacent light units (levels below km, pair offset even) become one 128-pixel item
     // in the pair's heavier class, so a claim over the sky / ground serves twice the pixels
     const auto light = [&](uint32_t c) { return (SCHED_CLASSES - 1u) - c < km; };
     for (uint32_t u = lo; u < hi; u++) {

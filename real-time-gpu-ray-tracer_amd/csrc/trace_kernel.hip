@@ -75,11 +75,11 @@ static_assert(LDS_DEPTH % 4 == 0, "half-pages move as 16 B pieces");
                                         // reciprocal-FMA planes is widened by a bound on its distance from the
                                         // reference's (mn - q) / d interval before the lo < hi test (and a popped entry's
                                         // lo before its lo < tmax re-test), so a FAST cull never rejects a box the
-                                        // reference's slab accepts.  A parallel axis (|d| < 1e-6) whose origin lies exactly
-                                        // on a face of the slab is the one case planes cannot widen (the reference keeps
+                                        // reference's slab accepts — but for a parallel axis (|d| < 1e-6) whose origin lies
+                                        // exactly on a face of the slab, which planes cannot widen (the reference keeps
                                         // q == min / max, BoundingBox.cu:47; the FAST planes there are the rounding residual
-                                        // of o / d), so every box test of a ray with a parallel axis is re-taken with the
-                                        // reference's slab (XD_PAR and up, XBOX; round 6: the host SAH trees' instances too).
+                                        // of o / d): the exact-decision instances (XD_ALL, XBOX) re-take every box test of a
+                                        // ray with a parallel axis with the reference's slab; the others keep the exception.
                                         // Entries keep the unwidened lo, so children are still ordered by it
 #endif
 #ifndef RT_BOX_EXACT
@@ -92,26 +92,19 @@ static_assert(LDS_DEPTH % 4 == 0, "half-pages move as 16 B pieces");
 // trees), 2 two-level quads in pair order (GPU-built trees), 3 the same with exact decisions (the reference's trees, and
 // GPU-built trees with option "exact_decisions").
 // Exact-decision level of a traversal instance (template argument XB):
-//   XD_CULL: conservative culls only;
-//   XD_PAR : also every box test of a ray with a parallel axis (|d| < 1e-6) re-taken with the reference's slab — the
-//            reciprocal planes cannot represent a parallel axis whose origin lies exactly on a face of the slab (the
-//            reference keeps q == min / max, BoundingBox.cu:47), so without it such a box could be culled.  Host SAH
-//            trees (mode 1) run at XD_CULL (RT_XPAR_SAH 0): that case is their one documented exception to "a FAST cull
-//            never rejects a box the reference keeps" (tests/test_gpu_box.py pins it to exactly that case);
-//   XD_ALL : also every decision inside the slabs' error margin, and (pair order) every comparison of two entry t's
-//            inside it: the traversal takes the reference's decisions.  The binary pairs and mode 3 — FAST then equals EXACT
-//            on the same trees (tests/test_gpu_parity_full.py: the reference's trees, and C5's benched LBVH trees).
-#ifndef RT_XBOX_GPU
-#define RT_XBOX_GPU 0                   // mode 2 at XD_ALL: C5 8.8 -> 11.9 ms, C2-LBVH 0.38 -> 0.49 ms serialised (ties
-                                        // between sibling boxes' entries are common, profiles/r06/exact_decisions/): GPU-built
-                                        // trees take exact decisions as mode 3, with option "exact_decisions"
-#endif
-#ifndef RT_XPAR_SAH
-#define RT_XPAR_SAH 0                   // host SAH trees at XD_PAR: C2 +4.4 %, C3 +2.5 % per frame (profiles/r06/exact_decisions/)
-#endif
-constexpr int XD_CULL = 0, XD_PAR = 1, XD_ALL = 2;
-#define XBOX(W) (!RT_BOX_EXACT ? XD_CULL : (((W) == 0 || (W) == 3 || (RT_XBOX_GPU && (W) == 2)) ? XD_ALL \
-                                           : (RT_XPAR_SAH ? XD_PAR : XD_CULL)))
+//   XD_CULL: conservative culls only (modes 1 and 2).  One documented exception to "a FAST cull never rejects a box the
+//            reference keeps": a ray with a parallel axis (|d| < 1e-6) whose origin lies exactly on a face of that
+//            axis's slab (the reference keeps q == min / max, BoundingBox.cu:47; reciprocal planes cannot represent it;
+//            tests/test_gpu_box.py pins the misses to exactly that case).  Re-taking such rays' decisions in modes 1 / 2
+//            (round 6) cost C2 4.4 % and C3 2.5 % per frame through register pressure alone;
+//   XD_ALL : every decision inside the slabs' error margin, every box test of a ray with a parallel axis and (pair
+//            order) every comparison of two entry t's inside the margin re-taken with the reference's slab: the traversal
+//            takes the reference's decisions.  The binary pairs and mode 3 — FAST then equals EXACT on the same trees
+//            (tests/test_gpu_parity_full.py: the reference's trees, and C5's benched LBVH trees with "exact_decisions").
+//            For mode 2 by default it cost C5 +34 % per frame (sibling boxes' entry t's often tie exactly:
+//            profiles/r06/exact_decisions/).
+constexpr int XD_CULL = 0, XD_ALL = 2;
+#define XBOX(W) ((RT_BOX_EXACT && ((W) == 0 || (W) == 3)) ? XD_ALL : XD_CULL)
 #ifndef RT_NZ_MIN
 #define RT_NZ_MIN FZERO                 // |d_axis| below this is clamped to +-1e-20 for the slab reciprocals (prep)
 #endif
@@ -820,20 +813,12 @@ __device__ __forceinline__ void quad_decide(const float4 *Q, const float4 &lx, c
         // again (keeping the 24 bounds live through the step would cost registers on the hot path), one box per
         // iteration so that one copy of the division slab serves all six.  Boxes of the mask m: bit k = slot k, bits 4 / 5
         // = the halves.  Re-taking only the two entries a close comparison involves (round 6) instead of all six boxes
-        // took C5 from ... ms per serialised launch.
-#ifndef RT_XD_DIAG
-#define RT_XD_DIAG 0
-#endif
-        const auto close = [&](float a, float b) {
-            return fabsf(a - b) <= box_margin(a, b, r.pad) && !((RT_XD_DIAG & 8) && a == b);
-        };
-#ifndef RT_XD_DIAG
-#define RT_XD_DIAG 0                    // diagnostic builds only: 1 no pair-order trigger, 2 no margin trigger, 4 no parallel
-#endif
-        uint32_t m = (!(RT_XD_DIAG & 4) && ray_parallel(r)) ? (PAIR ? 0x3Fu : 0xFu) : 0u;
-        if (XB == XD_ALL && !(RT_XD_DIAG & 2))
+        // took C5 with exact decisions from 13.6 to 11.9 ms per serialised launch.
+        const auto close = [&](float a, float b) { return fabsf(a - b) <= box_margin(a, b, r.pad); };
+        uint32_t m = ray_parallel(r) ? (PAIR ? 0x3Fu : 0xFu) : 0u;
+        if (XB == XD_ALL)
             m |= (h[0] && und[0] ? 1u : 0u) | (h[1] && und[1] ? 2u : 0u) | (h[2] && und[2] ? 4u : 0u) | (h[3] && und[3] ? 8u : 0u);
-        if (PAIR && XB == XD_ALL && !(RT_XD_DIAG & 1))
+        if (PAIR && XB == XD_ALL)
             m |= (h[0] && h[1] && !(low[0] && low[1]) && close(t[0], t[1]) ? 0x3u : 0u) |
                  (h[2] && h[3] && !(low[2] && low[3]) && close(t[2], t[3]) ? 0xCu : 0u) |
                  ((h[0] || h[1]) && (h[2] || h[3]) && !(low_a && low_b) && close(pa, pb) ? 0x30u : 0u);
@@ -1145,7 +1130,7 @@ __device__ __forceinline__ unsigned long long stamp() {
 
 // One round: interior loop until every traversing lane holds a leaf, then the leaf phase.
 // steps (when `track`): the lane's interior steps + leaf phases, the pixel's cost for the work order
-// leaf_early (option "leaf_early"): the interior loop also ends once no more than this many lanes are still looking
+// leaf_early (setting "leaf_early"): the interior loop also ends once no more than this many lanes are still looking
 // for a leaf while some hold one; the lanes without a leaf skip the leaf phase and go on descending next round
 template <bool COUNT, int WIDE = 0>
 __device__ __forceinline__ void spec_round(Trav &T, const SceneGPU &sc, SEnt *spill, LaneCount &cnt,
@@ -1468,8 +1453,7 @@ __device__ __forceinline__ void write_pixel(const OutputGPU &out, uint32_t oi, f
     const float cb = fminf(fmaxf(sqrtf(result.z), 0.0f), 0.999f);
     const uint32_t packed = (uint32_t)(uint8_t)(256.0f * cr) | ((uint32_t)(uint8_t)(256.0f * cg) << 8) |
                             ((uint32_t)(uint8_t)(256.0f * cb) << 16) | (255u << 24);
-    if (out.nt_store) __builtin_nontemporal_store(packed, reinterpret_cast<uint32_t *>(out.rgba) + oi);
-    else reinterpret_cast<uint32_t *>(out.rgba)[oi] = packed;
+    reinterpret_cast<uint32_t *>(out.rgba)[oi] = packed;
 }
 
 // Option "reorder": a unit's cost for the next launch's claim order (schedule.hip) is the traversal
@@ -1483,26 +1467,17 @@ __device__ __forceinline__ void write_pixel(const OutputGPU &out, uint32_t oi, f
 // atomics issued before it).  A lane that finishes a pixel of another unit before that flushes its old
 // sum at once.  Measured: per-shade-step atomics made each next node load wait for their memory-side
 // completion (~11 % of C2 throughput, profiles/r02_ab_unit_cost.jsonl).
-__device__ __forceinline__ uint32_t wave_max(uint32_t v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v = max(v, (uint32_t)__shfl_xor(v, off, 64));
-    return v;
-}
-// option "cost_max": a unit's recorded cost is 64 x the steps of its longest path (the launch ends with
-// its longest paths, which a unit's summed cost can rank mid-order); else the sum over its paths
-__device__ __forceinline__ void unit_cost_flush(uint32_t *cost, uint32_t unit, uint32_t c, bool use_max) {
-    if (use_max) atomicMax(cost + unit, c);
-    else atomicAdd(cost + unit, c);
-}
+// a unit's recorded cost is the sum over its paths (round 3's "cost_max", 64 x its longest path, ordered C2 slower)
+__device__ __forceinline__ void unit_cost_flush(uint32_t *cost, uint32_t unit, uint32_t c) { atomicAdd(cost + unit, c); }
 // the pending sums of the lanes in `fin`: one atomic per distinct unit
-__device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t unit, uint32_t c, bool use_max) {
+__device__ __forceinline__ void unit_cost_add(uint32_t *cost, bool fin, uint32_t unit, uint32_t c) {
     uint64_t m = __ballot(fin);
     while (m) {
         const uint32_t first = (uint32_t)__builtin_ctzll(m);
         const uint32_t u = __shfl(unit, (int)first, 64);
         const bool mine = fin && unit == u;
-        const uint32_t x = use_max ? wave_max(mine ? c : 0u) : wave_sum(mine ? c : 0u);
-        if ((threadIdx.x & 63u) == first) unit_cost_flush(cost, u, x, use_max);
+        const uint32_t x = wave_sum(mine ? c : 0u);
+        if ((threadIdx.x & 63u) == first) unit_cost_flush(cost, u, x);
         m &= ~(uint64_t)__ballot(mine);
     }
 }
@@ -1575,7 +1550,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                                       : p_end - p_begin;
                 }
                 if (track) {                         // completes under the claim's wait
-                    unit_cost_add(out.unit_cost, pend_cost != 0, pend_unit, pend_cost, out.cost_max != 0);
+                    unit_cost_add(out.unit_cost, pend_cost != 0, pend_unit, pend_cost);
                     pend_cost = 0;
                 }
                 uint32_t b = 0;
@@ -1597,7 +1572,7 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
                 }
                 if (out.order) {
                     const uint32_t it = out.order[4u * (p_begin >> 6) + b];
-                    // log2 pieces 3: two adjacent light units (schedule option "merge"), 128 pixels
+                    // log2 pieces 3: two adjacent light units (schedule setting "merge"), 128 pixels
                     const uint32_t ls = it & 3u, len = ls == 3u ? 128u : 64u >> ls;
                     pool_next = (it >> 4) * 64u + (ls == 3u ? 0u : ((it >> 2) & 3u) * len);
                     pool_end = pool_next + len;
@@ -1724,16 +1699,16 @@ __device__ __forceinline__ void render_persistent_body(const SceneGPU &sc, const
         if (track && fin) {
             const uint32_t u = item >> 6;
             if (u != pend_unit) {
-                if (pend_cost) unit_cost_flush(out.unit_cost, pend_unit, pend_cost, out.cost_max != 0);
+                if (pend_cost) unit_cost_flush(out.unit_cost, pend_unit, pend_cost);
                 pend_unit = u;
                 pend_cost = 0;
             }
-            pend_cost = out.cost_max ? max(pend_cost, (px_steps + 1u) * 64u) : pend_cost + px_steps + 1u;
+            pend_cost = pend_cost + px_steps + 1u;
         }
         DIAG_ADD(pc.shade, t_shade);
     }
 
-    if (track && pend_cost) unit_cost_flush(out.unit_cost, pend_unit, pend_cost, out.cost_max != 0);
+    if (track && pend_cost) unit_cost_flush(out.unit_cost, pend_unit, pend_cost);
     const uint32_t wr = wave_sum(rays);
     const uint32_t wp = wave_sum(pixels);
     if (COUNT) {
@@ -1820,10 +1795,10 @@ __global__ __launch_bounds__(BLOCK) void trace_rays_kernel(SceneGPU sc, const fl
 
 // rt_box_test (parity tests, not a render path): the box decisions the kernels take, on caller boxes and rays, one
 // thread per (box, ray, tmax) with tmin = 0.001.  Mode 0 (EXACT build): BoundingBox::hit (BoundingBox.cu:34-72).  FAST
-// build: 1 the single-box conservative cull (slab<XBOX(1)>: host SAH trees' instance and root boxes), 2 the same with
-// marginal decisions re-taken exactly (slab<XD_ALL>: binary pairs, instance and root boxes of the exact-decision
-// instances), 3 a quad slot in pair order with exact decisions (quad_decide<true, XD_ALL>: the reference's and
-// GPU-built trees), 4 a quad slot of the greedy collapse (quad_decide<false, XBOX(1)>: host SAH trees).  Modes 3 / 4 put the box in slot 0 of a quad whose slot 1 is
+// build: 1 the single-box conservative cull (slab<XD_CULL>: instance and root boxes of modes 1 / 2), 2 the same with
+// marginal decisions re-taken exactly (slab<XD_ALL>: binary pairs, instance and root boxes of mode 3), 3 a quad slot in
+// pair order with exact decisions (quad_decide<true, XD_ALL>: mode 3), 4 a quad slot's conservative cull
+// (quad_decide<false, XD_CULL>: modes 1 / 2).  Modes 3 / 4 put the box in slot 0 of a quad whose slot 1 is
 // its empty partner (a leaf child's) and whose slots 2 / 3 hold a box behind the ray's origin.
 __global__ __launch_bounds__(BLOCK) void box_test_kernel(const float *boxes, const float *rays, const float *tmaxs, uint32_t n,
                                                          uint32_t mode, uint8_t *hit, float *te) {
@@ -1843,7 +1818,7 @@ __global__ __launch_bounds__(BLOCK) void box_test_kernel(const float *boxes, con
 #else
     if (mode == 1 || mode == 2) {
         if (mode == 2) { prep<XD_ALL>(r); h = slab<XD_ALL>(b, r, TMIN, tmax, e); }
-        else { prep<XBOX(1)>(r); h = slab<XBOX(1)>(b, r, TMIN, tmax, e); }
+        else { prep<XD_CULL>(r); h = slab<XD_CULL>(b, r, TMIN, tmax, e); }
     } else {
         float4 Q[8];
         float bb[6];       // behind the origin: around o - d, half-width |d_a| / 2 per axis (exit t = -0.5 on every axis)
@@ -1865,8 +1840,8 @@ __global__ __launch_bounds__(BLOCK) void box_test_kernel(const float *boxes, con
             prep<XD_ALL>(r);
             quad_decide<true, XD_ALL>(Q, Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], R, r, tmax, t, hq, pa, pb);
         } else {
-            prep<XBOX(1)>(r);
-            quad_decide<false, XBOX(1)>(Q, Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], R, r, tmax, t, hq, pa, pb);
+            prep<XD_CULL>(r);
+            quad_decide<false, XD_CULL>(Q, Q[0], Q[1], Q[2], Q[3], Q[4], Q[5], R, r, tmax, t, hq, pa, pb);
         }
         h = hq[0];
         e = t[0];
@@ -1910,62 +1885,45 @@ uint32_t blocks_per_cu_wpe() {
     return n > 0 ? (uint32_t)n : 1u;
 }
 #if RT_EXACT
-constexpr bool HAS_WIDE = false;      // EXACT keeps the reference's binary trees and visit order
+constexpr int HAS_WIDE = 0;           // EXACT keeps the reference's binary trees and visit order
 #else
-constexpr bool HAS_WIDE = true;
+constexpr int HAS_WIDE = 1;
 #endif
 }  // namespace
 
-// variant: 0 = compiler's register budget (quad trees: at least 3 waves per SIMD), 4 = at least 4 waves per SIMD.
+// One instance per scene kind: traversal mode W (SceneGPU::wide, XBOX) and where a hit triangle's shading data lives
+// (finalize's RAW: GPU-built trees without cold records).  Quad trees hold 3 waves per SIMD (WPE 3); binary pairs take
+// the compiler's budget (WPE 0).  (Round 5's option "variant" 4 — at least 4 waves per SIMD — was 12 % slower: removed.)
+#define RT_DISPATCH_INSTANCE(wide, raw, CALL)                                                  \
+    do {                                                                                       \
+        if ((wide) && HAS_WIDE) {                                                              \
+            if ((raw) && (wide) == 3) return CALL(3, 3 * HAS_WIDE, 1);                         \
+            if (raw) return CALL(3, 2 * HAS_WIDE, 1);                                          \
+            if ((wide) == 3) return CALL(3, 3 * HAS_WIDE, 0);                                  \
+            if ((wide) == 2) return CALL(3, 2 * HAS_WIDE, 0);                                  \
+            return CALL(3, HAS_WIDE, 0);                                                       \
+        }                                                                                      \
+        return CALL(0, 0, 2);                                                                  \
+    } while (0)
+
 hipError_t RT_SUFFIX(launch_render_persistent)(const SceneGPU &sc, const CameraGPU &cam, const OutputGPU &out, bool count,
                                                unsigned long long *counters, uint32_t *queue, uint32_t blocks,
-                                               uint32_t threshold, uint32_t variant, bool reset_queue, hipStream_t stream) {
+                                               uint32_t threshold, bool reset_queue, hipStream_t stream) {
     if (out.units == 0) return hipSuccess;
     if (reset_queue) {       // else the schedule kernel (schedule.hip) just reset the heads
         const hipError_t e = hipMemsetAsync(queue, 0, QUEUE_MAX_PARTS * QUEUE_STRIDE * sizeof(uint32_t), stream);
         if (e != hipSuccess) return e;
     }
-    // quad trees: one instance per scene kind — traversal mode (SceneGPU::wide, XBOX) and where a hit triangle's shading
-    // data lives (finalize's RAW; GPU-built trees are always in pair order)
-    if (sc.wide && HAS_WIDE) {
-        if (sc.raw_tris) {
-            if (sc.wide == 3) {
-                if (variant == 4) return launch_persistent_wpe<4, 3 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-                return launch_persistent_wpe<3, 3 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-            }
-            if (variant == 4) return launch_persistent_wpe<4, 2 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-            return launch_persistent_wpe<3, 2 * HAS_WIDE, 1>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-        }
-#if !RT_XBOX_GPU                      // else modes 2 and 3 take the same (exact-decision) instance
-        if (sc.wide == 3) {
-            if (variant == 4) return launch_persistent_wpe<4, 3 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-            return launch_persistent_wpe<3, 3 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-        }
-#endif
-        if (sc.wide >= 2) {
-            if (variant == 4) return launch_persistent_wpe<4, 2 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-            return launch_persistent_wpe<3, 2 * HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-        }
-        if (variant == 4) return launch_persistent_wpe<4, HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-        return launch_persistent_wpe<3, HAS_WIDE, 0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-    }
-    if (variant == 4) return launch_persistent_wpe<4>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
-    return launch_persistent_wpe<0>(sc, cam, out, count, counters, queue, blocks, threshold, stream);
+#define RT_LAUNCH(WPE, W, RAW) launch_persistent_wpe<WPE, W, RAW>(sc, cam, out, count, counters, queue, blocks, threshold, stream)
+    RT_DISPATCH_INSTANCE(sc.wide, sc.raw_tris != nullptr, RT_LAUNCH);
+#undef RT_LAUNCH
 }
 
 // the occupancy of the instance launch_render_persistent runs for (wide, raw): the persistent grid is sized from it
-uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t variant, uint32_t wide, bool raw) {
-    if (wide && HAS_WIDE) {
-        if (raw && wide == 3) return variant == 4 ? blocks_per_cu_wpe<4, 3 * HAS_WIDE, 1>() : blocks_per_cu_wpe<3, 3 * HAS_WIDE, 1>();
-        if (raw) return variant == 4 ? blocks_per_cu_wpe<4, 2 * HAS_WIDE, 1>() : blocks_per_cu_wpe<3, 2 * HAS_WIDE, 1>();
-#if !RT_XBOX_GPU
-        if (wide == 3) return variant == 4 ? blocks_per_cu_wpe<4, 3 * HAS_WIDE, 0>() : blocks_per_cu_wpe<3, 3 * HAS_WIDE, 0>();
-#endif
-        if (wide >= 2) return variant == 4 ? blocks_per_cu_wpe<4, 2 * HAS_WIDE, 0>() : blocks_per_cu_wpe<3, 2 * HAS_WIDE, 0>();
-        return variant == 4 ? blocks_per_cu_wpe<4, HAS_WIDE, 0>() : blocks_per_cu_wpe<3, HAS_WIDE, 0>();
-    }
-    if (variant == 4) return blocks_per_cu_wpe<4>();
-    return blocks_per_cu_wpe<0>();
+uint32_t RT_SUFFIX(persistent_blocks_per_cu)(uint32_t wide, bool raw) {
+#define RT_OCC(WPE, W, RAW) blocks_per_cu_wpe<WPE, W, RAW>()
+    RT_DISPATCH_INSTANCE(wide, raw, RT_OCC);
+#undef RT_OCC
 }
 hipError_t RT_SUFFIX(launch_trace_rays)(const SceneGPU &sc, const float *rays, uint32_t n, rt_hit *hits,
                                         hipStream_t stream) {

@@ -15,8 +15,7 @@ using namespace rtamd;
 int main(int argc, char **argv) {
     const uint32_t n = argc > 1 ? (uint32_t)atoi(argv[1]) : 1000;
     const int sah = argc > 2 ? atoi(argv[2]) : 1;
-    const uint32_t merge = argc > 3 ? (uint32_t)atoi(argv[3]) : 0;
-    const bool halves = argc > 4 ? atoi(argv[4]) != 0 : true;        // two binary levels per quad, else greedy
+    const bool halves = argc > 3 ? atoi(argv[3]) != 0 : true;        // two binary levels per quad, else greedy
     std::mt19937 rng(n * 7 + sah);
     std::uniform_real_distribution<float> U(-10.0f, 10.0f), S(0.01f, 1.0f);
     std::vector<BuildItem> items(n);
@@ -28,7 +27,7 @@ int main(int argc, char **argv) {
     }
     const Tree t = sah ? build_sah_tree(items, 4) : build_median_tree(items, 4, 12345);
     const FlatTree f2 = flatten_tree(t, 0, 100, 2, true);
-    const FlatWide f4 = flatten_tree_wide(t, 0, 100, 2, true, halves, merge);
+    const FlatWide f4 = flatten_tree_wide(t, 0, 100, 2, true, halves);
     // leaves and boxes reachable from each form
     std::multiset<uint32_t> leaves2, leaves4;
     std::set<std::vector<float>> boxes2, boxes4;

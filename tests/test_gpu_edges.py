@@ -6,6 +6,8 @@ The oracle (tests only) traverses the reference-order compat trees; EXACT frames
 bit-identical in float RGB.  Single-primitive scenes have no hit ties, so every
 builder (compat / SAH / GPU LBVH) must give the oracle's bits there too.
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -60,21 +62,18 @@ def test_ragged_frame_sizes_exact(gpu_lib, w, h):
 
 @pytest.mark.parametrize("w,h", [(7, 5), (65, 33)])
 def test_ragged_frame_sizes_fast_kernels_agree(gpu_lib, w, h):
-    """FAST mode on ragged frames: the persistent kernel at every refill threshold gives the same
-    bytes, and stays within the FAST tolerance of the oracle."""
+    """FAST mode on ragged frames: the persistent kernel (quads, binary pairs) and the grid kernel give the same
+    bytes on the reference's trees (every box decision the reference's), equal to the oracle's float frame."""
     s = scenes.demo_with_particles(4)
     r = Renderer(s).build_acceleration_structure(0).configure_camera(w, h, ray_trace_depth=2, sample_count=4)
     o = _oracle(s, w, h, 0, ray_trace_depth=2, sample_count=4)
-    _, orgba, _ = o.render(threads=THREADS)
-    ref = None
-    for thr in (1, 16, 40, 64):
-        r.set_option("threshold", thr)
+    orgb, orgba, _ = o.render(threads=THREADS)
+    for kernel, wide in ((1, 1), (1, 0), (0, 1)):
+        r.set_option("kernel", kernel).set_option("wide", wide)
         rgba, rgb, st = r.render(0, want_rgb=True)
-        if ref is None:
-            ref = rgb
-        assert np.array_equal(rgb, ref), thr
+        assert np.array_equal(rgb, orgb), (kernel, wide)
         d = np.abs(rgba.astype(np.int32) - orgba.astype(np.int32)).max(axis=-1)
-        assert (d <= 1).mean() >= 0.99, thr
+        assert (d <= 1).all(), (kernel, wide)
 
 
 @pytest.mark.parametrize("kind", ["sphere", "parallelogram", "triangle"])
@@ -209,4 +208,34 @@ def test_synchronous_frame_after_pipelined_frames(gpu_lib):
         r.synchronize()
         for f in range(6):
             assert np.array_equal(outs[f].cpu().numpy().reshape(H, W, 4), ref[f]), (it, f)
+    r.cleanup()
+
+
+DOCUMENTED_OPTIONS = {"overlap": -1, "stage_depth": 8, "lane_priority": 1, "grid_pct": 0, "rebuild": 0, "cold_records": -1,
+                      "blas_double": 1, "blas_sets": 3, "tlas_small": 1, "exact_decisions": 0, "group": 1, "gpu_tlas": 0,
+                      "tlas_sah": 1, "kernel": 1, "wide": 1, "fast_math": 0, "reorder": 1, "timeline": 0, "costmap": 0}
+REMOVED_OPTIONS = ("threshold", "leaf_early", "queue_parts", "grab", "supertile", "merge", "split", "reorder_period",
+                   "reserve", "lds_scene", "lds_blas", "inst_by_slot", "blas_leaf", "tlas_leaf", "tlas_median_leaf",
+                   "variant", "nt_store", "cost_max", "tlas_classes", "wide_merge", "scene_priority")
+
+
+def test_option_surface_is_the_documented_one(gpu_lib):
+    """rt_scene_set_option accepts exactly the 19 keys include/rt.h documents (verdict r5 item 7: the A/B-only and
+    measured-negative switches are gone) and rejects the removed ones and bad values with RT_ERR_INVALID_ARGUMENT."""
+    import re
+    from rtamd import abi
+    hdr = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "rt.h")).read()
+    block = hdr[hdr.index("/* Scene options"):hdr.index("rt_status rt_scene_set_option(")]
+    documented = set(re.findall(r'^ \*   "(\w+)"', block, re.M))
+    assert documented == set(DOCUMENTED_OPTIONS), documented ^ set(DOCUMENTED_OPTIONS)
+    assert len(documented) <= 20
+    r = Renderer(scenes.demo_scene())
+    for k, v in DOCUMENTED_OPTIONS.items():
+        r.set_option(k, v)
+    for k in REMOVED_OPTIONS:
+        with pytest.raises(abi.RtError, match="RT_ERR_INVALID_ARGUMENT"):
+            r.set_option(k, 0)
+    for k in ("tlas_sah", "exact_decisions", "lane_priority", "reorder"):
+        with pytest.raises(abi.RtError, match="RT_ERR_INVALID_ARGUMENT"):
+            r.set_option(k, 2)
     r.cleanup()

@@ -63,28 +63,6 @@ def test_group_images_and_hits_match_oracle(gpu_lib):
         assert np.all(np.abs(h["t"][hit] - oh["t"][hit]) <= 1e-4 * oh["t"][hit])
 
 
-def test_group_with_instance_order_records(gpu_lib):
-    """inst_by_slot 0 (records by instance index, the group's record after the instances'): same frames."""
-    s = scenes.demo_with_particles(12)
-    r = Renderer(s).build_acceleration_structure(0, mode="sah").configure_camera(240, 136, ray_trace_depth=2)
-    ref = [r.render(f)[0] for f in range(3)]
-    r.set_option("inst_by_slot", 0)
-    for f in range(3):
-        assert np.array_equal(r.render(f)[0], ref[f]), f
-
-
-def test_group_with_instance_order_records_lbvh(gpu_lib):
-    """The same with GPU-built frames (one-workgroup TLAS, "tlas_small"): the trace reads the record-order array,
-    whose TLAS slots index every record (members included), so the LDS copy must hold all of them, not only the
-    live ones (frame_items = live read past the copied records)."""
-    s = scenes.demo_with_particles(12)
-    r = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(240, 136, ray_trace_depth=2)
-    ref = [r.render(f)[0] for f in range(3)]
-    r.set_option("inst_by_slot", 0)
-    for f in range(3):
-        assert np.array_equal(r.render(f)[0], ref[f]), f
-
-
 def test_broken_group_equals_ungrouped_scene(gpu_lib):
     """A member whose transform changes takes the group out of the TLAS: that frame equals the frame of the
     scene built without groups byte for byte (same per-instance items, same trees)."""

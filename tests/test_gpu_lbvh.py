@@ -280,20 +280,6 @@ def test_update_triangles_needs_lbvh(gpu_lib):
         r.set_option("rebuild", 1)
 
 
-def test_scene_priority_option(gpu_lib):
-    """"scene_priority" picks the scene stream's priority at rt_scene_build: the frames are the same, and it is
-    refused once the stream exists (include/rt.h)."""
-    s = scenes.demo_with_particles(4)
-    a = Renderer(s).build_acceleration_structure(0, mode="lbvh").configure_camera(64, 48, ray_trace_depth=2)
-    r = Renderer(s).set_option("scene_priority", 1).build_acceleration_structure(0, mode="lbvh").configure_camera(
-        64, 48, ray_trace_depth=2)
-    assert np.array_equal(r.render(3)[0], a.render(3)[0])
-    with pytest.raises(abi.RtError, match="RT_ERR_STATE"):
-        r.set_option("scene_priority", 0)
-    a.cleanup()
-    r.cleanup()
-
-
 def test_large_forest_c5_shape(gpu_lib):
     """1,000 particle BLASes (1.02 M triangles, the C5 shape at 1/10 scale): every primitive is in
     exactly one leaf of its BLAS, and a frame matches the oracle within the FAST tolerance."""
@@ -517,4 +503,9 @@ def test_cold_records_auto_same_frames(gpu_lib, rebuild):
         for a, b in zip(frames[-1], frames[cold]):
             assert np.array_equal(a, b), cold
     assert dev[-1] == (dev[0] if rebuild else dev[1]), dev
-    assert dev[1] > dev[0], dev
+    # device_bytes counts the builder's workspace since round 6: without cold records the prep kernel
+    # stages the TriHot records in item order (48 B per triangle), as many bytes as one set of TriCold records, so
+    # only the per-frame rebuild's spare BLAS sets (each with TriCold records when cold) make cold records cost more
+    assert dev[0] != dev[1], dev
+    if rebuild:
+        assert dev[1] > dev[0], dev

@@ -20,14 +20,12 @@ def checker(tmp_path_factory):
 
 
 @pytest.mark.parametrize("halves", [1, 0])
-@pytest.mark.parametrize("merge", [0, 4])
 @pytest.mark.parametrize("n,sah", [(1, 1), (3, 1), (5, 0), (17, 1), (1000, 1), (1000, 0), (20000, 1)])
-def test_quad_form_preserves_leaves_and_boxes(checker, n, sah, merge, halves):
-    """merge = 4: binary subtrees of <= 4 items become one leaf (option "wide_merge")."""
-    r = json.loads(subprocess.run([checker, str(n), str(sah), str(merge), str(halves)], check=True, capture_output=True,
+def test_quad_form_preserves_leaves_and_boxes(checker, n, sah, halves):
+    r = json.loads(subprocess.run([checker, str(n), str(sah), str(halves)], check=True, capture_output=True,
                                   text=True).stdout)
     assert r["slots_equal"] == 1 and r["bad_boxes"] == 0, r
     if r["quads"]:
-        assert 2 <= r["min_children"] <= 4 and r["mean_children"] > (2.5 if merge else 3.0) or n < 20, r
+        assert 2 <= r["min_children"] <= 4 and r["mean_children"] > 3.0 or n < 20, r
         assert r["height4"] <= (r["height2"] + 1) // 2 + 2, r
         assert r["quads"] <= r["pairs"], r
