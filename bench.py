@@ -56,6 +56,8 @@ def parse():
     p.add_argument("--build", default="sah", choices=("sah", "compat", "lbvh"),
                    help="BVH builder: SAH (default), the reference's random-axis median split, or the GPU LBVH builder")
     p.add_argument("--rebuild", action="store_true", help="--build lbvh: rebuild every BLAS on the GPU each frame (C5)")
+    p.add_argument("--no-rebuild-roofline", action="store_true",
+                   help="--rebuild: skip the untimed rebuild-alone stage timing (the line's \"rebuild\" block)")
     p.add_argument("--kernel", type=int, default=1, help="1 = persistent megakernel, 0 = grid kernel")
     p.add_argument("--overlap", type=int, default=None,
                    help="L >= 2: consecutive frames cycle L streams / library lanes so frame k+1 fills the CUs "
@@ -202,6 +204,62 @@ def load_traffic(tag):
 
 
 rt_scene_lanes_max = 8                                     # rt.h: "overlap" lanes 2..8
+
+
+# The per-frame GPU BLAS rebuild (--build lbvh --rebuild; csrc/lbvh.hip) priced per stage the way the trace is: the
+# bytes each stage's kernels must move at least (reads of their inputs, writes of their outputs, per item / interior
+# node / node pair of the forest; scratch and re-reads not counted), over the stage's HIP-event time in a rebuild alone
+# (option "timeline": events between the stages, rt_scene_debug_read "rebuild_stages").  N items (10 M triangles on
+# C5), NI = N - trees interior nodes, P node pairs written (interior nodes of > 4 items).
+REBUILD_STAGES = ("prep", "bounds", "morton", "sort", "karras_gather", "bottom_up", "scan", "emit_roots", "collapse")
+
+
+def rebuild_bytes(N, NI, P):
+    return {
+        # 36 B vertices + segment id + group member read; 24 B box, 16 B centroid, 48 B TriHot staged (item order)
+        "prep": N * (36 + 4 + 4 + 24 + 16 + 48),
+        "bounds": N * (16 + 4),                                # centroid + segment id
+        "morton": N * (16 + 4 + 4 + 4),                        # centroid + segment id in, key + item out
+        "sort": N * (4 + 4 * 16),                              # key histogram + 4 8-bit passes of (key, item) in / out
+        # sorted key + segment id + item id per item, child / range / flag / parent per interior node; the leaf-
+        # ordered gather: the staged 48 B record in, 48 B out
+        "karras_gather": N * (4 + 4 + 4 + 48 + 48) + NI * (8 + 8 + 4 + 8),
+        # per item: item box (24) by its id (4), segment id, parent; per node: children, range, parent in, box,
+        # height, kept flag out
+        "bottom_up": N * (24 + 4 + 4 + 4) + NI * (8 + 8 + 4 + 24 + 4 + 4),
+        "scan": NI * 8,                                        # kept flags in, pair indices out
+        # kept flag per node; per pair: children, range, segment, two child boxes, child pair indices, 64 B pair out
+        "emit_roots": NI * 4 + P * (8 + 8 + 4 + 48 + 8 + 64),
+        "collapse": P * (64 + 128 + 128),                      # own pair + <= 2 child pairs in, 128 B quad out
+    }
+
+
+def rebuild_roofline(r, frames):
+    """Rebuild-alone timing of the scene's per-frame BLAS rebuild (rt_scene_update, no trace) with stage events: mean
+    stage ms over `frames` updates, algorithmic bytes per stage, achieved GB/s and the fraction of HBM peak; the chain
+    total too.  Called after the timed region (events between the stages cost ~5 us each)."""
+    import numpy as np
+    r.set_option("timeline", 1)
+    rows = []
+    t0 = time.perf_counter()
+    for f in frames:
+        r.update(f)
+        rows.append(r.debug_read("rebuild_stages").view(np.float64).copy())
+    wall = (time.perf_counter() - t0) * 1e3 / len(frames)
+    r.set_option("timeline", 0)
+    a = np.mean(np.stack(rows), axis=0)
+    N, NI, P = int(a[0]), int(a[1]), int(round(a[2]))
+    ms = dict(zip(REBUILD_STAGES, a[3:].tolist()))
+    by = rebuild_bytes(N, NI, P)
+    stages = {k: {"ms": round(ms[k], 4), "bytes": int(by[k]), "achieved_gbs": round(by[k] / (ms[k] * 1e-3) / 1e9, 1),
+                  "frac": round(by[k] / (ms[k] * 1e-3) / 1e9 / HBM_PEAK_GBS, 3)} for k in REBUILD_STAGES}
+    tot_ms, tot_b = float(sum(ms.values())), float(sum(by.values()))
+    return {"items": N, "interior_nodes": NI, "node_pairs": P, "updates": len(frames),
+            "ms_stages_sum": round(tot_ms, 4), "ms_per_update_wall": round(wall, 4), "bytes": int(tot_b),
+            "achieved_gbs": round(tot_b / (tot_ms * 1e-3) / 1e9, 1),
+            "frac": round(tot_b / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3), "peak_gbs": HBM_PEAK_GBS,
+            "timing": "rebuild alone (rt_scene_update, no trace), HIP events between the builder's stages, mean over "
+                      "the updates", "stages": stages}
 
 
 def main():
@@ -440,6 +498,14 @@ def main():
                                  stream=stream)
     if n > 1:
         dist.barrier()
+    # the per-frame BLAS rebuild's own roofline (untimed; every rank rebuilds its replica, so rank 0's is the figure)
+    rebuild_block = None
+    if args.rebuild and not args.no_rebuild_roofline:
+        torch.cuda.synchronize()
+        r.synchronize()
+        rebuild_block = rebuild_roofline(r, [args.warmup + args.steps + k for k in range(6)])
+    if n > 1:
+        dist.barrier()
 
     if rank == 0:
         avg_kernel_ms = float(np.mean(kernel_ms))            # timed region: launches overlap (L lanes)
@@ -556,6 +622,8 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if rebuild_block is not None:
+            out["rebuild"] = rebuild_block
         if n == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(scene, cfg, args.cpu_seconds)
         print(json.dumps(out), flush=True)

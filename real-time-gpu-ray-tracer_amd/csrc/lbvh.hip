@@ -522,7 +522,13 @@ __global__ __launch_bounds__(BLOCK) void bottom_up_local_kernel(const LbvhSeg *s
 // edge records that arrival, and a second kernel climbs from each recorded arrival with the device-wide hand-off
 // described above (kernel boundary: the chunk-finished boxes are visible to it).
 // (One device-wide pass over all 10 M nodes took 1.7 ms per C5 rebuild: every level an agent-scope round trip.)
-constexpr uint32_t CHUNK = 1024;               // = the chunk kernel's workgroup: one thread per item
+#ifndef LBVH_CHUNK
+#define LBVH_CHUNK 1024                         // round 6: 2048-item chunks (two items per thread, ~153 KB of LDS, one
+#endif                                          // workgroup per CU) made the C5 rebuild slower: 2.33 against 2.17 ms
+constexpr uint32_t CHUNK = LBVH_CHUNK;         // sorted items per workgroup
+constexpr uint32_t CHUNK_THREADS = 1024;       // the chunk kernel's workgroup: CHUNK / CHUNK_THREADS items per thread
+constexpr uint32_t CHUNK_PER = CHUNK / CHUNK_THREADS;
+static_assert(CHUNK % CHUNK_THREADS == 0, "whole items per thread");
 __device__ __forceinline__ bool chunk_local(const uint32_t *range, uint32_t g) {
     return range[2 * g] / CHUNK == range[2 * g + 1] / CHUNK;
 }
@@ -552,14 +558,15 @@ __device__ __forceinline__ void climb_top(const LbvhSeg &S, uint32_t g, const ui
 }
 
 // The chunk's own nodes (the interior node at each of its positions: child refs, item range, parent) are staged
-// in LDS with one coalesced load per thread before the climbs, so a climb step waits on LDS only (reading them
-// from HBM / L2 per step made every level a dependent global round trip: 0.64 ms per C5 rebuild).
-__global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *segs, const uint32_t *seg_of,
-                                                                const uint32_t *vals, const float *item_box, uint32_t n,
-                                                                const uint32_t *child, const uint32_t *parent,
-                                                                const uint32_t *parent_leaf, const uint32_t *range,
-                                                                float *nbox, uint32_t *height, uint32_t *kept,
-                                                                uint32_t *frontier) {
+// in LDS with coalesced loads before the climbs, so a climb step waits on LDS only (reading them from HBM / L2 per
+// step made every level a dependent global round trip: 0.64 ms per C5 rebuild).  LBVH_CHUNK = 2048 (two items per
+// thread) halves the chunk edges and the top pass's device-wide climbs, but was measured slower (above).
+__global__ __launch_bounds__(CHUNK_THREADS) void bottom_up_chunk_kernel(const LbvhSeg *segs, const uint32_t *seg_of,
+                                                                        const uint32_t *vals, const float *item_box,
+                                                                        uint32_t n, const uint32_t *child,
+                                                                        const uint32_t *parent, const uint32_t *parent_leaf,
+                                                                        const uint32_t *range, float *nbox, uint32_t *height,
+                                                                        uint32_t *kept, uint32_t *frontier) {
     __shared__ float sleaf[CHUNK * 6];          // the chunk's item boxes, in sorted order
     __shared__ float sbox[CHUNK * 6];           // node boxes, at the node's own position
     __shared__ uint32_t sheight[CHUNK];
@@ -569,33 +576,42 @@ __global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *s
     constexpr uint32_t FRONT_LDS = 256;         // this chunk's arrivals for the top pass (~20 typical; more go direct)
     __shared__ uint32_t sfront[FRONT_LDS];
     __shared__ uint32_t sfront_n, sfront_at;
-    const uint32_t lo = blockIdx.x * CHUNK, p = lo + threadIdx.x;
-    sflag[threadIdx.x] = 0;
+    const uint32_t lo = blockIdx.x * CHUNK;
+    for (uint32_t j = 0; j < CHUNK_PER; j++) sflag[threadIdx.x + j * CHUNK_THREADS] = 0;
     if (threadIdx.x == 0) sfront_n = 0;
-    const uint32_t seg = p < n ? seg_of[p] : NONE;
-    const bool big = seg != NONE && segs[seg].count > LOCAL_MAX;   // else bottom_up_local_kernel
-    LbvhSeg S;
-    if (big) {
-        S = segs[seg];
-        const float2 *src = reinterpret_cast<const float2 *>(item_box + 6 * (size_t)vals[p]);
+    uint32_t seg[CHUNK_PER];
+    bool big[CHUNK_PER];
+    LbvhSeg S[CHUNK_PER];
 #pragma unroll
-        for (int k = 0; k < 3; k++) { const float2 v = src[k]; sleaf[6 * threadIdx.x + 2 * k] = v.x; sleaf[6 * threadIdx.x + 2 * k + 1] = v.y; }
-        if (p - S.item_base + 1u < S.count) {
-            const uint32_t g = S.node_base + (p - S.item_base);
-            schild[threadIdx.x] = reinterpret_cast<const uint2 *>(child)[g];
-            srange[threadIdx.x] = reinterpret_cast<const uint2 *>(range)[g];
-            sparent[threadIdx.x] = parent[g];
+    for (uint32_t j = 0; j < CHUNK_PER; j++) {
+        const uint32_t l = threadIdx.x + j * CHUNK_THREADS, p = lo + l;
+        seg[j] = p < n ? seg_of[p] : NONE;
+        big[j] = seg[j] != NONE && segs[seg[j]].count > LOCAL_MAX;   // else bottom_up_local_kernel
+        if (big[j]) {
+            S[j] = segs[seg[j]];
+            const float2 *src = reinterpret_cast<const float2 *>(item_box + 6 * (size_t)vals[p]);
+#pragma unroll
+            for (int k = 0; k < 3; k++) { const float2 v = src[k]; sleaf[6 * l + 2 * k] = v.x; sleaf[6 * l + 2 * k + 1] = v.y; }
+            if (p - S[j].item_base + 1u < S[j].count) {
+                const uint32_t g = S[j].node_base + (p - S[j].item_base);
+                schild[l] = reinterpret_cast<const uint2 *>(child)[g];
+                srange[l] = reinterpret_cast<const uint2 *>(range)[g];
+                sparent[l] = parent[g];
+            }
         }
     }
     __syncthreads();
-    if (big) {
+    for (uint32_t j = 0; j < CHUNK_PER; j++) {
+        if (!big[j]) continue;
+        const uint32_t p = lo + threadIdx.x + j * CHUNK_THREADS;
+        const LbvhSeg &Sj = S[j];
         uint32_t g = parent_leaf[p];
         bool first = false;                             // stopped as a node's first arrival
         while (g != NONE) {
-            const uint32_t l = S.item_base + (g - S.node_base) - lo;   // the node's own position, if in this chunk
-            if (l >= CHUNK) break;                                     // its range leaves the chunk
+            const uint32_t l = Sj.item_base + (g - Sj.node_base) - lo;   // the node's own position, if in this chunk
+            if (l >= CHUNK) break;                                       // its range leaves the chunk
             const uint2 rg = srange[l];
-            if (rg.x / CHUNK != rg.y / CHUNK) break;                   // the same
+            if (rg.x / CHUNK != rg.y / CHUNK) break;                     // the same
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
             if (atomicAdd(&sflag[l], 1u) == 0u) { first = true; break; }
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -603,14 +619,14 @@ __global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *s
             uint32_t h = 0;
             const uint2 cc = schild[l];
 #pragma unroll
-            for (int c = 0; c < 2; c++) {                              // union_children's order
+            for (int c = 0; c < 2; c++) {                                // union_children's order
                 const uint32_t ch = c == 0 ? cc.x : cc.y;
                 const float *cb;
                 uint32_t chh = 0;
-                if (ch & LEAF_BIT) {                                   // sorted position = the leaf's item index
+                if (ch & LEAF_BIT) {                                     // sorted position = the leaf's item index
                     cb = sleaf + 6 * ((ch & ~LEAF_BIT) - lo);
-                } else {                                               // inside the parent's range: this chunk
-                    const uint32_t lc = S.item_base + (ch - S.node_base) - lo;
+                } else {                                                 // inside the parent's range: this chunk
+                    const uint32_t lc = Sj.item_base + (ch - Sj.node_base) - lo;
                     cb = sbox + 6 * lc;
                     chh = sheight[lc];
                 }
@@ -628,7 +644,7 @@ __global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *s
             const uint32_t size = rg.y - rg.x + 1u;
 #pragma unroll
             for (int k = 0; k < 6; k++) sbox[6 * l + k] = b[k];
-            sheight[l] = size > S.leaf_cap ? h + 1u : 0u;
+            sheight[l] = size > Sj.leaf_cap ? h + 1u : 0u;
             g = sparent[l];
         }
         if (!first && g != NONE) {                      // g's range crosses a chunk edge: an arrival for the top pass
@@ -644,13 +660,17 @@ __global__ __launch_bounds__(CHUNK) void bottom_up_chunk_kernel(const LbvhSeg *s
     if (threadIdx.x == 0 && nf) sfront_at = atomicAdd(frontier, nf);
     __syncthreads();
     if (threadIdx.x < nf) frontier[1 + sfront_at + threadIdx.x] = sfront[threadIdx.x];
-    if (sflag[threadIdx.x] == 2u) {                                    // the node at this position finished here
-        const uint32_t l = threadIdx.x, g = S.node_base + (p - S.item_base);
-        const uint2 rg = srange[l];
 #pragma unroll
-        for (int k = 0; k < 6; k++) nbox[6 * (size_t)g + k] = sbox[6 * l + k];
-        height[g] = sheight[l];
-        kept[g] = (rg.y - rg.x + 1u) > S.leaf_cap ? 1u : 0u;
+    for (uint32_t j = 0; j < CHUNK_PER; j++) {
+        const uint32_t l = threadIdx.x + j * CHUNK_THREADS, p = lo + l;
+        if (sflag[l] == 2u) {                                            // the node at this position finished here
+            const uint32_t g = S[j].node_base + (p - S[j].item_base);
+            const uint2 rg = srange[l];
+#pragma unroll
+            for (int k = 0; k < 6; k++) nbox[6 * (size_t)g + k] = sbox[6 * l + k];
+            height[g] = sheight[l];
+            kept[g] = (rg.y - rg.x + 1u) > S[j].leaf_cap ? 1u : 0u;
+        }
     }
 }
 
@@ -1071,6 +1091,9 @@ static void dfree(T *&p) {
 }
 
 void LbvhBuilder::release() {
+    for (hipEvent_t &e : stage_ev_)
+        if (e) { (void)hipEventDestroy(e); e = nullptr; }
+    timing_ = false;
     dfree(segs_); dfree(seg_of_); dfree(members_); dfree(item_member_); dfree(own_box_); dfree(own_cent_); dfree(stage_); dfree(bounds_);
     dfree(k0_); dfree(k1_); dfree(v0_); dfree(v1_); dfree(child_); dfree(parent_); dfree(parent_leaf_);
     dfree(range_); dfree(flag_); dfree(height_); dfree(nbox_); dfree(kept_); dfree(pidx_); dfree(front_); dfree(count_); dfree(frontier_);
@@ -1122,7 +1145,29 @@ hipError_t LbvhBuilder::init(const std::vector<LbvhSeg> &segs, hipStream_t strea
     return hipStreamSynchronize(stream);
 }
 
+const char *const LbvhBuilder::STAGE_NAMES[LbvhBuilder::STAGES] = {
+    "prep", "bounds", "morton", "sort", "karras_gather", "bottom_up", "scan", "emit_roots", "collapse"};
+
+hipError_t LbvhBuilder::set_timing(bool on) {
+    if (on)
+        for (hipEvent_t &e : stage_ev_)
+            if (!e) LB_TRY(hipEventCreate(&e));
+    timing_ = on;
+    return hipSuccess;
+}
+
+hipError_t LbvhBuilder::stage_ms(float (&ms)[STAGES]) const {
+    for (int k = 0; k < STAGES; k++) {
+        ms[k] = 0.0f;
+        if (!stage_ev_[k] || !stage_ev_[k + 1]) return hipErrorInvalidValue;
+        LB_TRY(hipEventSynchronize(stage_ev_[k + 1]));
+        LB_TRY(hipEventElapsedTime(&ms[k], stage_ev_[k], stage_ev_[k + 1]));
+    }
+    return hipSuccess;
+}
+
 hipError_t LbvhBuilder::prep_blas_items(const RawPrimsGPU &raw, hipStream_t stream, bool stage_hot) {
+    LB_TRY(mark(0, stream));
     if (!own_box_) {
         LB_TRY(dalloc(own_box_, 6 * (size_t)n_items_));
         LB_TRY(dalloc(own_cent_, n_items_));
@@ -1133,7 +1178,8 @@ hipError_t LbvhBuilder::prep_blas_items(const RawPrimsGPU &raw, hipStream_t stre
     stage_ready_ = stage_hot;
     hipLaunchKernelGGL(prep_blas_kernel, dim3(blocks_for(n_items_)), dim3(BLOCK), 0, stream, segs_, seg_of_, n_items_, raw,
                        box_, cent_, stage_hot ? stage_ : nullptr, item_member_);
-    return hipGetLastError();
+    LB_TRY(hipGetLastError());
+    return mark(1, stream);
 }
 
 // item -> its member instance + 1 (group segments; 0 elsewhere), found once here instead of by every rebuild's gather
@@ -1203,8 +1249,11 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
         const uint32_t nb = (uint32_t)((N + (uint64_t)BLOCK * ipt - 1) / ((uint64_t)BLOCK * ipt));
         hipLaunchKernelGGL(bounds_kernel, dim3(nb), dim3(BLOCK), 0, stream, seg_of_, cent_, N, ipt, bounds_);
     }
+    if (box_ == own_box_) LB_TRY(mark(2, stream));           // BLAS builds: stage timing (TLAS builds record nothing)
+    const bool tm = box_ == own_box_;
     hipLaunchKernelGGL(morton_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, seg_of_, cent_, N, bounds_, k0_, v0_);
     LB_TRY(hipGetLastError());
+    if (tm) LB_TRY(mark(3, stream));
     size_t bytes = tmp_bytes_;
     if (big_segs_.size() < n_segs_)
         hipLaunchKernelGGL(local_sort_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, k0_, k1_, v1_);
@@ -1215,21 +1264,24 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
         LB_TRY(rocprim::radix_sort_pairs(tmp_, bytes, k0_ + b.first, k1_ + b.first, v0_ + b.first, v1_ + b.first, b.second, 0,
                                          end_bit, stream));
     }
+    if (tm) LB_TRY(mark(4, stream));
     hipLaunchKernelGGL(karras_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, seg_of_, k1_, N, child_, parent_,
                        parent_leaf_, range_, flag_, v1_, raw ? *raw : RawPrimsGPU{}, out ? *out : PrimOutGPU{}, item_member_,
                        stage_ready_ ? stage_ : nullptr, (uint32_t)(raw && out));
     stage_ready_ = false;
+    if (tm) LB_TRY(mark(5, stream));
     hipLaunchKernelGGL(bottom_up_local_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, v1_, box_, child_, parent_,
                        parent_leaf_, range_, nbox_, height_, kept_);
     if (max_count_ > LOCAL_MAX) {
         if (!frontier_) LB_TRY(dalloc(frontier_, 1 + 2 * (size_t)NI));   // <= 2 arrivals per internal node
         LB_TRY(hipMemsetAsync(frontier_, 0, sizeof(uint32_t), stream));
-        hipLaunchKernelGGL(bottom_up_chunk_kernel, dim3((N + CHUNK - 1) / CHUNK), dim3(CHUNK), 0, stream, segs_, seg_of_, v1_,
+        hipLaunchKernelGGL(bottom_up_chunk_kernel, dim3((N + CHUNK - 1) / CHUNK), dim3(CHUNK_THREADS), 0, stream, segs_, seg_of_, v1_,
                            box_, N, child_, parent_, parent_leaf_, range_, nbox_, height_, kept_, frontier_);
         hipLaunchKernelGGL(bottom_up_top_kernel, dim3(256), dim3(BLOCK), 0, stream, segs_, seg_of_, v1_, box_, child_, parent_,
                            range_, flag_, nbox_, height_, kept_, frontier_);
     }
     LB_TRY(hipGetLastError());
+    if (tm) LB_TRY(mark(6, stream));
     if (!pair_count) {                                // collapse_wide needs the count of this build's pairs
         if (!count_) LB_TRY(dalloc(count_, 1));
         pair_count = count_;
@@ -1238,28 +1290,34 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
     if (NI > 0) {
         bytes = tmp_bytes_;
         LB_TRY(rocprim::exclusive_scan(tmp_, bytes, kept_, pidx_, 0u, NI, rocprim::plus<uint32_t>(), stream));
+        if (tm) LB_TRY(mark(7, stream));
         hipLaunchKernelGGL(emit_kernel, dim3(blocks_for(NI)), dim3(BLOCK), 0, stream, segs_, seg_of_, v1_, box_, NI, child_,
                            range_, nbox_, kept_, pidx_, pairs, pair_count);
-    } else if (pair_count) {
-        LB_TRY(hipMemsetAsync(pair_count, 0, sizeof(uint32_t), stream));
+    } else {
+        if (pair_count) LB_TRY(hipMemsetAsync(pair_count, 0, sizeof(uint32_t), stream));
+        if (tm) LB_TRY(mark(7, stream));
     }
     hipLaunchKernelGGL(roots_kernel, dim3(blocks_for(n_segs_)), dim3(BLOCK), 0, stream, segs_, n_segs_, v1_, box_, nbox_,
                        height_, pidx_, roots);
-    return hipGetLastError();
+    LB_TRY(hipGetLastError());
+    return tm ? mark(8, stream) : hipSuccess;
 }
 
 hipError_t LbvhBuilder::collapse_wide(const NodePair *pairs, const TreeRoot *roots, NodeQuad *quads, TreeRoot *roots_wide,
                                       hipStream_t stream) {
+    const bool tm = box_ == own_box_;
     if (max_count_ > COLLAPSE_ALL_MIN && last_count_) {
         hipLaunchKernelGGL(collapse_all_kernel, dim3(blocks_for(max_pairs())), dim3(BLOCK), 0, stream, pairs, last_count_, quads);
         if (roots_wide)
             hipLaunchKernelGGL(copy_roots_kernel, dim3(blocks_for(n_segs_)), dim3(BLOCK), 0, stream, roots, n_segs_, roots_wide);
-        return hipGetLastError();
+        LB_TRY(hipGetLastError());
+        return tm ? mark(9, stream) : hipSuccess;
     }
     if (max_count_ - 1 > LDS_FRONT && !front_) LB_TRY(dalloc(front_, 2 * (size_t)max_pairs()));
     hipLaunchKernelGGL(collapse_wide_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, roots, pairs, quads, front_,
                        max_pairs(), roots_wide);
-    return hipGetLastError();
+    LB_TRY(hipGetLastError());
+    return tm ? mark(9, stream) : hipSuccess;
 }
 
 hipError_t LbvhBuilder::gather_items(uint32_t *slots, hipStream_t stream) {

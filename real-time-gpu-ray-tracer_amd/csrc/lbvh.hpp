@@ -118,6 +118,15 @@ public:
     // After build(): item index per leaf slot (TLAS: instance index per slot).
     hipError_t gather_items(uint32_t *slots, hipStream_t stream);
 
+    // Stage timing of a BLAS build (rt_api: option "timeline"): with timing on, prep_blas_items / build /
+    // collapse_wide record an event at the start and after each stage (STAGES: prep, bounds, morton, sort,
+    // karras + gather, bottom-up, scan, emit + roots, collapse); stage_ms() reads the last build's durations
+    // (after the stream has passed them).  Each record between two kernels idles the GPU ~5 us.
+    static constexpr int STAGES = 9;
+    static const char *const STAGE_NAMES[STAGES];
+    hipError_t set_timing(bool on);
+    hipError_t stage_ms(float (&ms)[STAGES]) const;
+
 private:
     uint32_t n_items_ = 0, n_segs_ = 0, max_count_ = 0;
     std::vector<std::pair<uint32_t, uint32_t>> big_segs_;   // {item_base, count} of trees sorted by rocPRIM
@@ -151,6 +160,9 @@ private:
     static constexpr uint32_t COLLAPSE_ALL_MIN = 65536;
     void *tmp_ = nullptr;
     size_t tmp_bytes_ = 0;
+    hipEvent_t stage_ev_[STAGES + 1] = {};
+    bool timing_ = false;
+    hipError_t mark(int k, hipStream_t stream) { return timing_ ? hipEventRecord(stage_ev_[k], stream) : hipSuccess; }
 };
 
 }  // namespace rtamd

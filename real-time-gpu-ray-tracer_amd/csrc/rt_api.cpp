@@ -641,8 +641,13 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
     s->stage_next = (si + 1) % s->stage_depth;
     if (s->r_staged[si]) RT_TRY(wait_event(s, s->r_staged[si]));   // no longer read by a pending copy
     if (!s->staging[si]) {
-        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->staging[si]), s->frame_block, hipHostMallocDefault));
-        HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s->staging_dev[si]), s->staging[si], 0));
+        // every buffer of the cycle at once, on the first frame that needs one: a pinned allocation inside a run of
+        // pipelined frames stalls the host's submission (one per frame for the first stage_depth frames)
+        for (int i = 0; i < s->stage_depth; i++) {
+            if (s->staging[i]) continue;
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s->staging[i]), s->frame_block, hipHostMallocDefault));
+            HIP_TRY(hipHostGetDevicePointer(reinterpret_cast<void **>(&s->staging_dev[i]), s->staging[i], 0));
+        }
     }
     s->update_wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count();
     if (s->update) {                                  // Renderer.cu:269
@@ -1033,6 +1038,7 @@ rt_status gpu_build_blas(rt_scene *s) {
         const RawPrimsGPU raw{s->raw_tris.p, s->raw_verts.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
         const PrimOutGPU out{sp.tri_hot.p, s->raw_shading() ? nullptr : sp.tri_cold.p, sp.sph_hot.p, sp.sph_cold.p,
                              sp.quad_hot.p, sp.quad_cold.p};
+        HIP_TRY(s->blas_builder->set_timing(s->timeline_on));      // option "timeline": stage events (debug_read)
         HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream, !out.tri_cold));
         HIP_TRY(s->blas_builder->build(sp.pairs.p, sp.roots.p, s->gpu_counts.p, s->stream, &raw, &out));   // + gather
         HIP_TRY(s->blas_builder->collapse_wide(sp.pairs.p, sp.roots.p, sp.quads.p, nullptr, s->stream));
@@ -1052,6 +1058,7 @@ rt_status gpu_build_blas(rt_scene *s) {
     const RawPrimsGPU raw{s->raw_tris.p, s->raw_verts.p, s->raw_sph.p, s->raw_quad.p, (uint32_t)s->roughs.size()};
     const PrimOutGPU out{s->tri_hot.p, s->raw_shading() ? nullptr : s->tri_cold.p, s->sph_hot.p, s->sph_cold.p,
                          s->quad_hot.p, s->quad_cold.p};
+    HIP_TRY(s->blas_builder->set_timing(s->timeline_on));      // option "timeline": stage events (debug_read)
     HIP_TRY(s->blas_builder->prep_blas_items(raw, s->stream, !out.tri_cold));
     HIP_TRY(s->blas_builder->build(s->blas_pairs.p, s->blas_roots.p, s->gpu_counts.p, s->stream, &raw, &out));   // + gather
     HIP_TRY(s->blas_builder->collapse_wide(s->blas_pairs.p, s->blas_roots.p, s->blas_quads.p, nullptr, s->stream));
@@ -2221,6 +2228,28 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
     const std::string k(name);
     const void *src = nullptr;
     size_t size = 0;
+    if (k == "rebuild_stages") {
+        // option "timeline" and RT_BUILD_LBVH: the last BLAS build's items, interior nodes, node pairs written, then
+        // the duration in ms of each LbvhBuilder stage (LbvhBuilder::STAGE_NAMES), as float64 (waits for the build)
+        if (!s->blas_builder) return fail(RT_ERR_STATE, "no GPU BLAS build (RT_BUILD_LBVH)");
+        constexpr int NS = LbvhBuilder::STAGES;
+        *bytes = (3 + NS) * sizeof(double);
+        if (!capacity) return RT_OK;
+        if (capacity < *bytes) return fail(RT_ERR_INVALID_ARGUMENT, "buffer too small");
+        HIP_TRY(hipSetDevice(s->device));
+        float ms[NS];
+        const hipError_t e = s->blas_builder->stage_ms(ms);
+        if (e != hipSuccess) return fail(RT_ERR_STATE, "no timed BLAS build: set option \"timeline\" before the frame");
+        uint32_t pairs = 0;
+        HIP_TRY(hipMemcpy(&pairs, s->gpu_counts.p, sizeof pairs, hipMemcpyDeviceToHost));
+        double v[3 + NS];
+        v[0] = s->blas_builder->items();
+        v[1] = s->blas_builder->max_pairs();
+        v[2] = pairs;
+        for (int j = 0; j < NS; j++) v[3 + j] = ms[j];
+        std::memcpy(dst, v, sizeof v);
+        return RT_OK;
+    }
     if (k == "timeline") {
         src = s->timeline.p;
         size = (size_t)s->timeline_waves * TIMELINE_WORDS * sizeof(uint64_t);
