@@ -136,7 +136,7 @@ struct DevBuf {
 // share one; lane q uses comm[q % ncomm] if "overlap" is raised after the attach (every rank issues the same
 // lane sequence, so a shared communicator still sees its operations in one order on every rank).
 struct CommState {
-    static constexpr int NLANE = 8;
+    static constexpr int NLANE = 8;        // = rt_scene::NLANE
     int rank = 0, world = 1;
     int ncomm = 1;
     uint32_t timeout_ms = 0;               // rt_comm_set_timeout: 0 = no deadline (async errors still polled)
@@ -170,7 +170,11 @@ struct rt_scene {
     std::vector<uint32_t> group_of; // per instance: its group + 1 (0: none)
     bool group_inst = true;         // option "group" (set before the build)
     bool lds_blas = true;           // fixed setting "lds_blas" (an option until round 5): with "lds_scene" 2, a group BLAS's top levels in LDS
-    uint32_t frame_items[8] = {};   // per frame block: TLAS items (= instance records when staged by slot)
+    // frame blocks (= NLANE, below).  Round 6 measured 12 and 16 lanes: 1/8 shares equal or slower (C2 0.0384-0.0388
+    // ms/frame at 8, 0.0394-0.0420 at 12, 0.0385-0.0392 at 16; C4 0.0465-0.0472 at 8, 0.0483-0.0499 at 16), the whole
+    // frame equal at 6 and 8 (profiles/r06/lanes/)
+    static constexpr int NBLOCK = 8;
+    uint32_t frame_items[NBLOCK] = {};   // per frame block: TLAS items (= instance records when staged by slot)
     Tree tlas;
     FlatTree tlas_flat;
     FlatWide tlas_wide;
@@ -220,14 +224,15 @@ struct rt_scene {
            off_tcent = 0, off_root_wide = 0, off_quads = 0, off_delta = 0, off_hot_s = 0, off_cold_s = 0;
     // frame blocks cycle through NLANE buffers, so "overlap" lanes never wait on each other's block
     static constexpr int NLANE = 8;
+    static_assert(NLANE == NBLOCK, "one frame block per lane");
     // GPU-built frames: per-instance parameters resident in HBM (instances.hip), one copy per frame block
     // (block b's at inst_params.p + b * records), so frames of different lanes update their records
     // concurrently; the host stages a delta (InstDelta at off_delta) only for the records whose transform
     // or local box changed since block b was last written: inst_dirty bit b (ALL_BLOCKS: every block)
     DevBuf<InstParams> inst_params;
-    std::vector<uint8_t> inst_dirty;
-    static constexpr uint8_t ALL_BLOCKS = 0xFF;
-    static_assert(NLANE <= 8, "inst_dirty holds one bit per frame block");
+    std::vector<uint16_t> inst_dirty;
+    static constexpr uint16_t ALL_BLOCKS = 0xFFFF;
+    static_assert(NLANE <= 16, "inst_dirty holds one bit per frame block");
     hipStream_t chain_stream[NLANE] = {};         // GPU-built frame b's records / TLAS were built on this stream
     hipEvent_t ev_blas_built = nullptr;           // the last GPU BLAS build on the scene stream finished
     hipEvent_t ev_caller = nullptr;               // rt_render with device outputs and no stream: the null stream's
@@ -239,8 +244,8 @@ struct rt_scene {
     // right after the copy kernel would idle the GPU ~5 us) — with one staging per block, the host waited for
     // frame k-8's whole trace before it could stage frame k (8 lanes of 1/8-frame shares: 0.12 ms lane gaps)
     // option "stage_depth" (default 2 x NLANE): buffers in the cycle, allocated on first use
-    static constexpr int NSTAGE = 8 * NLANE;
-    int stage_depth = 2 * NLANE;
+    static constexpr int NSTAGE = 64;
+    int stage_depth = 16;
     uint8_t *staging[NSTAGE] = {};
     uint8_t *staging_dev[NSTAGE] = {};            // the same, as device-visible pointers
     hipEvent_t r_staged[NSTAGE] = {};             // staging[i] no longer read (null: never used)
@@ -673,10 +678,10 @@ rt_status frame_update(rt_scene *s, uint64_t frame, hipStream_t upload, bool def
         // only the changed records cross PCIe: (index, shift, cos / sin of the angles, scale, local box, inactive)
         InstDelta *dl = reinterpret_cast<InstDelta *>(st + s->off_delta);
         uint32_t nd = 0;
-        const uint8_t bit = (uint8_t)(1u << b);
+        const uint16_t bit = (uint16_t)(1u << b);
         for (size_t i = 0; i < nrec; i++) {
             if (!(s->inst_dirty[i] & bit)) continue;
-            s->inst_dirty[i] &= (uint8_t)~bit;
+            s->inst_dirty[i] &= (uint16_t)~bit;
             const InstState &in = record_state(s, i);
             InstDelta &d = dl[nd++];
             std::memset(&d, 0, sizeof d);
@@ -1662,7 +1667,7 @@ rt_status rt_scene_detach_comm(rt_scene *s) {
 rt_status auto_lanes(rt_scene *s, const rt_render_opts &o) {
     const bool share = o.tile_count > 0 || (s->comm && s->comm->world > 1);
     const uint32_t L = s->rebuild_blas ? 2u : (share ? 8u : 4u);
-    const int depth = share ? rt_scene::NSTAGE : 2 * rt_scene::NLANE;
+    const int depth = share ? rt_scene::NSTAGE : 16;
     if (L == s->lanes && (s->stage_depth_set || depth == s->stage_depth)) return RT_OK;
     RT_TRY(drain(s));
     s->lanes = L;
