@@ -1094,6 +1094,7 @@ void LbvhBuilder::release() {
     for (hipEvent_t &e : stage_ev_)
         if (e) { (void)hipEventDestroy(e); e = nullptr; }
     timing_ = false;
+    last_timed_ = false;
     dfree(segs_); dfree(seg_of_); dfree(members_); dfree(item_member_); dfree(own_box_); dfree(own_cent_); dfree(stage_); dfree(bounds_);
     dfree(k0_); dfree(k1_); dfree(v0_); dfree(v1_); dfree(child_); dfree(parent_); dfree(parent_leaf_);
     dfree(range_); dfree(flag_); dfree(height_); dfree(nbox_); dfree(kept_); dfree(pidx_); dfree(front_); dfree(count_); dfree(frontier_);
@@ -1157,6 +1158,7 @@ hipError_t LbvhBuilder::set_timing(bool on) {
 }
 
 hipError_t LbvhBuilder::stage_ms(float (&ms)[STAGES]) const {
+    if (!last_timed_) return hipErrorNotReady;          // the last build ran without timing: no stale figures
     for (int k = 0; k < STAGES; k++) {
         ms[k] = 0.0f;
         if (!stage_ev_[k] || !stage_ev_[k + 1]) return hipErrorInvalidValue;
@@ -1167,6 +1169,7 @@ hipError_t LbvhBuilder::stage_ms(float (&ms)[STAGES]) const {
 }
 
 hipError_t LbvhBuilder::prep_blas_items(const RawPrimsGPU &raw, hipStream_t stream, bool stage_hot) {
+    last_timed_ = timing_;
     LB_TRY(mark(0, stream));
     if (!own_box_) {
         LB_TRY(dalloc(own_box_, 6 * (size_t)n_items_));

@@ -162,6 +162,7 @@ private:
     size_t tmp_bytes_ = 0;
     hipEvent_t stage_ev_[STAGES + 1] = {};
     bool timing_ = false;
+    bool last_timed_ = false;             // the last BLAS build recorded its stage events (stage_ms reads them)
     hipError_t mark(int k, hipStream_t stream) { return timing_ ? hipEventRecord(stage_ev_[k], stream) : hipSuccess; }
 };
 
