@@ -211,22 +211,29 @@ rt_scene_lanes_max = 8                                     # rt.h: "overlap" lan
 # node / node pair of the forest; scratch and re-reads not counted), over the stage's HIP-event time in a rebuild alone
 # (option "timeline": events between the stages, rt_scene_debug_read "rebuild_stages").  N items (10 M triangles on
 # C5), NI = N - trees interior nodes, P node pairs written (interior nodes of > 4 items).
-REBUILD_STAGES = ("prep", "bounds", "morton", "sort", "karras_gather", "bottom_up", "scan", "emit_roots", "collapse")
+REBUILD_STAGES = ("prep", "bounds", "morton", "sort", "hierarchy_small", "hierarchy_large", "scan", "emit_roots",
+                  "collapse")
 
 
-def rebuild_bytes(N, NI, P):
+def rebuild_bytes(N, NI, P, NL, TL):
+    """Algorithmic bytes per builder stage (csrc/lbvh.hip) of a rebuild over N items, NI interior nodes, P node pairs,
+    NL of the items in TL large trees (> 2048 items: rocPRIM sort, hierarchy_chunk_kernel / hierarchy_top_kernel)."""
+    NS, NIL = N - NL, max(NL - TL, 0)
+    NIS = max(NI - NIL, 0)
     return {
         # 36 B vertices + segment id + group member read; 24 B box, 16 B centroid, 48 B TriHot staged (item order)
         "prep": N * (36 + 4 + 4 + 24 + 16 + 48),
         "bounds": N * (16 + 4),                                # centroid + segment id
         "morton": N * (16 + 4 + 4 + 4),                        # centroid + segment id in, key + item out
-        "sort": N * (4 + 4 * 16),                              # key histogram + 4 8-bit passes of (key, item) in / out
-        # sorted key + segment id + item id per item, child / range / flag / parent per interior node; the leaf-
-        # ordered gather: the staged 48 B record in, 48 B out
-        "karras_gather": N * (4 + 4 + 4 + 48 + 48) + NI * (8 + 8 + 4 + 8),
-        # per item: item box (24) by its id (4), segment id, parent; per node: children, range, parent in, box,
-        # height, kept flag out
-        "bottom_up": N * (24 + 4 + 4 + 4) + NI * (8 + 8 + 4 + 24 + 4 + 4),
+        # small trees: one LDS pass (key + item in and out); large: key histogram + three 10-bit passes
+        "sort": NS * 16 + NL * (4 + 3 * 16),
+        # small trees: Karras (sorted key, segment id, item id; child / range / flag / parent per node), the leaf-
+        # ordered gather (staged 48 B record in, 48 B out), the LDS bottom-up (item box by id, parent per item; per node
+        # children, range, parent in, box, height, kept flag out)
+        "hierarchy_small": NS * (4 + 4 + 4 + 48 + 48 + 24 + 4 + 4) + NIS * (8 + 8 + 4 + 8 + 8 + 8 + 4 + 24 + 4 + 4),
+        # large trees, one bottom-up climb: sorted key, segment id, item id, item box (24) per item; children, range,
+        # box, height, kept flag out per node; the gather (staged 48 B record in, 48 B out)
+        "hierarchy_large": NL * (4 + 4 + 4 + 24 + 48 + 48) + NIL * (8 + 8 + 24 + 4 + 4),
         "scan": NI * 8,                                        # kept flags in, pair indices out
         # kept flag per node; per pair: children, range, segment, two child boxes, child pair indices, 64 B pair out
         "emit_roots": NI * 4 + P * (8 + 8 + 4 + 48 + 8 + 64),
@@ -248,13 +255,13 @@ def rebuild_roofline(r, frames):
     wall = (time.perf_counter() - t0) * 1e3 / len(frames)
     r.set_option("timeline", 0)
     a = np.mean(np.stack(rows), axis=0)
-    N, NI, P = int(a[0]), int(a[1]), int(round(a[2]))
-    ms = dict(zip(REBUILD_STAGES, a[3:].tolist()))
-    by = rebuild_bytes(N, NI, P)
+    N, NI, P, NL, TL = int(a[0]), int(a[1]), int(round(a[2])), int(a[3]), int(a[4])
+    ms = dict(zip(REBUILD_STAGES, a[5:].tolist()))
+    by = rebuild_bytes(N, NI, P, NL, TL)
     stages = {k: {"ms": round(ms[k], 4), "bytes": int(by[k]), "achieved_gbs": round(by[k] / (ms[k] * 1e-3) / 1e9, 1),
                   "frac": round(by[k] / (ms[k] * 1e-3) / 1e9 / HBM_PEAK_GBS, 3)} for k in REBUILD_STAGES}
     tot_ms, tot_b = float(sum(ms.values())), float(sum(by.values()))
-    return {"items": N, "interior_nodes": NI, "node_pairs": P, "updates": len(frames),
+    return {"items": N, "interior_nodes": NI, "node_pairs": P, "large_tree_items": NL, "updates": len(frames),
             "ms_stages_sum": round(tot_ms, 4), "ms_per_update_wall": round(wall, 4), "bytes": int(tot_b),
             "achieved_gbs": round(tot_b / (tot_ms * 1e-3) / 1e9, 1),
             "frac": round(tot_b / (tot_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 3), "peak_gbs": HBM_PEAK_GBS,

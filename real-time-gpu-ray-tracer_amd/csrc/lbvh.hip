@@ -263,6 +263,16 @@ __global__ void morton_kernel(const uint32_t *seg_of, const float4 *cent, uint32
 // one rocPRIM radix sort each over their 30- or 32-bit codes (LbvhBuilder::build).  A 64-bit (segment, code) key
 // over the whole forest cost C5 five 8-bit passes over 10 M 12-byte pairs per rebuild.
 constexpr uint32_t LOCAL_SORT_MAX = 2048;
+// The large trees' rocPRIM sort: onesweep over 10-bit digits (3 passes over a 30-bit code) instead of rocPRIM's gfx950
+// default of 8 (4 passes).  Measured on 10 M clustered Morton pairs (scripts/sort_bench.hip, profiles/r06/sort/):
+// 0.404 -> 0.279 ms per sort; 9 bits 0.401, 11 bits 0.376, 10 bits over 512 x 16 or 1024 x 24 items 0.33 / 0.35.
+#ifndef LBVH_SORT_BITS
+#define LBVH_SORT_BITS 10
+#endif
+using BigSortConfig = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, LBVH_SORT_BITS,
+                                        rocprim::block_radix_rank_algorithm::match>>;
 __global__ __launch_bounds__(BLOCK) void local_sort_kernel(const LbvhSeg *segs, const uint32_t *keys_in, uint32_t *keys_out,
                                                            uint32_t *vals_out) {
     __shared__ unsigned long long sk[LOCAL_SORT_MAX];
@@ -366,12 +376,18 @@ __device__ __forceinline__ void gather_item(const LbvhSeg &S, uint32_t p, const 
 // within KWIN positions of the workgroup's own are staged in LDS first: nearly every node's searches stay inside
 // that window (a range of <= KWIN / 2 items), so a search step is an LDS read, not a dependent global load.
 constexpr int KWIN = 256;
+constexpr uint32_t LOCAL_MAX = 2048;    // trees of <= LOCAL_MAX items: bottom_up_local_kernel (one workgroup, LDS)
 __global__ __launch_bounds__(BLOCK) void karras_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *keys,
                                                        uint32_t n, uint32_t *child, uint32_t *parent, uint32_t *parent_leaf,
                                                        uint32_t *range, uint32_t *flag, const uint32_t *vals, RawPrimsGPU raw,
                                                        PrimOutGPU out, const uint32_t *item_member, const TriHot *stage,
-                                                       uint32_t gather) {
+                                                       uint32_t gather, uint32_t small_only) {
     __shared__ uint32_t skey[BLOCK + 2 * KWIN];
+    if (small_only) {               // trees of > LOCAL_MAX items: hierarchy_chunk_kernel (block-uniform exit)
+        const uint32_t p0 = blockIdx.x * BLOCK, p1 = min(p0 + BLOCK, n) - 1u;
+        const uint32_t s0 = seg_of[p0];
+        if (s0 == seg_of[p1] && segs[s0].count > LOCAL_MAX) return;
+    }
     const int64_t w0 = (int64_t)blockIdx.x * BLOCK - KWIN;       // position of skey[0]
     for (int k = threadIdx.x; k < BLOCK + 2 * KWIN; k += BLOCK) {
         const int64_t q = w0 + k;
@@ -381,6 +397,7 @@ __global__ __launch_bounds__(BLOCK) void karras_kernel(const LbvhSeg *segs, cons
     const uint32_t p = blockIdx.x * BLOCK + threadIdx.x;
     if (p >= n) return;
     const LbvhSeg S = segs[seg_of[p]];
+    if (small_only && S.count > LOCAL_MAX) return;
     // fused BLAS gather (build() with raw / out): item p's leaf-ordered record; its loads overlap the searches below
     if (gather) gather_item(S, p, vals, raw, out, item_member, stage);
     const int m = (int)S.count;
@@ -432,16 +449,14 @@ __global__ __launch_bounds__(BLOCK) void karras_kernel(const LbvhSeg *segs, cons
 // Each leaf climbs; the second thread to reach a node finishes it (union of the two child boxes,
 // height) and climbs on.  Trees of <= LOCAL_MAX items (every particle BLAS, small TLASes) are
 // finished by one workgroup with node boxes and arrival counters in LDS, so the hand-off between
-// the two arriving threads is a workgroup-scope one.  Larger trees use the device-wide kernel, where
-// the two threads may sit on different XCDs (per-XCD L2s are not coherent): the finished node is
-// published with write-through (sc1) stores, drained (s_waitcnt vmcnt(0)) before the arrival
-// counter's agent-scope add, and the second arriver reads it with sc1 loads — no __threadfence()
-// (an L2 writeback + invalidate per step, MI355X_MICROARCH.md § visibility).
-constexpr uint32_t LOCAL_MAX = 2048;
-
+// the two arriving threads is a workgroup-scope one.  Larger trees end in a device-wide pass
+// (hierarchy_top_kernel), where the two threads may sit on different XCDs (per-XCD L2s are not
+// coherent): the finished node is published with write-through (sc1) stores, drained (s_waitcnt
+// vmcnt(0)) before the arrival's agent-scope atomic, and the second arriver reads it with sc1
+// loads — no __threadfence() (an L2 writeback + invalidate per step, MI355X_MICROARCH.md § visibility).
 __device__ __forceinline__ void union_children(const uint32_t *child, uint32_t g, const uint32_t *vals, const float *item_box,
                                                float *b, uint32_t &h, const float *node_box_lds, const uint32_t *height_lds,
-                                               uint32_t node_base, bool sc1) {
+                                               uint32_t node_base) {
     h = 0;
 #pragma unroll
     for (int c = 0; c < 2; c++) {
@@ -452,20 +467,11 @@ __device__ __forceinline__ void union_children(const uint32_t *child, uint32_t g
             const float2 *src = reinterpret_cast<const float2 *>(item_box + 6 * (size_t)vals[ch & ~LEAF_BIT]);
 #pragma unroll
             for (int k = 0; k < 3; k++) { const float2 v = src[k]; cb[2 * k] = v.x; cb[2 * k + 1] = v.y; }
-        } else if (!sc1) {
+        } else {
             const uint32_t l = ch - node_base;
 #pragma unroll
             for (int k = 0; k < 6; k++) cb[k] = node_box_lds[6 * l + k];
             chh = height_lds[l];
-        } else {
-            const unsigned long long *src = reinterpret_cast<const unsigned long long *>(node_box_lds + 6 * (size_t)ch);
-#pragma unroll
-            for (int k = 0; k < 3; k++) {
-                const unsigned long long v = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                cb[2 * k] = __uint_as_float((uint32_t)v);
-                cb[2 * k + 1] = __uint_as_float((uint32_t)(v >> 32));
-            }
-            chh = __hip_atomic_load(height_lds + ch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (c == 0) {
 #pragma unroll
@@ -498,7 +504,7 @@ __global__ __launch_bounds__(BLOCK) void bottom_up_local_kernel(const LbvhSeg *s
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             float b[6];
             uint32_t h;
-            union_children(child, g, vals, item_box, b, h, sbox, sheight, S.node_base, false);
+            union_children(child, g, vals, item_box, b, h, sbox, sheight, S.node_base);
             const uint32_t size = range[2 * g + 1] - range[2 * g] + 1u;
 #pragma unroll
             for (int k = 0; k < 6; k++) sbox[6 * l + k] = b[k];
@@ -516,88 +522,94 @@ __global__ __launch_bounds__(BLOCK) void bottom_up_local_kernel(const LbvhSeg *s
     }
 }
 
-// Large trees (> LOCAL_MAX items, e.g. C5's 10 M-triangle group BLAS): one workgroup per CHUNK consecutive sorted
-// items finishes, through LDS, every node whose item range lies inside its chunk (a node's range holds its own
-// index, so it has an LDS slot there) — nearly all nodes; a thread whose climb reaches a node crossing a chunk
-// edge records that arrival, and a second kernel climbs from each recorded arrival with the device-wide hand-off
-// described above (kernel boundary: the chunk-finished boxes are visible to it).
-// (One device-wide pass over all 10 M nodes took 1.7 ms per C5 rebuild: every level an agent-scope round trip.)
+// Large trees (> LOCAL_MAX items, e.g. C5's 10 M-triangle group BLAS): hierarchy_chunk_kernel / hierarchy_top_kernel
+// below.  (One device-wide pass over all 10 M nodes took 1.7 ms per C5 rebuild: every level an agent-scope round trip;
+// rounds 3-5 ran karras_kernel over them and then a chunk climb over its parent arrays: 0.42 + 0.47 ms per C5 rebuild
+// against 0.78 for the two kernels below, gather included, profiles/r06/hierarchy/.)
 #ifndef LBVH_CHUNK
-#define LBVH_CHUNK 1024                         // round 6: 2048-item chunks (two items per thread, ~153 KB of LDS, one
-#endif                                          // workgroup per CU) made the C5 rebuild slower: 2.33 against 2.17 ms
+#define LBVH_CHUNK 1024                         // 2048-item chunks (~150 KB of LDS, one workgroup per CU): 2.33 against
+#endif                                          // 2.17 ms per C5 rebuild (round 6, Karras chunks); 512: equal, 256: +0.27 ms
+#ifndef LBVH_TOP_BLOCKS
+#define LBVH_TOP_BLOCKS 4096                    // hierarchy_top_kernel's grid (its gather wants the waves; 256: +0.2 ms)
+#endif
 constexpr uint32_t CHUNK = LBVH_CHUNK;         // sorted items per workgroup
-constexpr uint32_t CHUNK_THREADS = 1024;       // the chunk kernel's workgroup: CHUNK / CHUNK_THREADS items per thread
+constexpr uint32_t CHUNK_THREADS = CHUNK < 1024 ? CHUNK : 1024;   // the chunk kernel's workgroup: CHUNK / CHUNK_THREADS items per thread
 constexpr uint32_t CHUNK_PER = CHUNK / CHUNK_THREADS;
 static_assert(CHUNK % CHUNK_THREADS == 0, "whole items per thread");
-__device__ __forceinline__ bool chunk_local(const uint32_t *range, uint32_t g) {
-    return range[2 * g] / CHUNK == range[2 * g + 1] / CHUNK;
+
+// ---- large trees without the Karras pass: hierarchy and boxes in one bottom-up climb ------------------------------
+// Apetrei, "Fast and Simple Agglomerative LBVH Construction" (CGVC 2014): over the sorted codes, a finished node
+// [l, r] is its parent's LEFT child iff l == 0 or (r != m - 1 and δ(r, r + 1) > δ(l - 1, l)) — the parent takes the
+// neighbour sharing the longer prefix (δ as karras_kernel's: code prefix, then the position's, so no two adjacent δ
+// are equal) — and the parent's split lies at r (left child) or l - 1 (right child).  That is the same binary radix
+// tree Karras' per-node searches build, and the Karras index of every node follows from it locally: a left child's
+// index is its last position, a right child's its first (the root's is 0), and the children of the node split at γ
+// are Karras nodes / leaves γ and γ + 1.  So each leaf climbs, the second arrival at a split finishes the parent
+// (range, children, box, height) and writes it at its Karras index: the arrays karras_kernel + a climb over its parent
+// arrays produce, bit for bit, without the searches, the parent arrays or a second pass over the chunk (tests/test_gpu_lbvh.py
+// compares every node with the restatement).  Arrival bits per split: 1 / 2 = the left / right child arrived, 4 / 8 =
+// that child is a leaf.
+struct SegKeys {
+    const uint32_t *keys;       // sorted codes (global)
+    const uint32_t *skey;       // staged codes at positions w0 .. w0 + wn - 1 (LDS), or null
+    int64_t w0;
+    int wn;
+    uint32_t base;              // the segment's first sorted position
+    int m;                      // the segment's items
+};
+__device__ __forceinline__ uint32_t seg_key(const SegKeys &K, int a) {
+    const int64_t pos = (int64_t)K.base + a, o = pos - K.w0;
+    return (o >= 0 && o < K.wn) ? K.skey[o] : K.keys[pos];
+}
+__device__ __forceinline__ int seg_delta(const SegKeys &K, int a, int b) {      // 0 <= a < m
+    if (b < 0 || b >= K.m) return -1;
+    const uint32_t ka = seg_key(K, a), kb = seg_key(K, b);
+    if (ka != kb) return __clz(ka ^ kb);
+    return 32 + __clz((uint32_t)a ^ (uint32_t)b);
+}
+__device__ __forceinline__ bool left_child(const SegKeys &K, int l, int r) {
+    return l == 0 || (r != K.m - 1 && seg_delta(K, r, r + 1) > seg_delta(K, l - 1, l));
 }
 
-// device-wide climb from node g (its range crosses a chunk edge): the hand-off described above
-__device__ __forceinline__ void climb_top(const LbvhSeg &S, uint32_t g, const uint32_t *vals, const float *item_box,
-                                          const uint32_t *child, const uint32_t *parent, const uint32_t *range,
-                                          uint32_t *flag, float *nbox, uint32_t *height, uint32_t *kept) {
-    while (g != NONE) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");              // this lane's sc1 stores have landed
-        if (atomicAdd(&flag[g], 1u) == 0u) return;
-        float b[6];
-        uint32_t h;
-        union_children(child, g, vals, item_box, b, h, nbox, height, 0, true);
-        unsigned long long *dst = reinterpret_cast<unsigned long long *>(nbox + 6 * (size_t)g);
-#pragma unroll
-        for (int k = 0; k < 3; k++)
-            __hip_atomic_store(dst + k, (unsigned long long)__float_as_uint(b[2 * k]) |
-                                            ((unsigned long long)__float_as_uint(b[2 * k + 1]) << 32),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint32_t size = range[2 * g + 1] - range[2 * g] + 1u;
-        const bool keep = size > S.leaf_cap;
-        __hip_atomic_store(height + g, keep ? h + 1u : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        kept[g] = keep ? 1u : 0u;
-        g = parent[g];
-    }
-}
-
-// The chunk's own nodes (the interior node at each of its positions: child refs, item range, parent) are staged
-// in LDS with coalesced loads before the climbs, so a climb step waits on LDS only (reading them from HBM / L2 per
-// step made every level a dependent global round trip: 0.64 ms per C5 rebuild).  LBVH_CHUNK = 2048 (two items per
-// thread) halves the chunk edges and the top pass's device-wide climbs, but was measured slower (above).
-__global__ __launch_bounds__(CHUNK_THREADS) void bottom_up_chunk_kernel(const LbvhSeg *segs, const uint32_t *seg_of,
-                                                                        const uint32_t *vals, const float *item_box,
-                                                                        uint32_t n, const uint32_t *child,
-                                                                        const uint32_t *parent, const uint32_t *parent_leaf,
-                                                                        const uint32_t *range, float *nbox, uint32_t *height,
+// Chunk pass: one workgroup per CHUNK sorted positions finishes every node whose range lies inside the chunk (LDS
+// arrivals, node records at their Karras index in LDS), and also writes the chunk's leaf-ordered primitive records
+// (karras_kernel's fused gather).  A climb whose parent split has a child outside the chunk, and every split that got
+// only one of its arrivals here, go to the top pass as (split, bits) arrivals.
+__global__ __launch_bounds__(CHUNK_THREADS) void hierarchy_chunk_kernel(const LbvhSeg *segs, const uint32_t *seg_of,
+                                                                        const uint32_t *keys, const uint32_t *vals,
+                                                                        const float *item_box, uint32_t n, uint32_t *child,
+                                                                        uint32_t *range, float *nbox, uint32_t *height,
                                                                         uint32_t *kept, uint32_t *frontier) {
+    __shared__ uint32_t skey[CHUNK + 2];        // codes at positions lo - 1 .. lo + CHUNK
     __shared__ float sleaf[CHUNK * 6];          // the chunk's item boxes, in sorted order
-    __shared__ float sbox[CHUNK * 6];           // node boxes, at the node's own position
+    __shared__ float sbox[CHUNK * 6];           // node boxes, at the node's Karras index
     __shared__ uint32_t sheight[CHUNK];
-    __shared__ uint32_t sflag[CHUNK];
-    __shared__ uint2 schild[CHUNK], srange[CHUNK];   // the interior node at each position (segment's last: unused)
-    __shared__ uint32_t sparent[CHUNK];
-    constexpr uint32_t FRONT_LDS = 256;         // this chunk's arrivals for the top pass (~20 typical; more go direct)
-    __shared__ uint32_t sfront[FRONT_LDS];
+    __shared__ uint2 srl[CHUNK];                // node range (segment-local first, last); x = NONE: not finished here
+    __shared__ uint32_t ssplit[CHUNK];          // node split (segment-local)
+    __shared__ uint32_t sarr[CHUNK];            // arrival bits per split position
+    constexpr uint32_t FRONT_LDS = 256;         // this chunk's arrivals for the top pass (more go direct)
+    __shared__ uint2 sfront[FRONT_LDS];
     __shared__ uint32_t sfront_n, sfront_at;
     const uint32_t lo = blockIdx.x * CHUNK;
-    for (uint32_t j = 0; j < CHUNK_PER; j++) sflag[threadIdx.x + j * CHUNK_THREADS] = 0;
     if (threadIdx.x == 0) sfront_n = 0;
-    uint32_t seg[CHUNK_PER];
+    for (uint32_t k = threadIdx.x; k < CHUNK + 2; k += CHUNK_THREADS) {
+        const int64_t q = (int64_t)lo - 1 + k;
+        skey[k] = (q >= 0 && q < (int64_t)n) ? keys[q] : 0u;
+    }
     bool big[CHUNK_PER];
     LbvhSeg S[CHUNK_PER];
 #pragma unroll
     for (uint32_t j = 0; j < CHUNK_PER; j++) {
         const uint32_t l = threadIdx.x + j * CHUNK_THREADS, p = lo + l;
-        seg[j] = p < n ? seg_of[p] : NONE;
-        big[j] = seg[j] != NONE && segs[seg[j]].count > LOCAL_MAX;   // else bottom_up_local_kernel
+        sarr[l] = 0;
+        srl[l].x = NONE;
+        const uint32_t seg = p < n ? seg_of[p] : NONE;
+        big[j] = seg != NONE && segs[seg].count > LOCAL_MAX;   // else karras_kernel + bottom_up_local_kernel
         if (big[j]) {
-            S[j] = segs[seg[j]];
+            S[j] = segs[seg];
             const float2 *src = reinterpret_cast<const float2 *>(item_box + 6 * (size_t)vals[p]);
 #pragma unroll
             for (int k = 0; k < 3; k++) { const float2 v = src[k]; sleaf[6 * l + 2 * k] = v.x; sleaf[6 * l + 2 * k + 1] = v.y; }
-            if (p - S[j].item_base + 1u < S[j].count) {
-                const uint32_t g = S[j].node_base + (p - S[j].item_base);
-                schild[l] = reinterpret_cast<const uint2 *>(child)[g];
-                srange[l] = reinterpret_cast<const uint2 *>(range)[g];
-                sparent[l] = parent[g];
-            }
         }
     }
     __syncthreads();
@@ -605,85 +617,187 @@ __global__ __launch_bounds__(CHUNK_THREADS) void bottom_up_chunk_kernel(const Lb
         if (!big[j]) continue;
         const uint32_t p = lo + threadIdx.x + j * CHUNK_THREADS;
         const LbvhSeg &Sj = S[j];
-        uint32_t g = parent_leaf[p];
-        bool first = false;                             // stopped as a node's first arrival
-        while (g != NONE) {
-            const uint32_t l = Sj.item_base + (g - Sj.node_base) - lo;   // the node's own position, if in this chunk
-            if (l >= CHUNK) break;                                       // its range leaves the chunk
-            const uint2 rg = srange[l];
-            if (rg.x / CHUNK != rg.y / CHUNK) break;                     // the same
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-            if (atomicAdd(&sflag[l], 1u) == 0u) { first = true; break; }
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-            float b[6];
-            uint32_t h = 0;
-            const uint2 cc = schild[l];
-#pragma unroll
-            for (int c = 0; c < 2; c++) {                                // union_children's order
-                const uint32_t ch = c == 0 ? cc.x : cc.y;
-                const float *cb;
-                uint32_t chh = 0;
-                if (ch & LEAF_BIT) {                                     // sorted position = the leaf's item index
-                    cb = sleaf + 6 * ((ch & ~LEAF_BIT) - lo);
-                } else {                                                 // inside the parent's range: this chunk
-                    const uint32_t lc = Sj.item_base + (ch - Sj.node_base) - lo;
-                    cb = sbox + 6 * lc;
-                    chh = sheight[lc];
+        const SegKeys K = {keys, skey, (int64_t)lo - 1, (int)CHUNK + 2, Sj.item_base, (int)Sj.count};
+        int l = (int)(p - Sj.item_base), r = l;
+        bool leaf = true, left = left_child(K, l, r);
+        for (;;) {
+            const int gam = left ? r : l - 1;
+            const uint32_t P = Sj.item_base + (uint32_t)gam;       // the split: children at positions P, P + 1
+            const uint32_t bits = (left ? 1u : 2u) | (leaf ? (left ? 4u : 8u) : 0u);
+            if (P < lo || P + 1 >= lo + CHUNK) {                 // a child outside the chunk: the top pass's
+                const uint32_t k = atomicAdd(&sfront_n, 1u);
+                if (k < FRONT_LDS) sfront[k] = make_uint2(P, bits);
+                else {
+                    const uint32_t at = atomicAdd(frontier, 1u);
+                    frontier[1 + 2 * at] = P;
+                    frontier[2 + 2 * at] = bits;
                 }
-                if (c == 0) {
-#pragma unroll
-                    for (int k = 0; k < 6; k++) b[k] = cb[k];
-                } else {
-                    float t[6];
-#pragma unroll
-                    for (int k = 0; k < 6; k++) t[k] = cb[k];
-                    merge_into(b, t);
-                }
-                h = chh > h ? chh : h;
+                break;
             }
-            const uint32_t size = rg.y - rg.x + 1u;
+            const uint32_t sl = P - lo, sr = sl + 1;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            const uint32_t old = atomicOr(&sarr[sl], bits);
+            if (old == 0u) break;                                 // first arrival: the sibling finishes the parent
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const uint32_t a = old | bits;
+            const int lL = (a & 4u) ? gam : (int)srl[sl].x;
+            const int rR = (a & 8u) ? gam + 1 : (int)srl[sr].y;
+            const float *c0 = (a & 4u) ? sleaf + 6 * sl : sbox + 6 * sl;
+            const float *c1 = (a & 8u) ? sleaf + 6 * sr : sbox + 6 * sr;
+            float b[6], t[6];
 #pragma unroll
-            for (int k = 0; k < 6; k++) sbox[6 * l + k] = b[k];
-            sheight[l] = size > Sj.leaf_cap ? h + 1u : 0u;
-            g = sparent[l];
-        }
-        if (!first && g != NONE) {                      // g's range crosses a chunk edge: an arrival for the top pass
-            const uint32_t k = atomicAdd(&sfront_n, 1u);
-            if (k < FRONT_LDS) sfront[k] = g;
-            else frontier[1 + atomicAdd(frontier, 1u)] = g;
+            for (int k = 0; k < 6; k++) { b[k] = c0[k]; t[k] = c1[k]; }
+            merge_into(b, t);                                     // union_children's order
+            const uint32_t h0 = (a & 4u) ? 0u : sheight[sl], h1 = (a & 8u) ? 0u : sheight[sr];
+            const uint32_t h = h0 > h1 ? h0 : h1;
+            const bool root = lL == 0 && rR == (int)Sj.count - 1;
+            const bool nleft = !root && left_child(K, lL, rR);
+            const uint32_t slot = Sj.item_base + (uint32_t)(root ? 0 : (nleft ? rR : lL)) - lo;
+            const uint32_t size = (uint32_t)(rR - lL) + 1u;
+#pragma unroll
+            for (int k = 0; k < 6; k++) sbox[6 * slot + k] = b[k];
+            sheight[slot] = size > Sj.leaf_cap ? h + 1u : 0u;
+            ssplit[slot] = (uint32_t)gam;
+            srl[slot] = make_uint2((uint32_t)lL, (uint32_t)rR);
+            if (root) break;
+            l = lL; r = rR; leaf = false; left = nleft;
         }
     }
     __syncthreads();
-    // one global reservation per chunk (~20 arrivals each): a per-arrival atomic on the one frontier counter
-    // serialised ~200 k same-address atomics per C5 rebuild at the L2 (0.64 ms for the whole kernel)
-    const uint32_t nf = sfront_n < FRONT_LDS ? sfront_n : FRONT_LDS;
+    // splits that got one arrival here: the other child finishes in the top pass
+#pragma unroll
+    for (uint32_t j = 0; j < CHUNK_PER; j++) {
+        const uint32_t l = threadIdx.x + j * CHUNK_THREADS;
+        const uint32_t a = sarr[l];
+        if (a != 0u && (a & 3u) != 3u) {
+            const uint32_t k = atomicAdd(&sfront_n, 1u);
+            if (k < FRONT_LDS) sfront[k] = make_uint2(lo + l, a);
+            else {
+                const uint32_t at = atomicAdd(frontier, 1u);
+                frontier[1 + 2 * at] = lo + l;
+                frontier[2 + 2 * at] = a;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t nf = sfront_n < FRONT_LDS ? sfront_n : FRONT_LDS;   // one global reservation per chunk
     if (threadIdx.x == 0 && nf) sfront_at = atomicAdd(frontier, nf);
     __syncthreads();
-    if (threadIdx.x < nf) frontier[1 + sfront_at + threadIdx.x] = sfront[threadIdx.x];
+    if (threadIdx.x < nf) {
+        frontier[1 + 2 * (sfront_at + threadIdx.x)] = sfront[threadIdx.x].x;
+        frontier[2 + 2 * (sfront_at + threadIdx.x)] = sfront[threadIdx.x].y;
+    }
 #pragma unroll
     for (uint32_t j = 0; j < CHUNK_PER; j++) {
         const uint32_t l = threadIdx.x + j * CHUNK_THREADS, p = lo + l;
-        if (sflag[l] == 2u) {                                            // the node at this position finished here
-            const uint32_t g = S[j].node_base + (p - S[j].item_base);
-            const uint2 rg = srange[l];
+        const uint2 rl = srl[l];
+        if (big[j] && rl.x != NONE) {                         // the node at this Karras position finished here
+            const LbvhSeg &Sj = S[j];
+            const uint32_t g = Sj.node_base + (p - Sj.item_base), gam = ssplit[l];
+            child[2 * g] = rl.x == gam ? (LEAF_BIT | (Sj.item_base + gam)) : Sj.node_base + gam;
+            child[2 * g + 1] = rl.y == gam + 1 ? (LEAF_BIT | (Sj.item_base + gam + 1)) : Sj.node_base + gam + 1;
+            range[2 * g] = Sj.item_base + rl.x;
+            range[2 * g + 1] = Sj.item_base + rl.y;
 #pragma unroll
             for (int k = 0; k < 6; k++) nbox[6 * (size_t)g + k] = sbox[6 * l + k];
             height[g] = sheight[l];
-            kept[g] = (rg.y - rg.x + 1u) > S[j].leaf_cap ? 1u : 0u;
+            kept[g] = (rl.y - rl.x + 1u) > Sj.leaf_cap ? 1u : 0u;
         }
     }
 }
 
-// the top pass: one climb per arrival the chunk pass recorded (frontier[0] = count, then crossing-node ids)
-__global__ void bottom_up_top_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *vals,
-                                     const float *item_box, const uint32_t *child, const uint32_t *parent,
-                                     const uint32_t *range, uint32_t *flag, float *nbox, uint32_t *height, uint32_t *kept,
-                                     const uint32_t *frontier) {
+// Top pass: one climb per recorded arrival, device-wide, with the hand-off described above bottom_up_local_kernel (node records published
+// with write-through stores, drained before the arrival's agent-scope atomic, read with sc1 loads).  Arrival bits per
+// split in `flag` (indexed by split position); the second arrival clears them for the next build.
+__device__ __forceinline__ uint32_t ld_sc1(const uint32_t *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(uint32_t *p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void hierarchy_top_kernel(const LbvhSeg *segs, const uint32_t *seg_of, const uint32_t *keys, const uint32_t *vals,
+                                     const float *item_box, uint32_t *child, uint32_t *range, float *nbox, uint32_t *height,
+                                     uint32_t *kept, uint32_t *flag, const uint32_t *frontier, uint32_t n, RawPrimsGPU raw,
+                                     PrimOutGPU out, const uint32_t *item_member, const TriHot *stage, uint32_t gather) {
     const uint32_t count = frontier[0];
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < count; i += gridDim.x * BLOCK) {
-        const uint32_t g = frontier[1 + i];
-        climb_top(segs[seg_of[range[2 * g]]], g, vals, item_box, child, parent, range, flag, nbox, height, kept);
+        uint32_t P = frontier[1 + 2 * i], bits = frontier[2 + 2 * i];
+        const LbvhSeg S = segs[seg_of[P]];
+        const SegKeys K = {keys, nullptr, 0, 0, S.item_base, (int)S.count};
+        for (;;) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // this lane's sc1 stores have landed
+            const uint32_t old = atomicOr(&flag[P], bits);
+            if (old == 0u) break;
+            flag[P] = 0u;                                              // no other arrival at P in this build
+            const uint32_t a = old | bits;
+            const int gam = (int)(P - S.item_base);
+            const uint32_t g0 = S.node_base + (uint32_t)gam, g1 = g0 + 1u;
+            float b[6], t[6];
+            uint32_t h = 0;
+            int lL, rR;
+            if (a & 4u) {
+                lL = gam;
+                const float *src = item_box + 6 * (size_t)vals[P];
+#pragma unroll
+                for (int k = 0; k < 6; k++) b[k] = src[k];
+            } else {
+                lL = (int)(ld_sc1(range + 2 * (size_t)g0) - S.item_base);
+                const unsigned long long *src = reinterpret_cast<const unsigned long long *>(nbox + 6 * (size_t)g0);
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const unsigned long long v = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    b[2 * k] = __uint_as_float((uint32_t)v);
+                    b[2 * k + 1] = __uint_as_float((uint32_t)(v >> 32));
+                }
+                h = ld_sc1(height + g0);
+            }
+            if (a & 8u) {
+                rR = gam + 1;
+                const float *src = item_box + 6 * (size_t)vals[P + 1];
+#pragma unroll
+                for (int k = 0; k < 6; k++) t[k] = src[k];
+            } else {
+                rR = (int)(ld_sc1(range + 2 * (size_t)g1 + 1) - S.item_base);
+                const unsigned long long *src = reinterpret_cast<const unsigned long long *>(nbox + 6 * (size_t)g1);
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const unsigned long long v = __hip_atomic_load(src + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    t[2 * k] = __uint_as_float((uint32_t)v);
+                    t[2 * k + 1] = __uint_as_float((uint32_t)(v >> 32));
+                }
+                const uint32_t h1 = ld_sc1(height + g1);
+                h = h1 > h ? h1 : h;
+            }
+            merge_into(b, t);
+            const bool root = lL == 0 && rR == (int)S.count - 1;
+            const bool nleft = !root && left_child(K, lL, rR);
+            const uint32_t g = S.node_base + (uint32_t)(root ? 0 : (nleft ? rR : lL));
+            const uint32_t size = (uint32_t)(rR - lL) + 1u;
+            const bool keep = size > S.leaf_cap;
+            unsigned long long *dst = reinterpret_cast<unsigned long long *>(nbox + 6 * (size_t)g);
+#pragma unroll
+            for (int k = 0; k < 3; k++)
+                __hip_atomic_store(dst + k, (unsigned long long)__float_as_uint(b[2 * k]) |
+                                                ((unsigned long long)__float_as_uint(b[2 * k + 1]) << 32),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            st_sc1(height + g, keep ? h + 1u : 0u);
+            st_sc1(range + 2 * (size_t)g, S.item_base + (uint32_t)lL);
+            st_sc1(range + 2 * (size_t)g + 1, S.item_base + (uint32_t)rR);
+            child[2 * (size_t)g] = (a & 4u) ? (LEAF_BIT | P) : g0;
+            child[2 * (size_t)g + 1] = (a & 8u) ? (LEAF_BIT | (P + 1u)) : g1;
+            kept[g] = keep ? 1u : 0u;
+            if (root) break;
+            P = S.item_base + (uint32_t)(nleft ? rR : lL - 1);
+            bits = nleft ? 1u : 2u;
+        }
     }
+    // the large trees' leaf-ordered primitive records (karras_kernel's fused gather for the small ones): bandwidth
+    // work that fills the issue slots the climbs above leave idle while they wait on their hand-offs
+    if (gather)
+        for (uint32_t p = blockIdx.x * BLOCK + threadIdx.x; p < n; p += gridDim.x * BLOCK) {
+            const LbvhSeg S = segs[seg_of[p]];
+            if (S.count > LOCAL_MAX) gather_item(S, p, vals, raw, out, item_member, stage);
+        }
 }
 
 struct ChildInfo { uint32_t ref; const float *box; };
@@ -1133,21 +1247,23 @@ hipError_t LbvhBuilder::init(const std::vector<LbvhSeg> &segs, hipStream_t strea
     LB_TRY(dalloc(bounds_, 6 * (size_t)n_segs_));
     LB_TRY(dalloc(k0_, N)); LB_TRY(dalloc(k1_, N)); LB_TRY(dalloc(v0_, N)); LB_TRY(dalloc(v1_, N));
     LB_TRY(dalloc(child_, 2 * NI)); LB_TRY(dalloc(parent_, NI)); LB_TRY(dalloc(parent_leaf_, N));
-    LB_TRY(dalloc(range_, 2 * NI)); LB_TRY(dalloc(flag_, NI)); LB_TRY(dalloc(height_, NI));
+    LB_TRY(dalloc(range_, 2 * NI)); LB_TRY(dalloc(flag_, N)); LB_TRY(dalloc(height_, NI));
     LB_TRY(dalloc(nbox_, 6 * NI)); LB_TRY(dalloc(kept_, NI)); LB_TRY(dalloc(pidx_, NI));
     size_t sort_bytes = 0, scan_bytes = 0;
-    if (big_max) LB_TRY(rocprim::radix_sort_pairs(nullptr, sort_bytes, k0_, k1_, v0_, v1_, big_max, 0, 32, stream));
+    if (big_max) LB_TRY(rocprim::radix_sort_pairs<BigSortConfig>(nullptr, sort_bytes, k0_, k1_, v0_, v1_, big_max, 0, 32, stream));
     LB_TRY(rocprim::exclusive_scan(nullptr, scan_bytes, kept_, pidx_, 0u, NI, rocprim::plus<uint32_t>(), stream));
     tmp_bytes_ = sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
     LB_TRY(hipMalloc(&tmp_, tmp_bytes_ ? tmp_bytes_ : 1));
     // kept/pidx of nodes that no thread visits (none in a valid forest) start defined
     LB_TRY(hipMemsetAsync(kept_, 0, NI * sizeof(uint32_t), stream));
+    // arrival bits of the top pass (hierarchy_top_kernel clears what it sets)
+    LB_TRY(hipMemsetAsync(flag_, 0, N * sizeof(uint32_t), stream));
     // synchronous: seg_of (host vector) must outlive the copy
     return hipStreamSynchronize(stream);
 }
 
 const char *const LbvhBuilder::STAGE_NAMES[LbvhBuilder::STAGES] = {
-    "prep", "bounds", "morton", "sort", "karras_gather", "bottom_up", "scan", "emit_roots", "collapse"};
+    "prep", "bounds", "morton", "sort", "hierarchy_small", "hierarchy_large", "scan", "emit_roots", "collapse"};
 
 hipError_t LbvhBuilder::set_timing(bool on) {
     if (on)
@@ -1224,13 +1340,13 @@ size_t LbvhBuilder::workspace_bytes() const {
     if (!segs_) return 0;
     const size_t N = n_items_, NI = max_pairs(), u = sizeof(uint32_t);
     size_t b = n_segs_ * sizeof(LbvhSeg) + N * u /*seg_of*/ + 6 * (size_t)n_segs_ * u /*bounds*/ + 4 * N * u /*keys, values*/ +
-               N * u /*parent_leaf*/ + NI * (2 + 1 + 2 + 1 + 1 + 6 + 1 + 1) * u /*child parent range flag height nbox kept pidx*/ +
+               N * u /*parent_leaf*/ + N * u /*flag*/ + NI * (2 + 1 + 2 + 1 + 6 + 1 + 1) * u /*child parent range height nbox kept pidx*/ +
                tmp_bytes_;
     if (own_box_) b += 6 * N * sizeof(float) + N * sizeof(float4);
     if (stage_) b += N * sizeof(TriHot);
     if (members_) b += members_n_ * u;
     if (item_member_) b += N * u;
-    if (frontier_) b += (1 + 2 * NI) * u;
+    if (frontier_) b += (1 + 2 * N) * u;
     if (front_) b += 2 * (size_t)max_pairs() * u;
     if (count_) b += u;
     return b;
@@ -1264,25 +1380,31 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
     const int end_bit = box_ == own_box_ ? 30 : 32;
     for (const auto &b : big_segs_) {
         bytes = tmp_bytes_;
-        LB_TRY(rocprim::radix_sort_pairs(tmp_, bytes, k0_ + b.first, k1_ + b.first, v0_ + b.first, v1_ + b.first, b.second, 0,
+        LB_TRY(rocprim::radix_sort_pairs<BigSortConfig>(tmp_, bytes, k0_ + b.first, k1_ + b.first, v0_ + b.first, v1_ + b.first, b.second, 0,
                                          end_bit, stream));
     }
     if (tm) LB_TRY(mark(4, stream));
+    // trees of > LOCAL_MAX items: hierarchy_chunk_kernel / hierarchy_top_kernel build them (and gather their records)
+    const bool fused = max_count_ > LOCAL_MAX;
+    const RawPrimsGPU graw = raw ? *raw : RawPrimsGPU{};
+    const PrimOutGPU gout = out ? *out : PrimOutGPU{};
+    const TriHot *gstage = stage_ready_ ? stage_ : nullptr;
     hipLaunchKernelGGL(karras_kernel, dim3(blocks_for(N)), dim3(BLOCK), 0, stream, segs_, seg_of_, k1_, N, child_, parent_,
-                       parent_leaf_, range_, flag_, v1_, raw ? *raw : RawPrimsGPU{}, out ? *out : PrimOutGPU{}, item_member_,
-                       stage_ready_ ? stage_ : nullptr, (uint32_t)(raw && out));
-    stage_ready_ = false;
-    if (tm) LB_TRY(mark(5, stream));
+                       parent_leaf_, range_, flag_, v1_, graw, gout, item_member_, gstage, (uint32_t)(raw && out),
+                       (uint32_t)fused);
     hipLaunchKernelGGL(bottom_up_local_kernel, dim3(n_segs_), dim3(BLOCK), 0, stream, segs_, v1_, box_, child_, parent_,
                        parent_leaf_, range_, nbox_, height_, kept_);
-    if (max_count_ > LOCAL_MAX) {
-        if (!frontier_) LB_TRY(dalloc(frontier_, 1 + 2 * (size_t)NI));   // <= 2 arrivals per internal node
+    if (tm) LB_TRY(mark(5, stream));
+    if (fused) {
+        if (!frontier_) LB_TRY(dalloc(frontier_, 1 + 2 * (size_t)N));    // <= 1 (split, bits) arrival per item
         LB_TRY(hipMemsetAsync(frontier_, 0, sizeof(uint32_t), stream));
-        hipLaunchKernelGGL(bottom_up_chunk_kernel, dim3((N + CHUNK - 1) / CHUNK), dim3(CHUNK_THREADS), 0, stream, segs_, seg_of_, v1_,
-                           box_, N, child_, parent_, parent_leaf_, range_, nbox_, height_, kept_, frontier_);
-        hipLaunchKernelGGL(bottom_up_top_kernel, dim3(256), dim3(BLOCK), 0, stream, segs_, seg_of_, v1_, box_, child_, parent_,
-                           range_, flag_, nbox_, height_, kept_, frontier_);
+        hipLaunchKernelGGL(hierarchy_chunk_kernel, dim3((N + CHUNK - 1) / CHUNK), dim3(CHUNK_THREADS), 0, stream, segs_, seg_of_,
+                           k1_, v1_, box_, N, child_, range_, nbox_, height_, kept_, frontier_);
+        hipLaunchKernelGGL(hierarchy_top_kernel, dim3(LBVH_TOP_BLOCKS), dim3(BLOCK), 0, stream, segs_, seg_of_, k1_, v1_, box_, child_,
+                           range_, nbox_, height_, kept_, flag_, frontier_, N, graw, gout, item_member_, gstage,
+                           (uint32_t)(raw && out));
     }
+    stage_ready_ = false;
     LB_TRY(hipGetLastError());
     if (tm) LB_TRY(mark(6, stream));
     if (!pair_count) {                                // collapse_wide needs the count of this build's pairs

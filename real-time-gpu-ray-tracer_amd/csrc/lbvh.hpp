@@ -89,6 +89,10 @@ public:
     uint32_t items() const { return n_items_; }
     uint32_t segments() const { return n_segs_; }
     uint32_t max_pairs() const { return n_items_ > n_segs_ ? n_items_ - n_segs_ : 1u; }
+    // items in trees of more than 2048 items (the rocPRIM sort, hierarchy_chunk_kernel / hierarchy_top_kernel) and
+    // those trees' count: the stage byte model of bench.py's rebuild roofline
+    uint32_t large_items() const { uint32_t c = 0; for (const auto &b : big_segs_) c += b.second; return c; }
+    uint32_t large_trees() const { return (uint32_t)big_segs_.size(); }
     // device bytes the builder's workspace holds now (sort keys, hierarchy, staged records, rocPRIM scratch, ...):
     // part of rt_scene_info::device_bytes
     size_t workspace_bytes() const;
@@ -120,7 +124,8 @@ public:
 
     // Stage timing of a BLAS build (rt_api: option "timeline"): with timing on, prep_blas_items / build /
     // collapse_wide record an event at the start and after each stage (STAGES: prep, bounds, morton, sort,
-    // karras + gather, bottom-up, scan, emit + roots, collapse); stage_ms() reads the last build's durations
+    // hierarchy of the small trees (Karras + gather, bottom-up), hierarchy of the large trees (chunk + top pass +
+    // gather), scan, emit + roots, collapse); stage_ms() reads the last build's durations
     // (after the stream has passed them).  Each record between two kernels idles the GPU ~5 us.
     static constexpr int STAGES = 9;
     static const char *const STAGE_NAMES[STAGES];

@@ -2234,11 +2234,12 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
     const void *src = nullptr;
     size_t size = 0;
     if (k == "rebuild_stages") {
-        // option "timeline" and RT_BUILD_LBVH: the last BLAS build's items, interior nodes, node pairs written, then
-        // the duration in ms of each LbvhBuilder stage (LbvhBuilder::STAGE_NAMES), as float64 (waits for the build)
+        // option "timeline" and RT_BUILD_LBVH: the last BLAS build's items, interior nodes, node pairs written, items
+        // in large trees (> 2048 items), large trees, then the duration in ms of each LbvhBuilder stage
+        // (LbvhBuilder::STAGE_NAMES), as float64 (waits for the build)
         if (!s->blas_builder) return fail(RT_ERR_STATE, "no GPU BLAS build (RT_BUILD_LBVH)");
         constexpr int NS = LbvhBuilder::STAGES;
-        *bytes = (3 + NS) * sizeof(double);
+        *bytes = (5 + NS) * sizeof(double);
         if (!capacity) return RT_OK;
         if (capacity < *bytes) return fail(RT_ERR_INVALID_ARGUMENT, "buffer too small");
         HIP_TRY(hipSetDevice(s->device));
@@ -2247,11 +2248,13 @@ rt_status rt_scene_debug_read(rt_scene *s, const char *name, void *dst, size_t c
         if (e != hipSuccess) return fail(RT_ERR_STATE, "no timed BLAS build: set option \"timeline\" before the frame");
         uint32_t pairs = 0;
         HIP_TRY(hipMemcpy(&pairs, s->gpu_counts.p, sizeof pairs, hipMemcpyDeviceToHost));
-        double v[3 + NS];
+        double v[5 + NS];
         v[0] = s->blas_builder->items();
         v[1] = s->blas_builder->max_pairs();
         v[2] = pairs;
-        for (int j = 0; j < NS; j++) v[3 + j] = ms[j];
+        v[3] = s->blas_builder->large_items();
+        v[4] = s->blas_builder->large_trees();
+        for (int j = 0; j < NS; j++) v[5 + j] = ms[j];
         std::memcpy(dst, v, sizeof v);
         return RT_OK;
     }

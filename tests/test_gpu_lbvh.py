@@ -513,8 +513,9 @@ def test_cold_records_auto_same_frames(gpu_lib, rebuild):
 
 def test_rebuild_stage_timing(gpu_lib):
     """Option "timeline" times the GPU BLAS rebuild's stages (bench.py's "rebuild" roofline block): after a timed
-    rebuild rt_scene_debug_read("rebuild_stages") gives the forest's items, interior nodes and node pairs and a
-    positive duration per stage; after an untimed rebuild it refuses rather than return the older figures."""
+    rebuild rt_scene_debug_read("rebuild_stages") gives the forest's items, interior nodes, node pairs, items in
+    large trees (> 2048 items) and large trees, and a positive duration per stage; after an untimed rebuild it
+    refuses rather than return the older figures."""
     s = scenes.demo_with_particles(6)
     r = Renderer(s).set_option("rebuild", 1).build_acceleration_structure(0, mode="lbvh").configure_camera(
         64, 48, ray_trace_depth=2)
@@ -523,8 +524,9 @@ def test_rebuild_stage_timing(gpu_lib):
     r.update(1)
     v = r.debug_read("rebuild_stages").view(np.float64)
     n_items = sum(1024 for _ in range(6))
-    assert len(v) == 3 + 9 and v[0] >= n_items and 0.9 * v[0] < v[1] <= v[0] and 0 < v[2] <= v[1]
-    assert (v[3:] > 0).all(), v
+    assert len(v) == 5 + 9 and v[0] >= n_items and 0.9 * v[0] < v[1] <= v[0] and 0 < v[2] <= v[1]
+    assert 0 <= v[3] <= v[0] and v[4] <= max(1.0, v[3] / 2049)
+    assert (v[5:] > 0).all(), v
     r.set_option("timeline", 0)
     r.update(2)
     with pytest.raises(abi.RtError, match="RT_ERR_STATE"):
