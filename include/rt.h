@@ -351,7 +351,7 @@ rt_status rt_box_test(int device, const float *boxes_host, const float *rays_hos
  *                 rt_scene_build (same pixels either way)
  *   "blas_double": per-frame rebuilds: 1 = write a spare BLAS set and swap it in, so a frame's rebuild overlaps the
  *                 previous frames' traces (default 1; 0 = one set, a rebuild waits for every lane's trace)
- *   "blas_sets" : with "blas_double": BLAS sets cycled (2..3, default 3): frame k+1's rebuild waits only for the trace
+ *   "blas_sets" : with "blas_double": BLAS sets cycled (2..8, default 3): frame k+1's rebuild waits only for the trace
  *                 of frame k + 1 - sets
  *   "tlas_small": 1 (default) = a GPU TLAS of at most 512 records is built by one workgroup in one launch; 0 = the
  *                 multi-kernel builder (results identical up to the tree's shape)

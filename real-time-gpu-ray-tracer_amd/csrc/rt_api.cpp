@@ -401,7 +401,9 @@ struct rt_scene {
             pairs.release(); quads.release(); roots.release(); tri_hot.release(); tri_cold.release();
             sph_hot.release(); sph_cold.release(); quad_hot.release(); quad_cold.release();
         }
-    } spare[2];
+    };
+    static constexpr uint32_t MAX_BLAS_SETS = 8;
+    BlasSet spare[MAX_BLAS_SETS - 1];   // spare[0]: the set read longest ago (written next) .. spare[sets - 2]: the newest
     uint32_t blas_sets = 3;
     hipEvent_t ev_blas_lane[NLANE] = {};
     bool blas_double = true;
@@ -1052,7 +1054,8 @@ rt_status gpu_build_blas(rt_scene *s) {
         std::swap(s->sph_hot, sp.sph_hot); std::swap(s->sph_cold, sp.sph_cold);
         std::swap(s->quad_hot, sp.quad_hot); std::swap(s->quad_cold, sp.quad_cold);
         for (int q = 0; q < rt_scene::NLANE; q++) std::swap(s->ev_blas_lane[q], sp.ev_lane[q]);
-        if (s->blas_sets == 3) std::swap(s->spare[0], s->spare[1]);   // the set frame k-1 read is written next
+        // the set just retired (frame k read it) becomes the newest spare; the one read longest ago is written next
+        std::rotate(s->spare, s->spare + 1, s->spare + (s->blas_sets - 1));
         s->blas_dirty = false;
         s->blas_builds++;
         return RT_OK;
@@ -2168,7 +2171,8 @@ rt_status rt_scene_set_option(rt_scene *s, const char *key, int64_t value) {
         if (s->built) return fail(RT_ERR_STATE, "cold_records must be set before rt_scene_build");
         s->cold_records = (int)value;
     } else if (k == "blas_sets") {
-        if (value != 2 && value != 3) return fail(RT_ERR_INVALID_ARGUMENT, "blas_sets must be 2 or 3");
+        if (value < 2 || value > (int64_t)rt_scene::MAX_BLAS_SETS)
+            return fail(RT_ERR_INVALID_ARGUMENT, "blas_sets must be in 2..8");
         RT_TRY(drain(s));
         s->blas_sets = (uint32_t)value;
     } else if (k == "blas_double") {

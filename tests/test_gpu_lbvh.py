@@ -172,15 +172,17 @@ def test_update_triangles_rebuilds(gpu_lib):
     assert np.array_equal(after, fresh.render(0, want_rgb=True)[1])
 
 
-@pytest.mark.parametrize("group", [1, 0])
-def test_update_triangles_pipelined_frames(gpu_lib, group):
+@pytest.mark.parametrize("group,L,sets", [(1, 3, 3), (0, 3, 3), (1, 6, 5), (1, 8, 8)])
+def test_update_triangles_pipelined_frames(gpu_lib, group, L, sets):
     """Deforming geometry without a device drain: each frame moves the particles' triangles and is launched on
-    one of three overlapped lanes without waiting; every frame equals the same sequence rendered synchronously
-    (the staged triangle copy is ordered behind the BLAS builds that read the array, never behind traces)."""
+    one of L overlapped lanes without waiting; every frame equals the same sequence rendered synchronously
+    (the staged triangle copy is ordered behind the BLAS builds that read the array, never behind traces; with
+    "blas_sets" spare sets in rotation a rebuild writes only a set no trace in flight still reads)."""
     import torch
     s = scenes.demo_with_particles(8)
     n_p = 8 * 1024
-    W, H, F, L = 256, 144, 9, 3
+    W, H = 256, 144
+    F = max(9, 2 * L + 3)
 
     def deform(f):
         t = s.triangles[:n_p].copy()
@@ -195,8 +197,8 @@ def test_update_triangles_pipelined_frames(gpu_lib, group):
         ref.append(ref_r.render(f)[0])
     ref_r.cleanup()
     assert not np.array_equal(ref[0], ref[F - 1])
-    r = Renderer(s).set_option("group", group).build_acceleration_structure(0, mode="lbvh").configure_camera(
-        W, H, ray_trace_depth=2)
+    r = Renderer(s).set_option("group", group).set_option("blas_sets", sets).build_acceleration_structure(
+        0, mode="lbvh").configure_camera(W, H, ray_trace_depth=2)
     r.set_option("overlap", L)
     lanes = [torch.cuda.Stream() for _ in range(L)]
     bufs = [torch.zeros(W * H * 4, dtype=torch.uint8, device="cuda") for _ in range(F)]
