@@ -549,18 +549,12 @@ static_assert(CHUNK % CHUNK_THREADS == 0, "whole items per thread");
 // arrays produce, bit for bit, without the searches, the parent arrays or a second pass over the chunk (tests/test_gpu_lbvh.py
 // compares every node with the restatement).  Arrival bits per split: 1 / 2 = the left / right child arrived, 4 / 8 =
 // that child is a leaf.
-struct SegKeys {
+struct SegKeys {                // the top pass's view of one tree's sorted codes (the chunk pass stages δ in LDS)
     const uint32_t *keys;       // sorted codes (global)
-    const uint32_t *skey;       // staged codes at positions w0 .. w0 + wn - 1 (LDS), or null
-    int64_t w0;
-    int wn;
     uint32_t base;              // the segment's first sorted position
     int m;                      // the segment's items
 };
-__device__ __forceinline__ uint32_t seg_key(const SegKeys &K, int a) {
-    const int64_t pos = (int64_t)K.base + a, o = pos - K.w0;
-    return (o >= 0 && o < K.wn) ? K.skey[o] : K.keys[pos];
-}
+__device__ __forceinline__ uint32_t seg_key(const SegKeys &K, int a) { return K.keys[(size_t)K.base + a]; }
 __device__ __forceinline__ int seg_delta(const SegKeys &K, int a, int b) {      // 0 <= a < m
     if (b < 0 || b >= K.m) return -1;
     const uint32_t ka = seg_key(K, a), kb = seg_key(K, b);
@@ -580,7 +574,7 @@ __global__ __launch_bounds__(CHUNK_THREADS) void hierarchy_chunk_kernel(const Lb
                                                                         const float *item_box, uint32_t n, uint32_t *child,
                                                                         uint32_t *range, float *nbox, uint32_t *height,
                                                                         uint32_t *kept, uint32_t *frontier) {
-    __shared__ uint32_t skey[CHUNK + 2];        // codes at positions lo - 1 .. lo + CHUNK
+    __shared__ int sdel[CHUNK + 1];             // δ(q, q + 1) for positions q = lo - 1 .. lo + CHUNK - 1 (-1 across trees)
     __shared__ float sleaf[CHUNK * 6];          // the chunk's item boxes, in sorted order
     __shared__ float sbox[CHUNK * 6];           // node boxes, at the node's Karras index
     __shared__ uint32_t sheight[CHUNK];
@@ -592,9 +586,19 @@ __global__ __launch_bounds__(CHUNK_THREADS) void hierarchy_chunk_kernel(const Lb
     __shared__ uint32_t sfront_n, sfront_at;
     const uint32_t lo = blockIdx.x * CHUNK;
     if (threadIdx.x == 0) sfront_n = 0;
-    for (uint32_t k = threadIdx.x; k < CHUNK + 2; k += CHUNK_THREADS) {
+    // the parent rule compares only adjacent δ's: each is computed once here (seg_delta's value) instead of from four
+    // staged codes per climb step
+    for (uint32_t k = threadIdx.x; k < CHUNK + 1; k += CHUNK_THREADS) {
         const int64_t q = (int64_t)lo - 1 + k;
-        skey[k] = (q >= 0 && q < (int64_t)n) ? keys[q] : 0u;
+        int d = -1;
+        if (q >= 0 && q + 1 < (int64_t)n) {
+            const uint32_t s0 = seg_of[q];
+            if (s0 == seg_of[q + 1]) {
+                const uint32_t ka = keys[q], kb = keys[q + 1], a = (uint32_t)q - segs[s0].item_base;
+                d = ka != kb ? __clz(ka ^ kb) : 32 + __clz(a ^ (a + 1u));
+            }
+        }
+        sdel[k] = d;
     }
     bool big[CHUNK_PER];
     LbvhSeg S[CHUNK_PER];
@@ -617,9 +621,13 @@ __global__ __launch_bounds__(CHUNK_THREADS) void hierarchy_chunk_kernel(const Lb
         if (!big[j]) continue;
         const uint32_t p = lo + threadIdx.x + j * CHUNK_THREADS;
         const LbvhSeg &Sj = S[j];
-        const SegKeys K = {keys, skey, (int64_t)lo - 1, (int)CHUNK + 2, Sj.item_base, (int)Sj.count};
+        const int m = (int)Sj.count;
+        const int off = (int)((int64_t)Sj.item_base - (int64_t)lo + 1);   // sdel[off + i] = δ(i, i + 1), segment-local i
+        const auto left_child_local = [&](int l, int r) {
+            return l == 0 || (r != m - 1 && sdel[off + r] > sdel[off + l - 1]);
+        };
         int l = (int)(p - Sj.item_base), r = l;
-        bool leaf = true, left = left_child(K, l, r);
+        bool leaf = true, left = left_child_local(l, r);
         for (;;) {
             const int gam = left ? r : l - 1;
             const uint32_t P = Sj.item_base + (uint32_t)gam;       // the split: children at positions P, P + 1
@@ -650,8 +658,8 @@ __global__ __launch_bounds__(CHUNK_THREADS) void hierarchy_chunk_kernel(const Lb
             merge_into(b, t);                                     // union_children's order
             const uint32_t h0 = (a & 4u) ? 0u : sheight[sl], h1 = (a & 8u) ? 0u : sheight[sr];
             const uint32_t h = h0 > h1 ? h0 : h1;
-            const bool root = lL == 0 && rR == (int)Sj.count - 1;
-            const bool nleft = !root && left_child(K, lL, rR);
+            const bool root = lL == 0 && rR == m - 1;
+            const bool nleft = !root && left_child_local(lL, rR);
             const uint32_t slot = Sj.item_base + (uint32_t)(root ? 0 : (nleft ? rR : lL)) - lo;
             const uint32_t size = (uint32_t)(rR - lL) + 1u;
 #pragma unroll
@@ -723,7 +731,7 @@ __global__ void hierarchy_top_kernel(const LbvhSeg *segs, const uint32_t *seg_of
     for (uint32_t i = blockIdx.x * BLOCK + threadIdx.x; i < count; i += gridDim.x * BLOCK) {
         uint32_t P = frontier[1 + 2 * i], bits = frontier[2 + 2 * i];
         const LbvhSeg S = segs[seg_of[P]];
-        const SegKeys K = {keys, nullptr, 0, 0, S.item_base, (int)S.count};
+        const SegKeys K = {keys, S.item_base, (int)S.count};
         for (;;) {
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // this lane's sc1 stores have landed
             const uint32_t old = atomicOr(&flag[P], bits);
@@ -792,7 +800,8 @@ __global__ void hierarchy_top_kernel(const LbvhSeg *segs, const uint32_t *seg_of
         }
     }
     // the large trees' leaf-ordered primitive records (karras_kernel's fused gather for the small ones): bandwidth
-    // work that fills the issue slots the climbs above leave idle while they wait on their hand-offs
+    // work that fills the issue slots the climbs above leave idle while they wait on their hand-offs (on a side stream
+    // beside the chunk and top kernels instead: rebuild 1.97 -> 2.06 ms, C5 frame 8.3 ms; profiles/r06/hierarchy/)
     if (gather)
         for (uint32_t p = blockIdx.x * BLOCK + threadIdx.x; p < n; p += gridDim.x * BLOCK) {
             const LbvhSeg S = segs[seg_of[p]];
