@@ -404,7 +404,11 @@ rt_status rt_scene_set_option(rt_scene *scene, const char *key, int64_t value);
  *   "blas_pairs", "blas_quads", "blas_roots": RT_BUILD_LBVH: the GPU-built forest as NodePair / NodeQuad /
  *               TreeRoot records (csrc/layout.hpp; quad q is the 4-wide node rooted at pair q);
  *   "leaf_prims": 1 u32 per leaf-ordered triangle slot: the caller's triangle index stored there (each
- *               BLAS owns the contiguous slots of its primitives, in leaf order).
+ *               BLAS owns the contiguous slots of its primitives, in leaf order);
+ *   "rebuild_stages": RT_BUILD_LBVH with option "timeline" set before the frame: float64 values — the last BLAS
+ *               build's items, interior nodes, node pairs written, items in trees of > 2048 items, such trees, then
+ *               the ms of each builder stage (prep, bounds, morton, sort, hierarchy_small, hierarchy_large, scan,
+ *               emit_roots, collapse); RT_ERR_STATE when the last build ran untimed.
  * Copies min(capacity, size) bytes to dst and stores the buffer's full size in *bytes. */
 rt_status rt_scene_debug_read(rt_scene *scene, const char *name, void *dst, size_t capacity, size_t *bytes);
 
