@@ -273,6 +273,11 @@ using BigSortConfig = rocprim::radix_sort_config<
     rocprim::default_config, rocprim::default_config,
     rocprim::radix_sort_onesweep_config<rocprim::kernel_config<1024, 16>, rocprim::kernel_config<1024, 16>, LBVH_SORT_BITS,
                                         rocprim::block_radix_rank_algorithm::match>>;
+// the pair-index scan over every interior node's kept flag: 256 x 32 items per block, 0.051 -> 0.036 ms over 10 M flags
+// against rocPRIM's default (scripts/scan_bench.hip, profiles/r06/sort/)
+using PairScanConfig = rocprim::scan_config<256, 32, rocprim::block_load_method::block_load_transpose,
+                                            rocprim::block_store_method::block_store_transpose,
+                                            rocprim::block_scan_algorithm::using_warp_scan>;
 __global__ __launch_bounds__(BLOCK) void local_sort_kernel(const LbvhSeg *segs, const uint32_t *keys_in, uint32_t *keys_out,
                                                            uint32_t *vals_out) {
     __shared__ unsigned long long sk[LOCAL_SORT_MAX];
@@ -1260,7 +1265,7 @@ hipError_t LbvhBuilder::init(const std::vector<LbvhSeg> &segs, hipStream_t strea
     LB_TRY(dalloc(nbox_, 6 * NI)); LB_TRY(dalloc(kept_, NI)); LB_TRY(dalloc(pidx_, NI));
     size_t sort_bytes = 0, scan_bytes = 0;
     if (big_max) LB_TRY(rocprim::radix_sort_pairs<BigSortConfig>(nullptr, sort_bytes, k0_, k1_, v0_, v1_, big_max, 0, 32, stream));
-    LB_TRY(rocprim::exclusive_scan(nullptr, scan_bytes, kept_, pidx_, 0u, NI, rocprim::plus<uint32_t>(), stream));
+    LB_TRY(rocprim::exclusive_scan<PairScanConfig>(nullptr, scan_bytes, kept_, pidx_, 0u, NI, rocprim::plus<uint32_t>(), stream));
     tmp_bytes_ = sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
     LB_TRY(hipMalloc(&tmp_, tmp_bytes_ ? tmp_bytes_ : 1));
     // kept/pidx of nodes that no thread visits (none in a valid forest) start defined
@@ -1423,7 +1428,7 @@ hipError_t LbvhBuilder::build(NodePair *pairs, TreeRoot *roots, uint32_t *pair_c
     last_count_ = pair_count;
     if (NI > 0) {
         bytes = tmp_bytes_;
-        LB_TRY(rocprim::exclusive_scan(tmp_, bytes, kept_, pidx_, 0u, NI, rocprim::plus<uint32_t>(), stream));
+        LB_TRY(rocprim::exclusive_scan<PairScanConfig>(tmp_, bytes, kept_, pidx_, 0u, NI, rocprim::plus<uint32_t>(), stream));
         if (tm) LB_TRY(mark(7, stream));
         hipLaunchKernelGGL(emit_kernel, dim3(blocks_for(NI)), dim3(BLOCK), 0, stream, segs_, seg_of_, v1_, box_, NI, child_,
                            range_, nbox_, kept_, pidx_, pairs, pair_count);
